@@ -1,0 +1,171 @@
+/*
+ * tde.h -- C ABI of the MI355X-native hot path of wrlife/tf_depth_estimation.
+ *
+ * The reference has no FFI: its hot path is a TensorFlow-1 graph built by Python functions
+ * (SURVEY.md §8b).  This ABI exports the kernels that replace the TF ops those functions emit;
+ * each entry point names the reference call site it stands in for.  The PyTorch-ROCm host layer
+ * (tf_depth_estimation_amd/) binds it with ctypes and exposes the reference's Python signatures
+ * (`disp_net`, `depth_net`, `projective_inverse_warp`, ...).
+ *
+ * Conventions
+ *   - All tensors are fp32, NHWC, in caller-owned device memory (no allocation inside).
+ *   - An activation operand is a *channel view*: element (n,h,w,c) of a view with pixel stride
+ *     `cstride` and channel offset `coff` lives at ptr[((n*H+h)*W+w)*cstride + coff + c].  This is
+ *     how skip-concats (tf.concat(..., axis=3), nets_optflow_depth.py:106-141) are fused: producers
+ *     write straight into their channel slice of the consumer's input buffer.
+ *   - Weights keep the TF checkpoint layout: conv [KH][KW][Cin][Cout],
+ *     conv2d_transpose [KH][KW][Cout][Cin].
+ *   - `stream` is a hipStream_t passed as void*.  Every call is stream-ordered, never synchronises
+ *     the host and is safe to capture in a hipGraph.  Re-entrant across streams.
+ *   - Return value: TDE_OK (0) or a negative tde_status.
+ *   - `ws` / `ws_bytes`: caller-provided device workspace; size it with the *_workspace_size query.
+ */
+#ifndef TDE_H_
+#define TDE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TDE_ABI_VERSION 1
+
+typedef enum {
+  TDE_OK = 0,
+  TDE_ERR_ARG = -1,        /* bad pointer / alignment / shape */
+  TDE_ERR_WORKSPACE = -2,  /* ws_bytes smaller than the query */
+  TDE_ERR_HIP = -3,        /* kernel launch failed */
+  TDE_ERR_UNSUPPORTED = -4
+} tde_status;
+
+/* Geometry of one conv layer, always expressed as a FORWARD conv x[N,H,W,C] -> y[N,OH,OW,K]
+ * with TF 'SAME' padding (pad_top/pad_left are TF's pad_before).  For conv2d_transpose layers the
+ * descriptor is that of the *virtual* forward conv whose Conv2DBackpropInput the deconv is:
+ * x = deconv output [N,2h,2w,Cout], y = deconv input [N,h,w,Cin], K = Cin, C = Cout. */
+typedef struct {
+  int N, H, W, C;          /* x; C may include zero pad channels (C % 4 == 0) */
+  int OH, OW, K;           /* y */
+  int KH, KW, stride, pad_top, pad_left;
+  int w_cin;               /* input channels of the weight tensor (<= C); rows ci >= w_cin are zero */
+  int x_cstride, x_coff;   /* channel view of x (and of dx) */
+  int y_cstride, y_coff;   /* channel view of y (and of dy) */
+} tde_conv_desc_t;
+
+int tde_abi_version(void);
+const char* tde_status_string(int status);
+
+/* ---------------------------------------------------------------- MFMA implicit-GEMM convs
+ * slim.conv2d (no bias; the BN that follows owns the shift), nets_optflow_depth.py:88-101,107-142
+ * -> TF Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter.
+ * Requires C, K, cstrides and coffs to be multiples of 4 (16-byte vectors). */
+size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
+int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y,
+                   int accumulate, void* ws, size_t ws_bytes, void* stream);
+int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx,
+                        int accumulate, void* ws, size_t ws_bytes, void* stream);
+int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw,
+                          int accumulate, void* ws, size_t ws_bytes, void* stream);
+
+/* slim.conv2d_transpose (stride 2, SAME), nets_optflow_depth.py:103,109,114,119,126,133,140.
+ * `d` is the virtual forward conv (see above); x = deconv input, y = deconv output.
+ *   fwd       : y_big  = Conv2DBackpropInput(x_small)     (weights [KH][KW][Cout][Cin])
+ *   bwd_data  : dx_small = Conv2D(dy_big)
+ *   bwd_filter: dW = Conv2DBackpropFilter(dy_big, x_small) */
+size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op);
+int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
+                     int accumulate, void* ws, size_t ws_bytes, void* stream);
+int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w,
+                          float* dx_small, int accumulate, void* ws, size_t ws_bytes, void* stream);
+int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small,
+                            float* dw, int accumulate, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- few-channel heads
+ * slim.conv2d(..., normalizer_fn=None, activation_fn=sigmoid|None) with bias: disp heads
+ * (nets_optflow_depth.py:122-144: DISP_SCALING*sigmoid(.) [+MIN_DISP]), flow heads (nets_depth.py:169-191),
+ * mask heads (nets_optflow_depth.py:193-198) and pose/pred 1x1 (:181).  K <= 8.
+ * act: 0 linear (y = z), 1 y = scale*sigmoid(z) + offset.  Backward takes y (not z). */
+size_t tde_head_workspace_size(const tde_conv_desc_t* d);
+int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias,
+                 float* y, int act, float scale, float offset, void* stream);
+int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* y,
+                 const float* dy, float* dx, int accumulate_dx, float* dw, float* dbias,
+                 int accumulate_dw, int act, float scale, float offset, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* ---------------------------------------------------------------- batch norm (+ReLU)
+ * slim.batch_norm(center=True, scale=False, epsilon=1e-3) -> TF FusedBatchNorm(+Grad)
+ * (arg_scope nets_optflow_depth.py:82-87).  z is the dense conv output [M][C] (M = N*H*W);
+ * y is a channel view (y_cstride, y_coff).  Training normalises with the biased batch variance and
+ * updates moving_mean/moving_var in place (v -= (v - batch) * (1 - decay)); `bessel` selects the
+ * FusedBatchNorm n/(n-1) correction of the variance fed to the moving average. */
+size_t tde_bn_workspace_size(int M, int C);
+int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps, float decay,
+                     int bessel, float* moving_mean, float* moving_var, float* save_mean,
+                     float* save_invstd, float* y, int y_cstride, int y_coff, int relu,
+                     void* ws, size_t ws_bytes, void* stream);
+int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps,
+                     const float* moving_mean, const float* moving_var, float* y, int y_cstride,
+                     int y_coff, int relu, void* stream);
+/* dz = d(BN+ReLU)/dz given dy (view); dbeta = sum(dy * relu'); accumulate_dbeta adds to dbeta. */
+int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd,
+               const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,
+               float* dbeta, int accumulate_dbeta, int relu, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- legacy resizes
+ * resize_like -> tf.image.resize_nearest_neighbor (nets_optflow_depth.py:11-16),
+ * tf.image.resize_bilinear of the disparity (nets_optflow_depth.py:124,131,138),
+ * tf.image.resize_area pyramids (train_depth_then_cam_lr.py:227-232).  align_corners=False. */
+int tde_resize_nearest_fwd(int N, int H, int W, int C, const float* x, int x_cstride, int x_coff,
+                           int OH, int OW, float* y, int y_cstride, int y_coff, void* stream);
+int tde_resize_nearest_bwd(int N, int H, int W, int C, float* dx, int dx_cstride, int dx_coff,
+                           int accumulate, int OH, int OW, const float* dy, int dy_cstride,
+                           int dy_coff, void* stream);
+int tde_resize_bilinear_fwd(int N, int H, int W, int C, const float* x, int x_cstride, int x_coff,
+                            int OH, int OW, float* y, int y_cstride, int y_coff, void* stream);
+int tde_resize_bilinear_bwd(int N, int H, int W, int C, float* dx, int dx_cstride, int dx_coff,
+                            int accumulate, int OH, int OW, const float* dy, int dy_cstride,
+                            int dy_coff, void* stream);
+int tde_resize_area_fwd(int N, int H, int W, int C, const float* x, int OH, int OW, float* y,
+                        void* stream);
+
+/* ---------------------------------------------------------------- loss head
+ * Fused forward+backward of the scalar loss terms: each call ADDS weight*term to loss[0] (a
+ * device fp64 accumulator) and ADDS d(weight*term)/d(pred) into grad (same view layout as pred).
+ *
+ * compute_smooth_loss (train_depth_then_cam_lr.py:59-68) of pred (recip=0) or of 1/pred (recip=1):
+ * mean|dx2| + mean|dxdy| + mean|dydx| + mean|dy2| over one channel c of a view. */
+int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int coff, int recip,
+                     float weight, double* loss, float* grad, int g_cstride, int g_coff,
+                     void* stream);
+/* mean|nf(label - pred)| (train_depth_only.py:183-184; replace_nonfinite when nonfinite=1,
+ * train_depth_then_cam_lr.py:241-243).  label is dense [N,H,W,1]; pred is a 1-channel view. */
+int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, const float* label,
+                int nonfinite, float weight, double* loss, float* grad, int g_cstride, int g_coff,
+                void* stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * tf.train.AdamOptimizer (train_depth_then_cam_lr.py:413-417), TF epsilon-hat form, one launch over
+ * a flat parameter buffer.  `step` is a device counter (incremented on device by tde_adam_step_begin)
+ * so a captured graph replays correctly.  lr_t = lr*sqrt(1-b2^t)/(1-b1^t). */
+int tde_adam_step_begin(float* step, void* stream);
+int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* v,
+                    const float* step, float lr, float beta1, float beta2, float eps, void* stream);
+
+/* ---------------------------------------------------------------- utilities */
+int tde_fill(size_t n, float* x, float value, void* stream);
+int tde_zero_bytes(size_t bytes, void* p, void* stream);
+/* pose_avg = tf.reduce_mean(pose_pred, [1, 2]) (nets_optflow_depth.py:183): x [N,HW,C] (pixel stride
+ * x_cstride) -> y [N,C], and its gradient (dx (+)= dy/HW). */
+int tde_spatial_mean_fwd(int N, int HW, int C, const float* x, int x_cstride, float* y, void* stream);
+int tde_spatial_mean_bwd(int N, int HW, int C, float* dx, int dx_cstride, int accumulate, const float* dy,
+                         void* stream);
+/* Copy a dense [M][C] tensor into a channel view (or back when `to_view`=0). */
+int tde_copy_view(int M, int C, const float* src, int s_cstride, int s_coff, float* dst,
+                  int d_cstride, int d_coff, int accumulate, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDE_H_ */

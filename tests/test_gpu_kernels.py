@@ -1,0 +1,319 @@
+"""GPU parity of every libtde.so kernel family against the float64 CPU oracle (called through the C ABI).
+
+Tolerance: the HIP path computes in fp32 (exact-f32 MFMA), the oracle in fp64; every check is
+max|gpu - ref| <= TOL * max|ref| (+ tiny absolute floor) with TOL = 1e-5 for single ops."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import geometry as OG
+from oracle import losses as OL
+from oracle import tf_ops as T
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def close(gpu, ref, tol=TOL, what=""):
+    g = gpu.detach().double().cpu()
+    r = ref.detach().double().cpu()
+    assert g.shape == r.shape, (what, g.shape, r.shape)
+    scale = max(r.abs().max().item(), 1e-6)
+    err = (g - r).abs().max().item()
+    assert err <= tol * scale + 1e-7, f"{what}: max err {err:.3e} vs scale {scale:.3e} (rel {err / scale:.3e})"
+
+
+def rnd(*shape, seed=0, lo=-1.0, hi=1.0):
+    g = np.random.default_rng(seed)
+    return torch.tensor(g.uniform(lo, hi, size=shape), dtype=torch.float64)
+
+
+def dev(t):
+    return t.float().cuda().contiguous()
+
+
+@pytest.fixture(scope="module")
+def L():
+    from tf_depth_estimation_amd import _lib
+    return _lib
+
+
+def conv_desc(L, **kw):
+    d = L.ConvDesc()
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+def ws_for(L, d, deconv=False):
+    lib = L.load()
+    q = lib.tde_deconv2d_workspace_size if deconv else lib.tde_conv2d_workspace_size
+    n = max(q(ctypes.byref(d), o) for o in range(3))
+    return torch.empty(max(n // 4 + 16, 16), device="cuda")
+
+
+CONV_CASES = [
+    # N, H, W, cin_real, C(view), K, k, s, x_cs, x_coff
+    (2, 10, 12, 6, 8, 16, 3, 1, 16, 4),
+    (2, 24, 32, 3, 4, 32, 7, 2, 4, 0),
+    (2, 13, 17, 32, 32, 64, 5, 2, 32, 0),
+    (2, 6, 8, 64, 64, 128, 3, 2, 64, 0),
+    (2, 2, 2, 512, 512, 512, 3, 1, 1024, 512),
+    (1, 9, 11, 129, 132, 64, 3, 1, 132, 0),
+    (3, 3, 4, 512, 512, 256, 3, 2, 512, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_fwd_bwd(L, case):
+    N, H, W, cin, C, K, k, s, xcs, xco = case
+    lib = L.load()
+    st = L.stream_ptr()
+    OH, pt, _ = T.same_pad(H, k, s)
+    OW, pl, _ = T.same_pad(W, k, s)
+    xfull = rnd(N, H, W, xcs, seed=1)
+    xfull[..., xco + cin:xco + C] = 0.0
+    w = rnd(k, k, cin, K, seed=2) * 0.2
+    d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
+                  w_cin=cin, x_cstride=xcs, x_coff=xco, y_cstride=K, y_coff=0)
+    ws = ws_for(L, d)
+    gx, gw = dev(xfull), dev(w)
+    gy = torch.empty(N, OH, OW, K, device="cuda")
+    L.check(lib.tde_conv2d_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(gy), 0, L.ptr(ws), ws.numel() * 4, st))
+    xr = xfull[..., xco:xco + cin].clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = T.conv2d_same(xr, wr, s)
+    close(gy, yr, what="conv fwd")
+    dy = rnd(N, OH, OW, K, seed=3)
+    yr.backward(dy)
+    # bwd data with accumulate into a pre-filled view
+    base = rnd(N, H, W, xcs, seed=4)
+    gdx = dev(base)
+    L.check(lib.tde_conv2d_bwd_data(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(gw), L.ptr(gdx), 1, L.ptr(ws),
+                                    ws.numel() * 4, st))
+    exp = base.clone()
+    exp[..., xco:xco + cin] += xr.grad
+    close(gdx[..., xco:xco + cin], exp[..., xco:xco + cin], what="conv dgrad")
+    close(gdx[..., :xco], base[..., :xco], what="dgrad untouched lo")
+    close(gdx[..., xco + C:], base[..., xco + C:], what="dgrad untouched hi")
+    gdw = torch.empty_like(gw)
+    L.check(lib.tde_conv2d_bwd_filter(ctypes.byref(d), L.ptr(gx), L.ptr(dev(dy)), L.ptr(gdw), 0, L.ptr(ws),
+                                      ws.numel() * 4, st))
+    close(gdw, wr.grad, what="conv wgrad")
+
+
+DECONV_CASES = [
+    # N, h, w, Cin(deconv input), Cout, k
+    (2, 6, 8, 32, 16, 3),
+    (2, 3, 4, 64, 32, 5),
+    (2, 4, 5, 32, 16, 7),
+    (2, 2, 2, 512, 512, 3),
+    (1, 12, 16, 256, 128, 3),
+]
+
+
+@pytest.mark.parametrize("case", DECONV_CASES)
+def test_deconv2d_fwd_bwd(L, case):
+    N, h, w_, cin, cout, k = case
+    lib = L.load()
+    st = L.stream_ptr()
+    H, W = 2 * h, 2 * w_
+    _, pt, _ = T.same_pad(H, k, 2)
+    _, pl, _ = T.same_pad(W, k, 2)
+    x = rnd(N, h, w_, cin, seed=5)
+    wt = rnd(k, k, cout, cin, seed=6) * 0.2
+    d = conv_desc(L, N=N, H=H, W=W, C=cout, OH=h, OW=w_, K=cin, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
+                  w_cin=cout, x_cstride=cout, x_coff=0, y_cstride=cin, y_coff=0)
+    ws = ws_for(L, d, deconv=True)
+    gy = torch.empty(N, H, W, cout, device="cuda")
+    L.check(lib.tde_deconv2d_fwd(ctypes.byref(d), L.ptr(dev(x)), L.ptr(dev(wt)), L.ptr(gy), 0, L.ptr(ws),
+                                 ws.numel() * 4, st))
+    xr, wr = x.clone().requires_grad_(True), wt.clone().requires_grad_(True)
+    yr = T.conv2d_transpose_same(xr, wr, 2)
+    close(gy, yr, what="deconv fwd")
+    dy = rnd(N, H, W, cout, seed=7)
+    yr.backward(dy)
+    gdx = torch.empty(N, h, w_, cin, device="cuda")
+    L.check(lib.tde_deconv2d_bwd_data(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(dev(wt)), L.ptr(gdx), 0, L.ptr(ws),
+                                      ws.numel() * 4, st))
+    close(gdx, xr.grad, what="deconv dgrad")
+    gdw = torch.empty(k, k, cout, cin, device="cuda")
+    L.check(lib.tde_deconv2d_bwd_filter(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(dev(x)), L.ptr(gdw), 0, L.ptr(ws),
+                                        ws.numel() * 4, st))
+    close(gdw, wr.grad, what="deconv wgrad")
+
+
+HEAD_CASES = [
+    # N, H, W, C, K, k, act, scale, offset, x_cs, x_co
+    (2, 12, 16, 16, 1, 3, 1, 4.0, 0.0, 16, 0),
+    (2, 12, 16, 32, 2, 3, 0, 1.0, 0.0, 36, 4),
+    (2, 2, 2, 256, 6, 1, 0, 1.0, 0.0, 256, 0),
+    (1, 16, 20, 16, 2, 7, 0, 1.0, 0.0, 16, 0),
+    (2, 6, 8, 128, 1, 3, 1, 10.0, 0.001, 128, 0),
+]
+
+
+@pytest.mark.parametrize("case", HEAD_CASES)
+def test_head_fwd_bwd(L, case):
+    N, H, W, C, K, k, act, scale, offset, xcs, xco = case
+    lib = L.load()
+    st = L.stream_ptr()
+    _, p, _ = T.same_pad(H, k, 1)
+    xfull = rnd(N, H, W, xcs, seed=8)
+    w = rnd(k, k, C, K, seed=9) * 0.3
+    b = rnd(K, seed=10) * 0.1
+    d = conv_desc(L, N=N, H=H, W=W, C=C, OH=H, OW=W, K=K, KH=k, KW=k, stride=1, pad_top=p, pad_left=p, w_cin=C,
+                  x_cstride=xcs, x_coff=xco, y_cstride=K, y_coff=0)
+    gx, gw, gb = dev(xfull), dev(w), dev(b)
+    gy = torch.empty(N, H, W, K, device="cuda")
+    L.check(lib.tde_head_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(gb), L.ptr(gy), act, scale, offset, st))
+    xr, wr, br = (xfull[..., xco:xco + C].clone().requires_grad_(True), w.clone().requires_grad_(True),
+                  b.clone().requires_grad_(True))
+    z = T.conv2d_same(xr, wr, 1) + br
+    yr = scale * torch.sigmoid(z) + offset if act else z
+    close(gy, yr, what="head fwd")
+    dy = rnd(N, H, W, K, seed=11)
+    yr.backward(dy)
+    gdx = torch.zeros(N, H, W, xcs, device="cuda")
+    gdw, gdb = torch.empty_like(gw), torch.empty_like(gb)
+    ws = torch.empty(lib.tde_head_workspace_size(ctypes.byref(d)) // 4 + 16, device="cuda")
+    L.check(lib.tde_head_bwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(gy), L.ptr(dev(dy)), L.ptr(gdx), 0,
+                             L.ptr(gdw), L.ptr(gdb), 0, act, scale, offset, L.ptr(ws), ws.numel() * 4, st))
+    close(gdx[..., xco:xco + C], xr.grad, tol=3e-5, what="head dgrad")
+    close(gdw, wr.grad, tol=3e-5, what="head wgrad")
+    close(gdb, br.grad, tol=3e-5, what="head dbias")
+
+
+@pytest.mark.parametrize("M,C,ycs,yco", [(8 * 96 * 128, 32, 68, 32), (32, 512, 1024, 512), (8 * 12 * 16, 256, 256, 0)])
+def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
+    lib = L.load()
+    st = L.stream_ptr()
+    z = rnd(M, C, seed=12) * 3 + 0.5
+    beta = rnd(C, seed=13) * 0.2
+    gz, gb = dev(z), dev(beta)
+    mm = torch.zeros(C, device="cuda")
+    mv = torch.ones(C, device="cuda")
+    sm = torch.empty(2, C, device="cuda")
+    y = torch.zeros(M, ycs, device="cuda")
+    ws = torch.empty(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
+    L.check(lib.tde_bn_fwd_train(M, C, L.ptr(gz), L.ptr(gb), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
+                                 L.ptr(sm[1]), L.ptr(y), ycs, yco, 1, L.ptr(ws), ws.numel() * 4, st))
+    zr = z.clone().reshape(1, 1, M, C).requires_grad_(True)
+    stt = T.BNState(C)
+    yr = torch.relu(T.batch_norm(zr, beta, stt, True, 0.99))
+    close(y[:, yco:yco + C], yr.reshape(M, C), what="bn fwd")
+    close(mm, stt.moving_mean, what="moving mean")
+    close(mv, stt.moving_variance, what="moving var")
+    dy = rnd(M, C, seed=14)
+    yr.reshape(M, C).backward(dy)
+    gdy = torch.zeros(M, ycs, device="cuda")
+    gdy[:, yco:yco + C] = dev(dy)
+    dz = torch.empty(M, C, device="cuda")
+    dbeta = torch.zeros(C, device="cuda")
+    L.check(lib.tde_bn_bwd(M, C, L.ptr(gz), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(gb), L.ptr(gdy), ycs, yco, L.ptr(dz),
+                           L.ptr(dbeta), 1, 1, L.ptr(ws), ws.numel() * 4, st))
+    close(dz, zr.grad.reshape(M, C), tol=5e-5, what="bn dz")
+    dbr = (dy * (yr.detach().reshape(M, C) > 0)).sum(0)
+    close(dbeta, dbr, tol=5e-5, what="dbeta")
+    yi = torch.zeros(M, ycs, device="cuda")
+    L.check(lib.tde_bn_fwd_infer(M, C, L.ptr(gz), L.ptr(gb), 1e-3, L.ptr(mm), L.ptr(mv), L.ptr(yi), ycs, yco, 1, st))
+    yir = torch.relu(T.batch_norm(z.reshape(1, 1, M, C), beta, stt, False, 0.99)).reshape(M, C)
+    close(yi[:, yco:yco + C], yir, what="bn infer")
+
+
+@pytest.mark.parametrize("kind,N,H,W,C,OH,OW", [("nearest", 2, 4, 4, 8, 3, 4), ("nearest", 1, 16, 20, 4, 15, 20),
+                                                 ("bilinear", 2, 24, 32, 1, 48, 64), ("bilinear", 2, 6, 8, 2, 12, 16),
+                                                 ("bilinear", 1, 5, 7, 1, 10, 14)])
+def test_resize_fwd_bwd(L, kind, N, H, W, C, OH, OW):
+    lib = L.load()
+    st = L.stream_ptr()
+    x = rnd(N, H, W, C, seed=15)
+    xcs, xco, ycs, yco = C + 4, 2, C + 8, 5
+    gxf = torch.zeros(N, H, W, xcs, device="cuda")
+    gxf[..., xco:xco + C] = dev(x)
+    gyf = torch.zeros(N, OH, OW, ycs, device="cuda")
+    fwd = lib.tde_resize_nearest_fwd if kind == "nearest" else lib.tde_resize_bilinear_fwd
+    bwd = lib.tde_resize_nearest_bwd if kind == "nearest" else lib.tde_resize_bilinear_bwd
+    L.check(fwd(N, H, W, C, L.ptr(gxf), xcs, xco, OH, OW, L.ptr(gyf), ycs, yco, st))
+    xr = x.clone().requires_grad_(True)
+    yr = (T.resize_nearest_legacy if kind == "nearest" else T.resize_bilinear_legacy)(xr, OH, OW)
+    close(gyf[..., yco:yco + C], yr, what=kind + " fwd")
+    dy = rnd(N, OH, OW, C, seed=16)
+    yr.backward(dy)
+    gdy = torch.zeros(N, OH, OW, ycs, device="cuda")
+    gdy[..., yco:yco + C] = dev(dy)
+    gdx = torch.zeros(N, H, W, xcs, device="cuda")
+    L.check(bwd(N, H, W, C, L.ptr(gdx), xcs, xco, 0, OH, OW, L.ptr(gdy), ycs, yco, st))
+    close(gdx[..., xco:xco + C], xr.grad, what=kind + " bwd")
+
+
+def test_resize_area(L):
+    lib = L.load()
+    x = rnd(2, 16, 24, 3, seed=17)
+    x[0, 3, 5, 1] = float("nan")
+    for f in (1, 2, 4, 8):
+        y = torch.empty(2, 16 // f, 24 // f, 3, device="cuda")
+        L.check(lib.tde_resize_area_fwd(2, 16, 24, 3, L.ptr(dev(x)), 16 // f, 24 // f, L.ptr(y), L.stream_ptr()))
+        r = T.resize_area(x, 16 // f, 24 // f)
+        assert torch.equal(torch.isnan(y.cpu()), torch.isnan(r))
+        m = ~torch.isnan(r)
+        close(y.cpu()[m], r[m], what=f"area {f}")
+
+
+@pytest.mark.parametrize("recip", [0, 1])
+def test_loss_smooth2(L, recip):
+    lib = L.load()
+    N, H, W = 2, 12, 16
+    p = rnd(N, H, W, 1, seed=18, lo=0.3, hi=2.0)
+    cs, co = 3, 1
+    gp = torch.zeros(N, H, W, cs, device="cuda")
+    gp[..., co:co + 1] = dev(p)
+    loss = torch.zeros(1, dtype=torch.float64, device="cuda")
+    g = torch.zeros(N, H, W, cs, device="cuda")
+    L.check(lib.tde_loss_smooth2(N, H, W, L.ptr(gp), cs, co, recip, 0.5, L.ptr(loss), L.ptr(g), cs, co,
+                                 L.stream_ptr()))
+    pr = p.clone().requires_grad_(True)
+    lr = 0.5 * OL.compute_smooth_loss(1.0 / pr if recip else pr)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * abs(lr.item())
+    close(g[..., co:co + 1], pr.grad, what="smooth grad")
+
+
+@pytest.mark.parametrize("nonfinite", [0, 1])
+def test_loss_l1(L, nonfinite):
+    lib = L.load()
+    N, H, W = 2, 12, 16
+    p = rnd(N, H, W, 1, seed=19)
+    lab = rnd(N, H, W, 1, seed=20)
+    if nonfinite:
+        lab[0, 2, 3, 0] = float("nan")
+        lab[1, 5, 7, 0] = float("inf")
+    loss = torch.zeros(1, dtype=torch.float64, device="cuda")
+    g = torch.zeros(N, H, W, 1, device="cuda")
+    L.check(lib.tde_loss_l1(N, H, W, L.ptr(dev(p)), 1, 0, L.ptr(dev(lab)), nonfinite, 2.0, L.ptr(loss), L.ptr(g), 1, 0,
+                            L.stream_ptr()))
+    pr = p.clone().requires_grad_(True)
+    diff = lab - pr
+    lr = 2.0 * (T.replace_nonfinite(diff) if nonfinite else diff).abs().mean()
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * abs(lr.item())
+    close(g, pr.grad, what="l1 grad")
+
+
+def test_adam_matches_tf_form(L):
+    lib = L.load()
+    n = 1000
+    p0, g1, g2 = rnd(n, seed=21), rnd(n, seed=22), rnd(n, seed=23)
+    gp, gm, gv = dev(p0), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    step = torch.zeros(1, device="cuda")
+    opt = OL.AdamTF(lr=2e-4)
+    pr = {"p": p0.clone()}
+    for g in (g1, g2):
+        L.check(lib.tde_adam_step_begin(L.ptr(step), L.stream_ptr()))
+        L.check(lib.tde_adam_update(n, L.ptr(gp), L.ptr(dev(g)), L.ptr(gm), L.ptr(gv), L.ptr(step), 2e-4, 0.9, 0.999,
+                                    1e-8, L.stream_ptr()))
+        opt.step(pr, {"p": g})
+    close(gp - dev(p0), pr["p"] - p0, tol=1e-4, what="adam delta")

@@ -1,0 +1,114 @@
+"""ctypes binding of libtde.so (the C ABI declared in include/tde.h).
+
+The library is built in-tree by `make -C tf_depth_estimation_amd/csrc` (or __graft_entry__.build()).
+It is loaded *after* torch so that its DT_NEEDED libamdhip64.so.7 resolves to the HIP runtime torch
+already loaded (one runtime per process: torch's streams and allocations are valid in our calls).
+There is no fallback: if the library is missing, `load()` raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported first, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtde.so")
+ABI_VERSION = 1
+
+c_int, c_float, c_size_t, c_void_p, c_double_p = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_double))
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of tde_conv_desc_t (include/tde.h)."""
+    _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "OH", "OW", "K", "KH", "KW", "stride", "pad_top",
+                                     "pad_left", "w_cin", "x_cstride", "x_coff", "y_cstride", "y_coff")]
+
+
+P = c_void_p
+_SIGS = {
+    "tde_abi_version": (c_int, []),
+    "tde_status_string": (ctypes.c_char_p, [c_int]),
+    "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),
+    "tde_deconv2d_workspace_size": (c_size_t, [P, c_int]),
+    "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_conv2d_bwd_data": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_conv2d_bwd_filter": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_deconv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_deconv2d_bwd_data": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_deconv2d_bwd_filter": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_head_workspace_size": (c_size_t, [P]),
+    "tde_head_fwd": (c_int, [P, P, P, P, P, c_int, c_float, c_float, P]),
+    "tde_head_bwd": (c_int, [P, P, P, P, P, P, c_int, P, P, c_int, c_int, c_float, c_float, P, c_size_t, P]),
+    "tde_bn_workspace_size": (c_size_t, [c_int, c_int]),
+    "tde_bn_fwd_train": (c_int, [c_int, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, c_int, c_int, c_int,
+                                 P, c_size_t, P]),
+    "tde_bn_fwd_infer": (c_int, [c_int, c_int, P, P, c_float, P, P, P, c_int, c_int, c_int, P]),
+    "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, c_size_t, P]),
+    "tde_resize_nearest_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
+    "tde_resize_nearest_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
+    "tde_resize_bilinear_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
+    "tde_resize_bilinear_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
+    "tde_resize_area_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, P, P]),
+    "tde_loss_smooth2": (c_int, [c_int, c_int, c_int, P, c_int, c_int, c_int, c_float, P, P, c_int, c_int, P]),
+    "tde_loss_l1": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, c_int, c_float, P, P, c_int, c_int, P]),
+    "tde_adam_step_begin": (c_int, [P, P]),
+    "tde_adam_update": (c_int, [c_size_t, P, P, P, P, P, c_float, c_float, c_float, c_float, P]),
+    "tde_fill": (c_int, [c_size_t, P, c_float, P]),
+    "tde_zero_bytes": (c_int, [c_size_t, P, P]),
+    "tde_spatial_mean_fwd": (c_int, [c_int, c_int, c_int, P, c_int, P, P]),
+    "tde_spatial_mean_bwd": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, P]),
+    "tde_copy_view": (c_int, [c_int, c_int, P, c_int, c_int, P, c_int, c_int, c_int, P]),
+}
+
+_lib = None
+
+
+class TdeError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libtde.so once; raise loudly if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise TdeError(f"libtde.so not built at {path}: run `make -C tf_depth_estimation_amd/csrc` "
+                       "or __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.tde_abi_version()
+    if v != ABI_VERSION:
+        raise TdeError(f"libtde ABI {v} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(status, what=""):
+    if status != 0:
+        msg = _lib.tde_status_string(status).decode() if _lib is not None else str(status)
+        raise TdeError(f"{what}: tde status {status} ({msg})")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def call(name, *args):
+    """Call an int-returning ABI function and raise on a non-zero status."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    check(st, name)

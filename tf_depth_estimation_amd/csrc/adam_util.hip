@@ -1,0 +1,140 @@
+// TF Adam over one flat parameter buffer (tf.train.AdamOptimizer, train_depth_then_cam_lr.py:413-417;
+// TF ApplyAdam kernel: m += (g-m)(1-b1); v += (g*g-v)(1-b2); var -= lr_t*m/(sqrt(v)+eps)) plus small
+// utilities.  Adam is HBM-bound: 4 reads + 3 writes of 4 B per parameter, 16-byte vectors.
+#include "tde_common.h"
+
+namespace {
+
+__global__ void step_begin_kernel(float* step) { step[0] += 1.f; }
+
+__global__ void __launch_bounds__(256) adam_kernel(long n4, f4* __restrict__ p, const f4* __restrict__ g,
+                                                   f4* __restrict__ m, f4* __restrict__ v, const float* step,
+                                                   float lr, float b1, float b2, float eps) {
+  const double t = (double)step[0];
+  const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f4 gi = g[i];
+    f4 mi = m[i], vi = v[i], pi = p[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mi[j] += (gi[j] - mi[j]) * (1.f - b1);
+      vi[j] += (gi[j] * gi[j] - vi[j]) * (1.f - b2);
+      pi[j] -= lr_t * mi[j] / (sqrtf(vi[j]) + eps);
+    }
+    m[i] = mi; v[i] = vi; p[i] = pi;
+  }
+}
+
+__global__ void __launch_bounds__(256) fill_kernel(long n, float* x, float val) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] = val;
+}
+
+__global__ void __launch_bounds__(256) copy_view_kernel(int M, int C, const float* s, int scs, int sco, float* d,
+                                                        int dcs, int dco, int acc) {
+  const long total = (long)M * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = (int)(i - r * C);
+    const float v = s[r * scs + sco + c];
+    float* o = d + r * dcs + dco + c;
+    *o = acc ? *o + v : v;
+  }
+}
+
+// pose_avg = tf.reduce_mean(pose_pred, [1, 2]) (nets_optflow_depth.py:183): x [N,HW,C] -> y [N,C]
+__global__ void spatial_mean_fwd_kernel(int N, int HW, int C, const float* x, int xcs, float* y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += x[((long)n * HW + p) * xcs + c];
+  y[i] = s / (float)HW;
+}
+
+__global__ void spatial_mean_bwd_kernel(int N, int HW, int C, float* dx, int dxcs, int acc, const float* dy) {
+  const long total = (long)N * HW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = (int)(i - r * C);
+    const int n = (int)(r / HW);
+    const float g = dy[n * C + c] / (float)HW;
+    float* o = dx + r * dxcs + c;
+    *o = acc ? *o + g : g;
+  }
+}
+
+int ew_grid(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+int tde_abi_version(void) { return TDE_ABI_VERSION; }
+
+const char* tde_status_string(int s) {
+  switch (s) {
+    case TDE_OK: return "ok";
+    case TDE_ERR_ARG: return "invalid argument (pointer, alignment or shape)";
+    case TDE_ERR_WORKSPACE: return "workspace too small";
+    case TDE_ERR_HIP: return "HIP launch error";
+    case TDE_ERR_UNSUPPORTED: return "unsupported configuration";
+    default: return "unknown status";
+  }
+}
+
+int tde_adam_step_begin(float* step, void* stream) {
+  TDE_CHECK_ARG(step != nullptr);
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), step);
+  return tde_launch_status();
+}
+
+int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* v, const float* step, float lr,
+                    float beta1, float beta2, float eps, void* stream) {
+  TDE_CHECK_ARG(n % 4 == 0 && param && grad && m && v && step);
+  TDE_CHECK_ARG(tde_aligned16(param) && tde_aligned16(grad) && tde_aligned16(m) && tde_aligned16(v));
+  const long n4 = (long)(n / 4);
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(n4)), dim3(256), 0, static_cast<hipStream_t>(stream), n4,
+                     reinterpret_cast<f4*>(param), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(m),
+                     reinterpret_cast<f4*>(v), step, lr, beta1, beta2, eps);
+  return tde_launch_status();
+}
+
+int tde_zero_bytes(size_t bytes, void* p, void* stream) {
+  TDE_CHECK_ARG(p != nullptr);
+  return hipMemsetAsync(p, 0, bytes, static_cast<hipStream_t>(stream)) == hipSuccess ? TDE_OK : TDE_ERR_HIP;
+}
+
+int tde_spatial_mean_fwd(int N, int HW, int C, const float* x, int x_cstride, float* y, void* stream) {
+  TDE_CHECK_ARG(N > 0 && HW > 0 && C > 0 && x && y);
+  hipLaunchKernelGGL(spatial_mean_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), N, HW, C, x, x_cstride, y);
+  return tde_launch_status();
+}
+
+int tde_spatial_mean_bwd(int N, int HW, int C, float* dx, int dx_cstride, int accumulate, const float* dy,
+                         void* stream) {
+  TDE_CHECK_ARG(N > 0 && HW > 0 && C > 0 && dx && dy);
+  hipLaunchKernelGGL(spatial_mean_bwd_kernel, dim3(ew_grid((long)N * HW * C)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), N, HW, C, dx, dx_cstride, accumulate, dy);
+  return tde_launch_status();
+}
+
+int tde_fill(size_t n, float* x, float value, void* stream) {
+  TDE_CHECK_ARG(x != nullptr);
+  hipLaunchKernelGGL(fill_kernel, dim3(ew_grid((long)n)), dim3(256), 0, static_cast<hipStream_t>(stream), (long)n, x,
+                     value);
+  return tde_launch_status();
+}
+
+int tde_copy_view(int M, int C, const float* src, int s_cstride, int s_coff, float* dst, int d_cstride, int d_coff,
+                  int accumulate, void* stream) {
+  TDE_CHECK_ARG(M > 0 && C > 0 && src && dst);
+  hipLaunchKernelGGL(copy_view_kernel, dim3(ew_grid((long)M * C)), dim3(256), 0, static_cast<hipStream_t>(stream), M,
+                     C, src, s_cstride, s_coff, dst, d_cstride, d_coff, accumulate);
+  return tde_launch_status();
+}
+
+}  // extern "C"

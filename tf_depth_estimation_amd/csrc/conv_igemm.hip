@@ -1,0 +1,522 @@
+// MFMA implicit-GEMM convolution for gfx950 (fp32 in, fp32 accumulate, exact fp32 MFMA).
+//
+// Replaces TF's Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter as emitted by slim.conv2d and
+// slim.conv2d_transpose in nets_optflow_depth.py:88-144, nets_depth.py:88-191 (SURVEY.md §8a rows a1,a2).
+// One kernel template, three operand-gather modes over the *virtual forward conv*
+//   y[n,oh,ow,k] = sum_{kh,kw,c} x[n, oh*S-PT+kh, ow*S-PL+kw, c] * w[kh,kw,c,k]:
+//   FWD  : C[m=(n,oh,ow)][k]      = sum_{(kh,kw,c)}  x(...) w            (conv fwd, deconv bwd-data)
+//   DGRAD: C[m=(n,ih,iw)][c]      = sum_{(th,tw,k)}  dy(...) w           (conv bwd-data, deconv fwd)
+//          stride-S problems split into S*S output-parity classes, each a dense stride-1 GEMM
+//          over only the taps that hit it (sub-pixel decomposition, no zero-insertion).
+//   WGRAD: C[m=(kh,kw,c)][k]      = sum_{pixels}     x(...) dy           (conv/deconv bwd-filter)
+// Tiles: BM x BN x 16 per 256-thread block (4 waves), each wave TM x TN 16x16 accumulators driven by
+// v_mfma_f32_16x16x4_f32 (exact f32: bit-for-bit an fma chain, so results match the fp32 oracle to
+// rounding).  Operands are register-staged into a double-buffered LDS image whose layout follows the
+// operand's natural 16-byte vector direction in HBM (m-major [row][k] or k-major [k][row]), so every
+// global load is a coalesced dwordx4 and every LDS store a ds_write_b128.  Split-K partials go to a
+// caller workspace and are reduced by a second kernel (deterministic; no float atomics).
+#include "tde_common.h"
+
+namespace {
+
+constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
+constexpr int BK = 16;
+constexpr int NT = 256;
+
+struct ConvArgs {
+  int N, H, W, C, OH, OW, K, KH, KW, S, PT, PL, wcin;
+  const float* x; float* dx; int xcs, xco;
+  const float* dy; float* y; int ycs, yco;
+  const float* w; float* dw;
+  float* ws; int splits; int accumulate;
+  int kt_per;  // k-tiles per split
+};
+
+// Per-class geometry of the DGRAD sub-pixel decomposition.
+struct DgClass {
+  int py, px, khs, kws, dh, dw, nth, ntw, HH, WW, M, Kd;
+};
+
+__device__ __forceinline__ DgClass dg_class(const ConvArgs& p, int cls) {
+  DgClass g;
+  g.py = cls / p.S;
+  g.px = cls - g.py * p.S;
+  g.khs = (g.py + p.PT) % p.S;
+  g.kws = (g.px + p.PL) % p.S;
+  g.dh = (g.py + p.PT - g.khs) / p.S;
+  g.dw = (g.px + p.PL - g.kws) / p.S;
+  g.nth = (p.KH - g.khs + p.S - 1) / p.S;
+  g.ntw = (p.KW - g.kws + p.S - 1) / p.S;
+  g.HH = (p.H - g.py + p.S - 1) / p.S;
+  g.WW = (p.W - g.px + p.S - 1) / p.S;
+  g.M = p.N * g.HH * g.WW;
+  g.Kd = g.nth * g.ntw * p.K;
+  return g;
+}
+
+// LDS operand images. MMAJ: [rows][LDK] (k contiguous, read with one ds_read_b128 per fragment);
+// KMAJ: [BK][rows+4] (rows contiguous, 4 ds_read_b32 per fragment; conflict-free for 16-row groups).
+constexpr int LDK = BK + 4;
+
+template <int ROWS, bool KMAJ>
+struct LdsImg {
+  static constexpr int LD = KMAJ ? (ROWS + 4) : LDK;
+  static constexpr int SIZE = KMAJ ? BK * (ROWS + 4) : ROWS * LDK;
+  __device__ static __forceinline__ f4 frag(const float* s, int row, int q) {
+    if constexpr (KMAJ) {
+      f4 r;
+      r[0] = s[(4 * q + 0) * LD + row];
+      r[1] = s[(4 * q + 1) * LD + row];
+      r[2] = s[(4 * q + 2) * LD + row];
+      r[3] = s[(4 * q + 3) * LD + row];
+      return r;
+    } else {
+      return *reinterpret_cast<const f4*>(s + row * LDK + 4 * q);
+    }
+  }
+  // store 4 consecutive elements: along k (MMAJ, at [row][k..k+3]) or along rows (KMAJ, [k][row..row+3])
+  __device__ static __forceinline__ void put(float* s, int row, int k, f4 v) {
+    if constexpr (KMAJ) *reinterpret_cast<f4*>(s + k * LD + row) = v;
+    else *reinterpret_cast<f4*>(s + row * LDK + k) = v;
+  }
+};
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT) igemm_kernel(const ConvArgs p) {
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1, "tile");
+  // A/B LDS image orientation per mode (see header)
+  constexpr bool A_KMAJ = (MODE == MODE_WGRAD);
+  constexpr bool B_KMAJ = (MODE != MODE_DGRAD);
+  using IA = LdsImg<BM, A_KMAJ>;
+  using IB = LdsImg<BN, B_KMAJ>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::SIZE + IB::SIZE)];
+  float* const As0 = smem;
+  float* const Bs0 = smem + 2 * IA::SIZE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  // ---- problem geometry for this block
+  int M, Nn, Kd;
+  DgClass g{};
+  int zsplit;
+  if constexpr (MODE == MODE_DGRAD) {
+    const int ncls = p.S * p.S;
+    const int cls = blockIdx.z % ncls;
+    zsplit = blockIdx.z / ncls;
+    g = dg_class(p, cls);
+    M = g.M; Nn = p.C; Kd = g.Kd;
+  } else if constexpr (MODE == MODE_FWD) {
+    zsplit = blockIdx.z;
+    M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
+  } else {
+    zsplit = blockIdx.z;
+    M = p.KH * p.KW * p.C; Nn = p.K; Kd = p.N * p.OH * p.OW;
+  }
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (m0 >= M || n0 >= Nn) return;
+  const int nkt = (Kd + BK - 1) / BK;
+  const int kt0 = zsplit * p.kt_per;
+  const int kt1 = min(nkt, kt0 + p.kt_per);
+
+  // ---- staging slot bookkeeping
+  // A slots: MMAJ -> (row = s>>2, kq = s&3); KMAJ -> (kk = s / (BM/4), rq = s % (BM/4))
+  constexpr int A_SLOTS = BM * BK / 4, B_SLOTS = BN * BK / 4;
+  constexpr int A_PER = (A_SLOTS + NT - 1) / NT, B_PER = (B_SLOTS + NT - 1) / NT;
+  int a_i0[A_PER], a_i1[A_PER], a_i2[A_PER];  // per-slot precomputed row geometry
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int s = tid + i * NT;
+    a_ok[i] = false; a_i0[i] = a_i1[i] = a_i2[i] = 0;
+    if (s >= A_SLOTS) continue;
+    if constexpr (MODE == MODE_FWD) {
+      const int m = m0 + (s >> 2);
+      if (m < M) {
+        const int ohw = p.OH * p.OW;
+        const int n = m / ohw, r = m - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+        a_ok[i] = true; a_i0[i] = n; a_i1[i] = oh * p.S - p.PT; a_i2[i] = ow * p.S - p.PL;
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int m = m0 + (s >> 2);
+      if (m < M) {
+        const int hw = g.HH * g.WW;
+        const int n = m / hw, r = m - n * hw, ihh = r / g.WW, iww = r - ihh * g.WW;
+        a_ok[i] = true; a_i0[i] = n; a_i1[i] = ihh + g.dh; a_i2[i] = iww + g.dw;
+      }
+    } else {
+      const int m = m0 + 4 * (s % (BM / 4));
+      if (m < M) {
+        const int tap = m / p.C, c = m - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
+        a_ok[i] = true; a_i0[i] = c; a_i1[i] = kh - p.PT; a_i2[i] = kw - p.PL;
+      }
+    }
+  }
+
+  f4 ra[A_PER], rb[B_PER];
+
+  auto load_tiles = [&](int kt) {
+    const int kbase = kt * BK;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int s = tid + i * NT;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (s < A_SLOTS && a_ok[i]) {
+        if constexpr (MODE == MODE_FWD) {
+          const int k = kbase + 4 * (s & 3);
+          if (k < Kd) {
+            const int tap = k / p.C, c = k - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
+            const int ih = a_i1[i] + kh, iw = a_i2[i] + kw;
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              v = ld4(p.x + ((long)(a_i0[i] * p.H + ih) * p.W + iw) * p.xcs + p.xco + c);
+          }
+        } else if constexpr (MODE == MODE_DGRAD) {
+          const int k = kbase + 4 * (s & 3);
+          if (k < Kd) {
+            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
+            const int oh = a_i1[i] - th, ow = a_i2[i] - tw;
+            if ((unsigned)oh < (unsigned)p.OH && (unsigned)ow < (unsigned)p.OW)
+              v = ld4(p.dy + ((long)(a_i0[i] * p.OH + oh) * p.OW + ow) * p.ycs + p.yco + co);
+          }
+        } else {
+          const int pix = kbase + s / (BM / 4);
+          if (pix < Kd) {
+            const int ohw = p.OH * p.OW;
+            const int n = pix / ohw, r = pix - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+            const int ih = oh * p.S + a_i1[i], iw = ow * p.S + a_i2[i];
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              v = ld4(p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + a_i0[i]);
+          }
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int s = tid + i * NT;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (s < B_SLOTS) {
+        if constexpr (MODE == MODE_FWD) {
+          const int k = kbase + s / (BN / 4), n = n0 + 4 * (s % (BN / 4));
+          if (k < Kd && n < Nn) {
+            const int tap = k / p.C, c = k - tap * p.C;
+            if (c < p.wcin) v = ld4(p.w + (long)(tap * p.wcin + c) * p.K + n);
+          }
+        } else if constexpr (MODE == MODE_DGRAD) {
+          const int ci = n0 + (s >> 2), k = kbase + 4 * (s & 3);
+          if (k < Kd && ci < p.wcin) {
+            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
+            const int kh = g.khs + p.S * th, kw = g.kws + p.S * tw;
+            v = ld4(p.w + ((long)(kh * p.KW + kw) * p.wcin + ci) * p.K + co);
+          }
+        } else {
+          const int pix = kbase + s / (BN / 4), n = n0 + 4 * (s % (BN / 4));
+          if (pix < Kd && n < Nn) v = ld4(p.dy + (long)pix * p.ycs + p.yco + n);
+        }
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int s = tid + i * NT;
+      if (s < A_SLOTS) {
+        if constexpr (A_KMAJ) IA::put(As0 + buf * IA::SIZE, 4 * (s % (BM / 4)), s / (BM / 4), ra[i]);
+        else IA::put(As0 + buf * IA::SIZE, s >> 2, 4 * (s & 3), ra[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int s = tid + i * NT;
+      if (s < B_SLOTS) {
+        if constexpr (B_KMAJ) IB::put(Bs0 + buf * IB::SIZE, 4 * (s % (BN / 4)), s / (BN / 4), rb[i]);
+        else IB::put(Bs0 + buf * IB::SIZE, s >> 2, 4 * (s & 3), rb[i]);
+      }
+    }
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wrow0 = wm * TM * 16, wcol0 = wn * TN * 16;
+
+  if (kt0 < kt1) {
+    load_tiles(kt0);
+    store_tiles(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = (kt + 1 < kt1);
+      if (more) load_tiles(kt + 1);
+      f4 fa[TM], fb[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) fa[a] = IA::frag(As0 + cur * IA::SIZE, wrow0 + a * 16 + r16, q);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) fb[b] = IB::frag(Bs0 + cur * IB::SIZE, wcol0 + b * 16 + r16, q);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][j], fb[b][j], acc[a][b], 0, 0, 0);
+      if (more) store_tiles(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---- epilogue: C/D map of 16x16x4: col = lane&15, row = 4*(lane>>4) + reg
+  const bool direct = (p.splits == 1);
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wrow0 + a * 16 + 4 * q + r;
+      if (m >= M) continue;
+      long rowaddr;
+      bool rowok = true;
+      if constexpr (MODE == MODE_FWD) {
+        rowaddr = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const int hw = g.HH * g.WW;
+        const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
+        const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
+        rowaddr = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
+      } else {
+        if (direct) {
+          const int tap = m / p.C, c = m - tap * p.C;
+          rowok = c < p.wcin;
+          rowaddr = (long)(tap * p.wcin + c) * p.K;
+        } else {
+          rowaddr = ((long)zsplit * M + m) * Nn;
+        }
+      }
+      if (!rowok) continue;
+      float* base;
+      if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
+      else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
+      else base = direct ? p.dw : p.ws;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wcol0 + b * 16 + r16;
+        if (n < Nn) {
+          float* dst = base + rowaddr + n;
+          const float v = acc[a][b][r];
+          *dst = (direct && p.accumulate) ? (*dst + v) : v;
+        }
+      }
+    }
+  }
+}
+
+// Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col]
+template <int MODE>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols) {
+  const long total4 = (long)rows * (cols / 4);
+  const long stride = (long)rows * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / (cols / 4));
+    const int col = 4 * (int)(i - (long)row * (cols / 4));
+    f4 s = ld4(p.ws + (long)row * cols + col);
+    for (int z = 1; z < p.splits; ++z) s += ld4(p.ws + z * stride + (long)row * cols + col);
+    float* dst;
+    if constexpr (MODE == MODE_FWD) {
+      dst = p.y + (long)row * p.ycs + p.yco + col;
+    } else if constexpr (MODE == MODE_DGRAD) {
+      dst = p.dx + (long)row * p.xcs + p.xco + col;
+    } else {
+      const int tap = row / p.C, c = row - tap * p.C;
+      if (c >= p.wcin) continue;
+      dst = p.dw + (long)(tap * p.wcin + c) * p.K + col;
+    }
+    if (p.accumulate) s += ld4(dst);
+    *reinterpret_cast<f4*>(dst) = s;
+  }
+}
+
+// ------------------------------------------------------------------ host dispatch
+struct Plan {
+  int bm, bn, splits, kt_per, gx, gy, gz;
+  int rows, cols;  // reduce extent
+  size_t ws_bytes;
+};
+
+static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, long& Kd, int& ncls) {
+  ncls = 1;
+  if (mode == MODE_FWD) {
+    M = (long)d.N * d.OH * d.OW; Nn = d.K; Kd = (long)d.KH * d.KW * d.C;
+  } else if (mode == MODE_DGRAD) {
+    ncls = d.stride * d.stride;
+    const long hh = (d.H + d.stride - 1) / d.stride, ww = (d.W + d.stride - 1) / d.stride;
+    M = (long)d.N * hh * ww;  // largest class
+    Nn = d.C;
+    const long th = (d.KH + d.stride - 1) / d.stride, tw = (d.KW + d.stride - 1) / d.stride;
+    Kd = th * tw * d.K;
+  } else {
+    M = (long)d.KH * d.KW * d.C; Nn = d.K; Kd = (long)d.N * d.OH * d.OW;
+  }
+}
+
+static Plan make_plan(const tde_conv_desc_t& d, int mode) {
+  long M, Nn, Kd; int ncls;
+  gemm_dims(d, mode, M, Nn, Kd, ncls);
+  Plan pl{};
+  pl.bn = Nn <= 16 ? 16 : (Nn <= 32 ? 32 : (Nn <= 64 ? 64 : 128));
+  pl.bm = 128;
+  long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
+  if (tiles < 256 && M <= 4096) {
+    pl.bm = 64;
+    tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
+  }
+  const int nkt = tde_cdiv(Kd, BK);
+  // split K until ~2 blocks per CU, keeping >= 8 k-tiles per split
+  int splits = 1;
+  const long target = 512;
+  if (tiles < target) {
+    splits = (int)((target + tiles - 1) / tiles);
+    splits = splits > nkt / 8 ? nkt / 8 : splits;
+    if (splits < 1) splits = 1;
+    if (splits > 64) splits = 64;
+  }
+  pl.kt_per = tde_cdiv(nkt, splits);
+  pl.splits = tde_cdiv(nkt, pl.kt_per);
+  pl.gx = tde_cdiv(M, pl.bm);
+  pl.gy = tde_cdiv(Nn, pl.bn);
+  pl.gz = pl.splits * ncls;
+  if (mode == MODE_FWD) { pl.rows = (int)M; pl.cols = (int)Nn; }
+  else if (mode == MODE_DGRAD) { pl.rows = d.N * d.H * d.W; pl.cols = d.C; }
+  else { pl.rows = (int)M; pl.cols = (int)Nn; }
+  pl.ws_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.rows * pl.cols * sizeof(float) : 0;
+  return pl;
+}
+
+template <int MODE, int BM, int BN>
+static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
+  constexpr int WN = BN >= 32 ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+}
+
+template <int MODE>
+static void launch_mode(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  dim3 grid(pl.gx, pl.gy, pl.gz);
+  if (pl.bm == 128) {
+    switch (pl.bn) {
+      case 16: launch_cfg<MODE, 128, 16>(a, grid, st); break;
+      case 32: launch_cfg<MODE, 128, 32>(a, grid, st); break;
+      case 64: launch_cfg<MODE, 128, 64>(a, grid, st); break;
+      default: launch_cfg<MODE, 128, 128>(a, grid, st); break;
+    }
+  } else {
+    switch (pl.bn) {
+      case 16: launch_cfg<MODE, 64, 16>(a, grid, st); break;
+      case 32: launch_cfg<MODE, 64, 32>(a, grid, st); break;
+      case 64: launch_cfg<MODE, 64, 64>(a, grid, st); break;
+      default: launch_cfg<MODE, 64, 128>(a, grid, st); break;
+    }
+  }
+}
+
+static bool desc_ok(const tde_conv_desc_t* d) {
+  if (!d) return false;
+  if (d->N <= 0 || d->H <= 0 || d->W <= 0 || d->C <= 0 || d->OH <= 0 || d->OW <= 0 || d->K <= 0) return false;
+  if (d->KH <= 0 || d->KW <= 0 || d->stride <= 0 || d->pad_top < 0 || d->pad_left < 0) return false;
+  if (d->C % 4 || d->K % 4 || d->x_cstride % 4 || d->x_coff % 4 || d->y_cstride % 4 || d->y_coff % 4) return false;
+  if (d->w_cin <= 0 || d->w_cin > d->C) return false;
+  if (d->x_coff + d->C > d->x_cstride || d->y_coff + d->K > d->y_cstride) return false;
+  return true;
+}
+
+static ConvArgs make_args(const tde_conv_desc_t& d) {
+  ConvArgs a{};
+  a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.OH = d.OH; a.OW = d.OW; a.K = d.K;
+  a.KH = d.KH; a.KW = d.KW; a.S = d.stride; a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
+  a.xcs = d.x_cstride; a.xco = d.x_coff; a.ycs = d.y_cstride; a.yco = d.y_coff;
+  return a;
+}
+
+template <int MODE>
+static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  const Plan pl = make_plan(*d, MODE);
+  if (pl.ws_bytes > ws_bytes || (pl.ws_bytes && !tde_aligned16(ws))) return TDE_ERR_WORKSPACE;
+  a.ws = static_cast<float*>(ws);
+  a.splits = pl.splits;
+  a.kt_per = pl.kt_per;
+  a.accumulate = accumulate;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  launch_mode<MODE>(pl, a, st);
+  if (pl.splits > 1) {
+    const long n4 = (long)pl.rows * (pl.cols / 4);
+    int blocks = (int)((n4 + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3(blocks), dim3(256), 0, st, a, pl.rows, pl.cols);
+  }
+  return tde_launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op) {
+  if (!desc_ok(d) || op < 0 || op > 2) return 0;
+  return make_plan(*d, op == 0 ? MODE_FWD : (op == 1 ? MODE_DGRAD : MODE_WGRAD)).ws_bytes;
+}
+
+size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op) {
+  // deconv fwd = DGRAD, bwd_data = FWD, bwd_filter = WGRAD of the virtual conv
+  if (!desc_ok(d) || op < 0 || op > 2) return 0;
+  return make_plan(*d, op == 0 ? MODE_DGRAD : (op == 1 ? MODE_FWD : MODE_WGRAD)).ws_bytes;
+}
+
+int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y, int accumulate,
+                   void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y));
+  ConvArgs a = make_args(*d);
+  a.x = x; a.w = w; a.y = y;
+  return run<MODE_FWD>(d, a, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
+                        void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx));
+  ConvArgs a = make_args(*d);
+  a.dy = dy; a.w = w; a.dx = dx;
+  return run<MODE_DGRAD>(d, a, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
+                          void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(dw));
+  ConvArgs a = make_args(*d);
+  a.x = x; a.dy = dy; a.dw = dw;
+  return run<MODE_WGRAD>(d, a, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
+                     int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return tde_conv2d_bwd_data(d, x_small, w, y_big, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,
+                          int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return tde_conv2d_fwd(d, dy_big, w, dx_small, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, float* dw,
+                            int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return tde_conv2d_bwd_filter(d, dy_big, x_small, dw, accumulate, ws, ws_bytes, stream);
+}
+
+}  // extern "C"

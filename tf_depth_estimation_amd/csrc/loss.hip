@@ -1,0 +1,118 @@
+// Fused forward+backward loss-head kernels.  Each call adds
+// weight*term into a device fp64 scalar and adds d(weight*term)/d(pred) into a gradient view, in one
+// pass over the prediction: the loss is the top of the graph, so its backward needs no saved state.
+#include "tde_common.h"
+
+namespace {
+
+// value of the smoothed map at (n,i,j): pred or 1/pred (train_depth_then_cam_lr.py:217 smooths 1/disp)
+struct Map {
+  const float* p; int H, W, cs, co, recip;
+  __device__ __forceinline__ float operator()(int n, int i, int j) const {
+    const float v = p[((long)(n * H + i) * W + j) * cs + co];
+    return recip ? 1.f / v : v;
+  }
+};
+
+// compute_smooth_loss (train_depth_then_cam_lr.py:59-68): with f the map, TF evaluates
+//   dx = f[:, :, 1:] - f[:, :, :-1], dy = f[:, 1:] - f[:, :-1]
+//   dx2 = dx[:, :, 1:] - dx[:, :, :-1]; dxdy = dx[:, 1:] - dx[:, :-1]
+//   dydx = dy[:, :, 1:] - dy[:, :, :-1]; dy2 = dy[:, 1:] - dy[:, :-1]
+// and sums mean|.| of each.  The four second differences are evaluated here in the same fp32 order.
+__device__ __forceinline__ float t_dx2(const Map& f, int n, int i, int j) {
+  return (f(n, i, j + 2) - f(n, i, j + 1)) - (f(n, i, j + 1) - f(n, i, j));
+}
+__device__ __forceinline__ float t_dxdy(const Map& f, int n, int i, int j) {
+  return (f(n, i + 1, j + 1) - f(n, i + 1, j)) - (f(n, i, j + 1) - f(n, i, j));
+}
+__device__ __forceinline__ float t_dydx(const Map& f, int n, int i, int j) {
+  return (f(n, i + 1, j + 1) - f(n, i, j + 1)) - (f(n, i + 1, j) - f(n, i, j));
+}
+__device__ __forceinline__ float t_dy2(const Map& f, int n, int i, int j) {
+  return (f(n, i + 2, j) - f(n, i + 1, j)) - (f(n, i + 1, j) - f(n, i, j));
+}
+
+__global__ void __launch_bounds__(256) smooth2_kernel(int N, int H, int W, Map f, float weight, double* loss,
+                                                      float* g, int gcs, int gco) {
+  __shared__ double sh[4];
+  const double n1 = (double)N * H * (W - 2), n23 = (double)N * (H - 1) * (W - 1), n4 = (double)N * (H - 2) * W;
+  const float w1 = (float)(weight / n1), w23 = (float)(weight / n23), w4 = (float)(weight / n4);
+  const long total = (long)N * H * W;
+  double lsum = 0.0;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % W);
+    const long t = idx / W;
+    const int i = (int)(t % H), n = (int)(t / H);
+    // forward terms anchored at (i,j)
+    float lv = 0.f;
+    if (j < W - 2) lv += fabsf(t_dx2(f, n, i, j)) * w1;
+    if (i < H - 1 && j < W - 1) lv += (fabsf(t_dxdy(f, n, i, j)) + fabsf(t_dydx(f, n, i, j))) * w23;
+    if (i < H - 2) lv += fabsf(t_dy2(f, n, i, j)) * w4;
+    lsum += lv;
+    // gradient wrt f(n,i,j): every term that contains it, times d|t|/dt = sign(t)
+    float gf = 0.f;
+    if (j < W - 2) gf += tde_sign(t_dx2(f, n, i, j)) * w1;
+    if (j >= 1 && j - 1 < W - 2) gf -= 2.f * tde_sign(t_dx2(f, n, i, j - 1)) * w1;
+    if (j >= 2) gf += tde_sign(t_dx2(f, n, i, j - 2)) * w1;
+    if (i < H - 2) gf += tde_sign(t_dy2(f, n, i, j)) * w4;
+    if (i >= 1 && i - 1 < H - 2) gf -= 2.f * tde_sign(t_dy2(f, n, i - 1, j)) * w4;
+    if (i >= 2) gf += tde_sign(t_dy2(f, n, i - 2, j)) * w4;
+    // dxdy/dydx(a,b) = f(a+1,b+1) - f(a+1,b) - f(a,b+1) + f(a,b)
+    if (i < H - 1 && j < W - 1) gf += (tde_sign(t_dxdy(f, n, i, j)) + tde_sign(t_dydx(f, n, i, j))) * w23;
+    if (i < H - 1 && j >= 1) gf -= (tde_sign(t_dxdy(f, n, i, j - 1)) + tde_sign(t_dydx(f, n, i, j - 1))) * w23;
+    if (i >= 1 && j < W - 1) gf -= (tde_sign(t_dxdy(f, n, i - 1, j)) + tde_sign(t_dydx(f, n, i - 1, j))) * w23;
+    if (i >= 1 && j >= 1) gf += (tde_sign(t_dxdy(f, n, i - 1, j - 1)) + tde_sign(t_dydx(f, n, i - 1, j - 1))) * w23;
+    if (f.recip) {
+      const float p = f.p[((long)(n * H + i) * W + j) * f.cs + f.co];
+      gf *= -1.f / (p * p);
+    }
+    g[((long)(n * H + i) * W + j) * gcs + gco] += gf;
+  }
+  const double bs = tde_block_sum_d(lsum, sh);
+  if (threadIdx.x == 0) atomicAdd(loss, bs);
+}
+
+__global__ void __launch_bounds__(256) l1_kernel(long total, const float* pred, int cs, int co, const float* label,
+                                                 int nonfinite, float weight, double* loss, float* g, int gcs,
+                                                 int gco) {
+  __shared__ double sh[4];
+  const float wn = (float)(weight / (double)total);
+  double lsum = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    float d = label[i] - pred[i * cs + co];
+    if (nonfinite && !isfinite(d)) d = 0.f;  // lmbspecialops.replace_nonfinite; gradient masked too
+    lsum += fabsf(d);
+    g[i * gcs + gco] += -tde_sign(d) * wn;
+  }
+  const double bs = tde_block_sum_d(lsum, sh);
+  if (threadIdx.x == 0) atomicAdd(loss, bs * (double)weight / (double)total);
+}
+
+int ew_grid(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+extern "C" {
+
+int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int coff, int recip, float weight,
+                     double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  TDE_CHECK_ARG(N > 0 && H >= 3 && W >= 3 && pred && loss && grad);
+  Map f{pred, H, W, cstride, coff, recip};
+  hipLaunchKernelGGL(smooth2_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     N, H, W, f, weight, loss, grad, g_cstride, g_coff);
+  return tde_launch_status();
+}
+
+int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, const float* label, int nonfinite,
+                float weight, double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && pred && label && loss && grad);
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(l1_kernel, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, pred,
+                     cstride, coff, label, nonfinite, weight, loss, grad, g_cstride, g_coff);
+  return tde_launch_status();
+}
+
+}  // extern "C"

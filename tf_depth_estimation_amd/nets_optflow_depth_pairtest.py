@@ -1,0 +1,19 @@
+"""MI355X-native `nets_optflow_depth_pairtest` (reference: nets_optflow_depth_pairtest.py): the
+4-scale `depth_net` whose outputs match the 4-scale loss loop of train_depth_then_cam_lr.py:211
+(SURVEY.md Appendix C, config 4).
+
+    depth_net(tgt_image, is_training=True)
+        -> ([disp1..disp4], pose[b,1,6], [mask1..mask4], end_points)      (:151-276)
+BN uses slim's default decay 0.999 (:152).
+"""
+from . import _api, _netlib, pose_ops
+
+DISP_SCALING = 4
+MIN_DISP = 0
+
+
+def depth_net(tgt_image, is_training=True):
+    outs, prog = _api.run_net("depth_cam_net", _netlib.depth_net_spec, tgt_image, is_training, levels=4)
+    disps, pose_pred, masks = outs[:4], outs[4], outs[5:]
+    pose_final = pose_ops.reduce_mean_hw(pose_pred).reshape(-1, 1, 6)
+    return disps, pose_final, masks, {"program": prog}

@@ -1,0 +1,416 @@
+"""Layer-program executor: a static schedule of C-ABI kernel calls for one encoder/decoder network.
+
+The reference builds each network as a TF-1 graph of slim layers (nets_optflow_depth.py:76-276,
+nets_depth.py:76-199).  Here a network is built once per (input H, W) into a `NetSpec`: a list of ops
+over *channel views* of NHWC activation buffers.  tf.concat(axis=3) is never materialised: each
+producer writes its result straight into its channel slice of the consumer's buffer, and the
+consumer's implicit-GEMM reads the whole buffer (include/tde.h "channel view").  Concat buffers whose
+width is not a multiple of 4 (e.g. 64+64+1 = 129 for icnv3) are zero-padded to 4 so every conv
+operand is a 16-byte vector; the padded weight rows read as zero (`w_cin`).
+
+Backward is the reverse schedule: for every op, the gradient of its output view is complete when it
+is reached (all consumers come later in forward order), and the op writes (first writer) or
+accumulates (later writers) into the gradient view of its input.  Parameter gradients always
+accumulate into the ParamChunk's flat gradient buffer, which the trainer zeroes once per step, so a
+network called twice with shared variables (train_depth_then_cam_lr.py:130-136) sums both calls like
+TF does.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ConvDesc, ptr
+
+
+def same_pad(n, k, s):
+    out = -(-n // s)
+    tot = max((out - 1) * s + k - n, 0)
+    return out, tot // 2
+
+
+def pad4(c):
+    return (c + 3) // 4 * 4
+
+
+class Buf:
+    def __init__(self, name, H, W, cs, zero=False):
+        self.name, self.H, self.W, self.cs, self.zero = name, H, W, cs, zero
+
+
+class View:
+    def __init__(self, buf, coff, C, creal=None):
+        self.buf, self.coff, self.C = buf, coff, C
+        self.creal = C if creal is None else creal
+
+    @property
+    def H(self):
+        return self.buf.H
+
+    @property
+    def W(self):
+        return self.buf.W
+
+
+class Op:
+    params = ()
+
+
+class ConvBN(Op):
+    """slim.conv2d / slim.conv2d_transpose with normalizer_fn=batch_norm (+ReLU); or, with bn=False,
+    with bias (+ReLU) as in the BN-free pairtest disp_net (nets_optflow_depth_pairtest.py:83-85)."""
+
+    def __init__(self, layer, src, dst, K, k, s, deconv=False, bn=True, decay=0.99):
+        self.layer, self.src, self.dst, self.K, self.k, self.s = layer, src, dst, K, k, s
+        self.deconv, self.bn, self.decay = deconv, bn, decay
+        cin = src.creal
+        if deconv:
+            # virtual forward conv: x = deconv output (dst, 2h x 2w x K), y = deconv input (src)
+            self.OH, self.OW = src.H, src.W
+            H, W = dst.H, dst.W
+            _, self.pt = same_pad(H, k, s)
+            _, self.pl = same_pad(W, k, s)
+            wshape = (k, k, K, cin)
+        else:
+            self.OH, self.pt = same_pad(src.H, k, s)
+            self.OW, self.pl = same_pad(src.W, k, s)
+            wshape = (k, k, cin, K)
+        assert (dst.H, dst.W) == ((src.H * s, src.W * s) if deconv else (self.OH, self.OW)), layer
+        self.params = [(f"{layer}/weights", wshape, "glorot")]
+        if bn:
+            self.params.append((f"{layer}/BatchNorm/beta", (K,), "zeros"))
+            self.bn_stats = [(f"{layer}/BatchNorm", K)]
+        else:
+            self.params.append((f"{layer}/biases", (K,), "zeros"))
+            self.bn_stats = []
+
+    def desc(self, N):
+        d = ConvDesc()
+        if self.deconv:
+            d.N, d.H, d.W, d.C = N, self.dst.H, self.dst.W, self.K
+            d.OH, d.OW, d.K = self.src.H, self.src.W, self.src.C
+            d.w_cin = self.K
+            d.x_cstride, d.x_coff = self.K, 0                       # dense pre-BN z (big)
+            d.y_cstride, d.y_coff = self.src.buf.cs, self.src.coff  # deconv input view
+        else:
+            d.N, d.H, d.W, d.C = N, self.src.H, self.src.W, self.src.C
+            d.OH, d.OW, d.K = self.OH, self.OW, self.K
+            d.w_cin = self.src.creal
+            d.x_cstride, d.x_coff = self.src.buf.cs, self.src.coff
+            d.y_cstride, d.y_coff = self.K, 0                       # dense pre-BN z
+        d.KH = d.KW = self.k
+        d.stride, d.pad_top, d.pad_left = self.s, self.pt, self.pl
+        return d
+
+    def zshape(self, N):
+        return (N, self.dst.H, self.dst.W, self.K)
+
+
+class Head(Op):
+    """slim.conv2d(normalizer_fn=None) head with bias: act 1 -> scale*sigmoid(.)+offset, 0 -> linear."""
+
+    def __init__(self, layer, src, dst, K, k, act, scale=1.0, offset=0.0):
+        self.layer, self.src, self.dst, self.K, self.k = layer, src, dst, K, k
+        self.act, self.scale, self.offset = act, scale, offset
+        _, self.pt = same_pad(src.H, k, 1)
+        _, self.pl = same_pad(src.W, k, 1)
+        self.params = [(f"{layer}/weights", (k, k, src.creal, K), "glorot"), (f"{layer}/biases", (K,), "zeros")]
+        self.bn_stats = []
+
+    def desc(self, N):
+        d = ConvDesc()
+        d.N, d.H, d.W, d.C = N, self.src.H, self.src.W, self.src.C
+        d.OH, d.OW, d.K = self.src.H, self.src.W, self.K
+        d.KH = d.KW = self.k
+        d.stride, d.pad_top, d.pad_left = 1, self.pt, self.pl
+        d.w_cin = self.src.creal
+        d.x_cstride, d.x_coff = self.src.buf.cs, self.src.coff
+        d.y_cstride, d.y_coff = self.dst.buf.cs, self.dst.coff
+        return d
+
+
+class Resize(Op):
+    """tf.image.resize_nearest_neighbor (resize_like) or resize_bilinear, legacy semantics."""
+
+    def __init__(self, kind, src, dst):
+        self.kind, self.src, self.dst = kind, src, dst
+        self.bn_stats = []
+
+
+class Copy(Op):
+    """Second placement of a tensor that two concats consume (nets_depth.py shares the encoder)."""
+
+    def __init__(self, src, dst):
+        self.src, self.dst = src, dst
+        self.bn_stats = []
+
+
+class NetSpec:
+    """Builder used by the per-net modules (nets_optflow_depth.py etc.)."""
+
+    def __init__(self, scope, H, W, cin):
+        self.scope, self.H, self.W, self.cin = scope, H, W, cin
+        self.bufs, self.ops, self.outputs = [], [], []
+        self.input = self.buffer("input", H, W, pad4(cin), zero=True)
+        self.input_view = View(self.input, 0, pad4(cin), cin)
+
+    def buffer(self, name, H, W, cs, zero=False):
+        b = Buf(name, H, W, cs, zero)
+        self.bufs.append(b)
+        return b
+
+    def concat(self, name, H, W, widths):
+        """Allocate a concat buffer; returns its slice views and the full (padded) view."""
+        total = sum(widths)
+        cs = pad4(total)
+        b = self.buffer(name, H, W, cs, zero=(cs != total))
+        views, off = [], 0
+        for w in widths:
+            views.append(View(b, off, w))
+            off += w
+        return views, View(b, 0, cs, total)
+
+    def dense(self, name, H, W, C):
+        return View(self.buffer(name, H, W, C), 0, C)
+
+    def add(self, op):
+        self.ops.append(op)
+        return op
+
+    def param_specs(self):
+        seen, specs, bn = set(), [], []
+        for op in self.ops:
+            for p in op.params:
+                if p[0] not in seen:
+                    seen.add(p[0])
+                    specs.append(p)
+            for b in op.bn_stats:
+                bn.append(b)
+        return specs, bn
+
+
+class Workspace:
+    """Per-(program, batch) scratch shared by all calls on one stream: split-K / reduction workspace
+    and the dense dz buffer of the BN backward."""
+
+    def __init__(self):
+        self.ws = None
+        self.dz = None
+
+    def get(self, ws_bytes, dz_numel, device):
+        if self.ws is None or self.ws.numel() * 4 < ws_bytes:
+            self.ws = torch.empty(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
+        if self.dz is None or self.dz.numel() < dz_numel:
+            self.dz = torch.empty(max(dz_numel, 4), dtype=torch.float32, device=device)
+        return self.ws, self.dz
+
+
+class NetRun:
+    """Per-invocation state of a program: activations, pre-BN outputs and batch statistics (the
+    'tape' the backward pass needs)."""
+
+    def __init__(self, prog, N, device="cuda"):
+        self.prog, self.N, self.device = prog, N, device
+        self.act = {}
+        for b in prog.spec.bufs:
+            shape = (N, b.H, b.W, b.cs)
+            self.act[b.name] = (torch.zeros(shape, device=device) if b.zero
+                                else torch.empty(shape, device=device))
+        self.z, self.stats = {}, {}
+        for i, op in enumerate(prog.spec.ops):
+            if isinstance(op, ConvBN) and op.bn:
+                self.z[i] = torch.empty(op.zshape(N), device=device)
+                self.stats[i] = torch.empty((2, op.K), device=device)
+            elif isinstance(op, ConvBN):
+                self.z[i] = None
+        self.grad = None
+
+    def vptr(self, v, grad=False):
+        t = (self.grad if grad else self.act)[v.buf.name]
+        return ptr(t)
+
+    def view_tensor(self, v, grad=False):
+        t = (self.grad if grad else self.act)[v.buf.name]
+        return t[..., v.coff:v.coff + v.C]
+
+
+class NetProgram:
+    """Compiled network: spec + parameter chunk + launch schedule (forward and backward)."""
+
+    def __init__(self, spec, chunk, bessel=True):
+        self.spec, self.chunk, self.bessel = spec, chunk, bessel
+        self.prefix = chunk.prefix
+        self._ws = {}
+        self._sizes = {}
+
+    # ---------------------------------------------------------------- helpers
+    def P(self, name):
+        return self.chunk.view(f"{self.prefix}/{name}")
+
+    def G(self, name):
+        return self.chunk.grad_view(f"{self.prefix}/{name}")
+
+    def _scratch(self, N):
+        if N not in self._sizes:
+            lib = _lib.load()
+            ws, dz = 0, 0
+            for op in self.spec.ops:
+                if isinstance(op, ConvBN):
+                    d = op.desc(N)
+                    q = lib.tde_deconv2d_workspace_size if op.deconv else lib.tde_conv2d_workspace_size
+                    for o in range(3):
+                        ws = max(ws, q(ctypes_ref(d), o))
+                    M = N * op.dst.H * op.dst.W
+                    ws = max(ws, lib.tde_bn_workspace_size(M, op.K))
+                    dz = max(dz, M * op.K)
+                elif isinstance(op, Head):
+                    ws = max(ws, lib.tde_head_workspace_size(ctypes_ref(op.desc(N))))
+            self._sizes[N] = (ws, dz)
+        ws, dz = self._sizes[N]
+        w = self._ws.setdefault(N, Workspace())
+        return w.get(ws, dz, "cuda")
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, run, x, is_training=True):
+        """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors."""
+        N = run.N
+        lib = _lib.load()
+        st = _lib.stream_ptr()
+        spec = self.spec
+        iv = spec.input_view
+        assert tuple(x.shape) == (N, spec.H, spec.W, spec.cin), (x.shape, spec.H, spec.W, spec.cin)
+        x = x.contiguous()
+        _lib.check(lib.tde_copy_view(N * spec.H * spec.W, spec.cin, ptr(x), spec.cin, 0, run.vptr(iv), iv.buf.cs, 0,
+                                     0, st), "copy input")
+        ws, _ = self._scratch(N)
+        wsb = ws.numel() * 4
+        for i, op in enumerate(spec.ops):
+            if isinstance(op, ConvBN):
+                d = op.desc(N)
+                w = self.P(f"{op.layer}/weights")
+                z = run.z[i] if op.bn else None
+                if op.deconv:
+                    out_ptr = ptr(z) if op.bn else run.vptr(op.dst)
+                    if not op.bn:
+                        raise NotImplementedError("BN-free deconv")
+                    _lib.check(lib.tde_deconv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), out_ptr, 0, ptr(ws),
+                                                    wsb, st), op.layer)
+                else:
+                    if not op.bn:
+                        raise NotImplementedError("BN-free conv")
+                    _lib.check(lib.tde_conv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb,
+                                                  st), op.layer)
+                M = N * op.dst.H * op.dst.W
+                beta = self.P(f"{op.layer}/BatchNorm/beta")
+                sm = run.stats[i]
+                if is_training:
+                    mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
+                    _lib.check(lib.tde_bn_fwd_train(M, op.K, ptr(z), ptr(beta), 1e-3, op.decay, int(self.bessel),
+                                                    ptr(mm), ptr(mv), ptr(sm[0]), ptr(sm[1]), run.vptr(op.dst),
+                                                    op.dst.buf.cs, op.dst.coff, 1, ptr(ws), wsb, st), op.layer)
+                else:
+                    mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
+                    _lib.check(lib.tde_bn_fwd_infer(M, op.K, ptr(z), ptr(beta), 1e-3, ptr(mm), ptr(mv),
+                                                    run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st), op.layer)
+            elif isinstance(op, Head):
+                d = op.desc(N)
+                _lib.check(lib.tde_head_fwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
+                                            ptr(self.P(f"{op.layer}/biases")), run.vptr(op.dst), op.act, op.scale,
+                                            op.offset, st), op.layer)
+            elif isinstance(op, Resize):
+                s, t = op.src, op.dst
+                fn = lib.tde_resize_nearest_fwd if op.kind == "nearest" else lib.tde_resize_bilinear_fwd
+                _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s), s.buf.cs, s.coff, t.H, t.W, run.vptr(t), t.buf.cs,
+                              t.coff, st), op.kind)
+            elif isinstance(op, Copy):
+                s, t = op.src, op.dst
+                _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(s), s.buf.cs, s.coff, run.vptr(t),
+                                             t.buf.cs, t.coff, 0, st), "copy")
+        return [run.view_tensor(v) for v in spec.outputs]
+
+    # ---------------------------------------------------------------- backward
+    def backward(self, run, grad_outputs, need_input_grad=False):
+        """grad_outputs: list (aligned with spec.outputs) of tensors or None.  Accumulates parameter
+        gradients into chunk.grad.  Returns d(input) if requested."""
+        N = run.N
+        lib = _lib.load()
+        st = _lib.stream_ptr()
+        spec = self.spec
+        if run.grad is None:
+            run.grad = {b.name: torch.empty((N, b.H, b.W, b.cs), device=run.device) for b in spec.bufs}
+        written = {b.name: [] for b in spec.bufs}
+
+        def mark(v):
+            """Return accumulate flag for writing gradient view v and record it."""
+            lst = written[v.buf.name]
+            lo, hi = v.coff, v.coff + v.C
+            for a, b in lst:
+                if a <= lo and hi <= b:
+                    return 1
+                assert hi <= a or b <= lo, f"partial gradient overlap on {v.buf.name}"
+            lst.append((lo, hi))
+            return 0
+
+        for v, g in zip(spec.outputs, grad_outputs):
+            acc = mark(v)
+            if g is None:
+                g = torch.empty((N, v.H, v.W, v.C), device=run.device)
+                _lib.check(lib.tde_fill(g.numel(), ptr(g), 0.0, st), "zero grad_out")
+            g = g.contiguous()
+            _lib.check(lib.tde_copy_view(N * v.H * v.W, v.C, ptr(g), v.C, 0, run.vptr(v, True), v.buf.cs, v.coff,
+                                         acc, st), "grad_out")
+        ws, dz = self._scratch(N)
+        wsb = ws.numel() * 4
+        iv = spec.input_view
+        for i in range(len(spec.ops) - 1, -1, -1):
+            op = spec.ops[i]
+            src_needs = need_input_grad or op.src.buf is not spec.input
+            if isinstance(op, ConvBN):
+                d = op.desc(N)
+                M = N * op.dst.H * op.dst.W
+                sm = run.stats[i]
+                _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
+                                          ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
+                                          op.dst.buf.cs, op.dst.coff, ptr(dz), ptr(self.G(f"{op.layer}/BatchNorm/beta")),
+                                          1, 1, ptr(ws), wsb, st), op.layer + " bn_bwd")
+                w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
+                if op.deconv:
+                    _lib.check(lib.tde_deconv2d_bwd_filter(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(gw), 1,
+                                                           ptr(ws), wsb, st), op.layer + " wgrad")
+                    if src_needs:
+                        acc = mark(op.src)
+                        _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
+                                                             acc, ptr(ws), wsb, st), op.layer + " dgrad")
+                else:
+                    _lib.check(lib.tde_conv2d_bwd_filter(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(gw), 1,
+                                                         ptr(ws), wsb, st), op.layer + " wgrad")
+                    if src_needs:
+                        acc = mark(op.src)
+                        _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True), acc,
+                                                           ptr(ws), wsb, st), op.layer + " dgrad")
+            elif isinstance(op, Head):
+                d = op.desc(N)
+                acc = mark(op.src) if src_needs else 0
+                _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
+                                            run.vptr(op.dst), run.vptr(op.dst, True),
+                                            run.vptr(op.src, True) if src_needs else None, acc,
+                                            ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")), 1,
+                                            op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
+            elif isinstance(op, Resize):
+                s, t = op.src, op.dst
+                acc = mark(s)
+                fn = lib.tde_resize_nearest_bwd if op.kind == "nearest" else lib.tde_resize_bilinear_bwd
+                _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s, True), s.buf.cs, s.coff, acc, t.H, t.W,
+                              run.vptr(t, True), t.buf.cs, t.coff, st), op.kind + " bwd")
+            elif isinstance(op, Copy):
+                s, t = op.src, op.dst
+                acc = mark(s)
+                _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
+                                             run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
+        if need_input_grad:
+            return run.view_tensor(iv, grad=True)[..., :spec.cin]
+        return None
+
+
+def ctypes_ref(d):
+    import ctypes
+    return ctypes.byref(d)
