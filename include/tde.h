@@ -155,6 +155,7 @@ int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* 
 
 /* ---------------------------------------------------------------- utilities */
 int tde_fill(size_t n, float* x, float value, void* stream);
+int tde_scale(size_t n, float* x, float alpha, void* stream);   /* x *= alpha (DP gradient mean) */
 int tde_zero_bytes(size_t bytes, void* p, void* stream);
 /* pose_avg = tf.reduce_mean(pose_pred, [1, 2]) (nets_optflow_depth.py:183): x [N,HW,C] (pixel stride
  * x_cstride) -> y [N,C], and its gradient (dx (+)= dy/HW). */

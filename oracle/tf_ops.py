@@ -31,7 +31,7 @@ def conv2d_same(x, w, stride):
     _, pt, pb = same_pad(H, kh, stride)
     _, pl, pr = same_pad(W, kw, stride)
     xp = F.pad(x.permute(0, 3, 1, 2), (pl, pr, pt, pb))
-    y = F.conv2d(xp, w.permute(3, 2, 0, 1), stride=stride)
+    y = F.conv2d(xp, w.permute(3, 2, 0, 1).contiguous(), stride=stride)
     return y.permute(0, 2, 3, 1)
 
 
@@ -44,7 +44,7 @@ def conv2d_transpose_same(x, w, stride=2):
     H, W = stride * h, stride * wd
     _, pt, _ = same_pad(H, kh, stride)
     _, pl, _ = same_pad(W, kw, stride)
-    full = F.conv_transpose2d(x.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), stride=stride)
+    full = F.conv_transpose2d(x.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1).contiguous(), stride=stride)
     # full index o_full = s*i + k ; TF index o = o_full - pad_before
     fh, fw = full.shape[2], full.shape[3]
     need_h, need_w = pt + H, pl + W

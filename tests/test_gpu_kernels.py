@@ -21,6 +21,8 @@ def close(gpu, ref, tol=TOL, what=""):
     g = gpu.detach().double().cpu()
     r = ref.detach().double().cpu()
     assert g.shape == r.shape, (what, g.shape, r.shape)
+    if r.numel() == 0:
+        return
     scale = max(r.abs().max().item(), 1e-6)
     err = (g - r).abs().max().item()
     assert err <= tol * scale + 1e-7, f"{what}: max err {err:.3e} vs scale {scale:.3e} (rel {err / scale:.3e})"
@@ -31,8 +33,23 @@ def rnd(*shape, seed=0, lo=-1.0, hi=1.0):
     return torch.tensor(g.uniform(lo, hi, size=shape), dtype=torch.float64)
 
 
+_KEEP = []
+
+
 def dev(t):
-    return t.float().cuda().contiguous()
+    """Device copy that stays alive until the next test: `L.ptr(dev(x))` passes a raw pointer, so
+    the tensor must outlive the (asynchronous) kernel and must not be recycled by the allocator for
+    the next temporary in the same call."""
+    d = t.float().cuda().contiguous()
+    _KEEP.append(d)
+    return d
+
+
+@pytest.fixture(autouse=True)
+def _release_temps():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
 
 
 @pytest.fixture(scope="module")

@@ -54,6 +54,7 @@ _SIGS = {
     "tde_adam_step_begin": (c_int, [P, P]),
     "tde_adam_update": (c_int, [c_size_t, P, P, P, P, P, c_float, c_float, c_float, c_float, P]),
     "tde_fill": (c_int, [c_size_t, P, c_float, P]),
+    "tde_scale": (c_int, [c_size_t, P, c_float, P]),
     "tde_zero_bytes": (c_int, [c_size_t, P, P]),
     "tde_spatial_mean_fwd": (c_int, [c_int, c_int, c_int, P, c_int, P, P]),
     "tde_spatial_mean_bwd": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, P]),

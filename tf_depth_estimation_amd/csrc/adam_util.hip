@@ -25,6 +25,10 @@ __global__ void __launch_bounds__(256) adam_kernel(long n4, f4* __restrict__ p, 
   }
 }
 
+__global__ void __launch_bounds__(256) scale_kernel(long n, float* x, float a) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= a;
+}
+
 __global__ void __launch_bounds__(256) fill_kernel(long n, float* x, float val) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] = val;
 }
@@ -119,6 +123,13 @@ int tde_spatial_mean_bwd(int N, int HW, int C, float* dx, int dx_cstride, int ac
   TDE_CHECK_ARG(N > 0 && HW > 0 && C > 0 && dx && dy);
   hipLaunchKernelGGL(spatial_mean_bwd_kernel, dim3(ew_grid((long)N * HW * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, HW, C, dx, dx_cstride, accumulate, dy);
+  return tde_launch_status();
+}
+
+int tde_scale(size_t n, float* x, float alpha, void* stream) {
+  TDE_CHECK_ARG(x != nullptr);
+  hipLaunchKernelGGL(scale_kernel, dim3(ew_grid((long)n)), dim3(256), 0, static_cast<hipStream_t>(stream), (long)n, x,
+                     alpha);
   return tde_launch_status();
 }
 

@@ -21,7 +21,8 @@ class _SpatialMean(torch.autograd.Function):
     def backward(ctx, dy):
         N, H, W, C = ctx.shape
         dx = torch.empty((N, H, W, C), device=dy.device)
-        _lib.call("tde_spatial_mean_bwd", N, H * W, C, ptr(dx), C, 0, ptr(dy.contiguous()), _lib.stream_ptr())
+        dy = dy.contiguous()
+        _lib.call("tde_spatial_mean_bwd", N, H * W, C, ptr(dx), C, 0, ptr(dy), _lib.stream_ptr())
         return dx
 
 

@@ -241,6 +241,10 @@ class NetProgram:
         self.prefix = chunk.prefix
         self._ws = {}
         self._sizes = {}
+        self.timer = None
+
+    def _span(self, family, flops=0.0):
+        return NO_SPAN if self.timer is None else self.timer.span(family, flops)
 
     # ---------------------------------------------------------------- helpers
     def P(self, name):
@@ -288,39 +292,39 @@ class NetProgram:
                 d = op.desc(N)
                 w = self.P(f"{op.layer}/weights")
                 z = run.z[i] if op.bn else None
-                if op.deconv:
-                    out_ptr = ptr(z) if op.bn else run.vptr(op.dst)
-                    if not op.bn:
-                        raise NotImplementedError("BN-free deconv")
-                    _lib.check(lib.tde_deconv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), out_ptr, 0, ptr(ws),
-                                                    wsb, st), op.layer)
-                else:
-                    if not op.bn:
-                        raise NotImplementedError("BN-free conv")
-                    _lib.check(lib.tde_conv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb,
-                                                  st), op.layer)
+                if not op.bn:
+                    raise NotImplementedError("BN-free conv/deconv layers")
+                with self._span("conv_fwd", conv_flops(op, N)):
+                    if op.deconv:
+                        _lib.check(lib.tde_deconv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws),
+                                                        wsb, st), op.layer)
+                    else:
+                        _lib.check(lib.tde_conv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws),
+                                                      wsb, st), op.layer)
                 M = N * op.dst.H * op.dst.W
                 beta = self.P(f"{op.layer}/BatchNorm/beta")
                 sm = run.stats[i]
-                if is_training:
-                    mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
-                    _lib.check(lib.tde_bn_fwd_train(M, op.K, ptr(z), ptr(beta), 1e-3, op.decay, int(self.bessel),
-                                                    ptr(mm), ptr(mv), ptr(sm[0]), ptr(sm[1]), run.vptr(op.dst),
-                                                    op.dst.buf.cs, op.dst.coff, 1, ptr(ws), wsb, st), op.layer)
-                else:
-                    mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
-                    _lib.check(lib.tde_bn_fwd_infer(M, op.K, ptr(z), ptr(beta), 1e-3, ptr(mm), ptr(mv),
-                                                    run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st), op.layer)
+                mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
+                with self._span("bn_fwd"):
+                    if is_training:
+                        _lib.check(lib.tde_bn_fwd_train(M, op.K, ptr(z), ptr(beta), 1e-3, op.decay, int(self.bessel),
+                                                        ptr(mm), ptr(mv), ptr(sm[0]), ptr(sm[1]), run.vptr(op.dst),
+                                                        op.dst.buf.cs, op.dst.coff, 1, ptr(ws), wsb, st), op.layer)
+                    else:
+                        _lib.check(lib.tde_bn_fwd_infer(M, op.K, ptr(z), ptr(beta), 1e-3, ptr(mm), ptr(mv),
+                                                        run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st), op.layer)
             elif isinstance(op, Head):
                 d = op.desc(N)
-                _lib.check(lib.tde_head_fwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
-                                            ptr(self.P(f"{op.layer}/biases")), run.vptr(op.dst), op.act, op.scale,
-                                            op.offset, st), op.layer)
+                with self._span("head_fwd", conv_flops(op, N)):
+                    _lib.check(lib.tde_head_fwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
+                                                ptr(self.P(f"{op.layer}/biases")), run.vptr(op.dst), op.act, op.scale,
+                                                op.offset, st), op.layer)
             elif isinstance(op, Resize):
                 s, t = op.src, op.dst
                 fn = lib.tde_resize_nearest_fwd if op.kind == "nearest" else lib.tde_resize_bilinear_fwd
-                _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s), s.buf.cs, s.coff, t.H, t.W, run.vptr(t), t.buf.cs,
-                              t.coff, st), op.kind)
+                with self._span("resize"):
+                    _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s), s.buf.cs, s.coff, t.H, t.W, run.vptr(t), t.buf.cs,
+                                  t.coff, st), op.kind)
             elif isinstance(op, Copy):
                 s, t = op.src, op.dst
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(s), s.buf.cs, s.coff, run.vptr(t),
@@ -368,39 +372,49 @@ class NetProgram:
                 d = op.desc(N)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
-                _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
-                                          ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
-                                          op.dst.buf.cs, op.dst.coff, ptr(dz), ptr(self.G(f"{op.layer}/BatchNorm/beta")),
-                                          1, 1, ptr(ws), wsb, st), op.layer + " bn_bwd")
+                with self._span("bn_bwd"):
+                    _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
+                                              ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
+                                              op.dst.buf.cs, op.dst.coff, ptr(dz),
+                                              ptr(self.G(f"{op.layer}/BatchNorm/beta")), 1, 1, ptr(ws), wsb, st),
+                               op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
+                fl = conv_flops(op, N)
                 if op.deconv:
-                    _lib.check(lib.tde_deconv2d_bwd_filter(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(gw), 1,
-                                                           ptr(ws), wsb, st), op.layer + " wgrad")
+                    with self._span("conv_wgrad", fl):
+                        _lib.check(lib.tde_deconv2d_bwd_filter(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(gw), 1,
+                                                               ptr(ws), wsb, st), op.layer + " wgrad")
                     if src_needs:
                         acc = mark(op.src)
-                        _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
-                                                             acc, ptr(ws), wsb, st), op.layer + " dgrad")
+                        with self._span("conv_dgrad", fl):
+                            _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w),
+                                                                 run.vptr(op.src, True), acc, ptr(ws), wsb, st),
+                                       op.layer + " dgrad")
                 else:
-                    _lib.check(lib.tde_conv2d_bwd_filter(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(gw), 1,
-                                                         ptr(ws), wsb, st), op.layer + " wgrad")
+                    with self._span("conv_wgrad", fl):
+                        _lib.check(lib.tde_conv2d_bwd_filter(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(gw), 1,
+                                                             ptr(ws), wsb, st), op.layer + " wgrad")
                     if src_needs:
                         acc = mark(op.src)
-                        _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True), acc,
-                                                           ptr(ws), wsb, st), op.layer + " dgrad")
+                        with self._span("conv_dgrad", fl):
+                            _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
+                                                               acc, ptr(ws), wsb, st), op.layer + " dgrad")
             elif isinstance(op, Head):
                 d = op.desc(N)
                 acc = mark(op.src) if src_needs else 0
-                _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
-                                            run.vptr(op.dst), run.vptr(op.dst, True),
-                                            run.vptr(op.src, True) if src_needs else None, acc,
-                                            ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")), 1,
-                                            op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
+                with self._span("head_bwd", 2 * conv_flops(op, N)):
+                    _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
+                                                run.vptr(op.dst), run.vptr(op.dst, True),
+                                                run.vptr(op.src, True) if src_needs else None, acc,
+                                                ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")),
+                                                1, op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
             elif isinstance(op, Resize):
                 s, t = op.src, op.dst
                 acc = mark(s)
                 fn = lib.tde_resize_nearest_bwd if op.kind == "nearest" else lib.tde_resize_bilinear_bwd
-                _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s, True), s.buf.cs, s.coff, acc, t.H, t.W,
-                              run.vptr(t, True), t.buf.cs, t.coff, st), op.kind + " bwd")
+                with self._span("resize"):
+                    _lib.check(fn(N, s.H, s.W, s.C, run.vptr(s, True), s.buf.cs, s.coff, acc, t.H, t.W,
+                                  run.vptr(t, True), t.buf.cs, t.coff, st), op.kind + " bwd")
             elif isinstance(op, Copy):
                 s, t = op.src, op.dst
                 acc = mark(s)
@@ -414,3 +428,60 @@ class NetProgram:
 def ctypes_ref(d):
     import ctypes
     return ctypes.byref(d)
+
+
+class KernelTimer:
+    """HIP-event spans on the current stream, summed per kernel family (used by bench.py on an
+    instrumented eager step; never active inside a captured graph)."""
+
+    def __init__(self):
+        self.spans = []   # (family, start_event, end_event, flops)
+
+    def span(self, family, flops=0.0):
+        return _Span(self, family, flops)
+
+    def totals(self):
+        torch.cuda.synchronize()
+        out = {}
+        for fam, a, b, fl in self.spans:
+            t, f, n = out.get(fam, (0.0, 0.0, 0))
+            out[fam] = (t + a.elapsed_time(b), f + fl, n + 1)
+        return out   # family -> (ms, flops, launches)
+
+
+class _Span:
+    def __init__(self, timer, family, flops):
+        self.timer, self.family, self.flops = timer, family, flops
+
+    def __enter__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.b = torch.cuda.Event(enable_timing=True)
+        self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        self.b.record()
+        self.timer.spans.append((self.family, self.a, self.b, self.flops))
+        return False
+
+
+class _NoSpan:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+NO_SPAN = _NoSpan()
+
+
+def conv_flops(op, N):
+    """Algorithmic MACs*2 of one conv / deconv layer (all taps of the dense conv)."""
+    if isinstance(op, ConvBN):
+        if op.deconv:
+            return 2.0 * N * op.src.H * op.src.W * op.K * op.k * op.k * op.src.creal
+        return 2.0 * N * op.OH * op.OW * op.K * op.k * op.k * op.src.creal
+    if isinstance(op, Head):
+        return 2.0 * N * op.src.H * op.src.W * op.K * op.k * op.k * op.src.creal
+    return 0.0
