@@ -11,7 +11,14 @@ from oracle import losses as L
 from oracle import np_loops as NL
 from oracle import tf_ops as T
 
-torch.set_default_dtype(torch.float64)
+
+@pytest.fixture(autouse=True)
+def _float64_default():
+    """float64 default only inside this module's tests (never leak into other test modules)."""
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    yield
+    torch.set_default_dtype(old)
 
 
 def t(a):

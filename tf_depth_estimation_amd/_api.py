@@ -22,7 +22,7 @@ def get_program(net_scope, builder, H, W, cin, **kw):
         specs, bn = spec.param_specs()
         chunk = variables.get_store().get_or_create(prefix, specs, bn, variables.current_reuse())
         if not hasattr(chunk, "anchor"):
-            chunk.anchor = torch.zeros(1, device="cuda", requires_grad=True)
+            chunk.anchor = torch.zeros(1, device="cuda", dtype=torch.float32, requires_grad=True)
         prog = NetProgram(spec, chunk)
         _PROGRAMS[key] = prog
     return prog

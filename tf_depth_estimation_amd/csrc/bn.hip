@@ -16,11 +16,36 @@ RowSplit row_split(int M, int C) {
   RowSplit r;
   r.cq = C / 4;
   r.ty_n = r.cq >= 256 ? 1 : 256 / r.cq;
-  int target = 1024;
+  // <= 256 chunks (the finalize reads chunks x C partials), >= 4 rows per thread lane
+  const int target = 256;
   r.rows_per_chunk = (M + target - 1) / target;
-  if (r.rows_per_chunk < r.ty_n) r.rows_per_chunk = r.ty_n;
+  if (r.rows_per_chunk < 4 * r.ty_n) r.rows_per_chunk = 4 * r.ty_n;
+  r.rows_per_chunk = (r.rows_per_chunk + r.ty_n - 1) / r.ty_n * r.ty_n;
   r.chunks = (M + r.rows_per_chunk - 1) / r.rows_per_chunk;
   return r;
+}
+
+// Sum the per-chunk fp64 partials [chunks][2][C] for 64 channels per block: 4 waves split the
+// chunk range, one LDS combine.  Returns (in wave 0) the two totals for channel c.
+__device__ __forceinline__ bool reduce_chunks(int C, int chunks, const double* part, double& s0, double& s1,
+                                              int& c) {
+  __shared__ double sh[2][256];
+  const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
+  c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int k = w; k < chunks; k += 4) {
+      a += part[(long)k * 2 * C + c];
+      b += part[(long)k * 2 * C + C + c];
+    }
+  }
+  sh[0][threadIdx.x] = a;
+  sh[1][threadIdx.x] = b;
+  __syncthreads();
+  if (w != 0 || c >= C) return false;
+  s0 = sh[0][cl] + sh[0][cl + 64] + sh[0][cl + 128] + sh[0][cl + 192];
+  s1 = sh[1][cl] + sh[1][cl + 64] + sh[1][cl + 128] + sh[1][cl + 192];
+  return true;
 }
 
 // MODE 0: sums of z and z^2.  MODE 1 (backward): sums of g and g*xhat where g = dy * relu'(y).
@@ -89,10 +114,9 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(int M, int C, const flo
 
 __global__ void bn_stats_finalize_kernel(int M, int C, int chunks, const double* part, float eps, float decay,
                                          int bessel, float* mm, float* mv, float* save_mean, float* save_invstd) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0, ss = 0;
-  for (int k = 0; k < chunks; ++k) { s += part[(long)k * 2 * C + c]; ss += part[(long)k * 2 * C + C + c]; }
+  double s, ss;
+  int c;
+  if (!reduce_chunks(C, chunks, part, s, ss, c)) return;
   const double mean = s / M;
   double var = ss / M - mean * mean;
   if (var < 0) var = 0;
@@ -148,10 +172,9 @@ __global__ void __launch_bounds__(256) bn_infer_kernel(int M, int C, const float
 
 __global__ void bn_bwd_finalize_kernel(int M, int C, int chunks, const double* part, float* dbeta, int acc,
                                        float* coef /*[2][C]: mean(g), mean(g*xhat)*/) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0, sx = 0;
-  for (int k = 0; k < chunks; ++k) { s += part[(long)k * 2 * C + c]; sx += part[(long)k * 2 * C + C + c]; }
+  double s, sx;
+  int c;
+  if (!reduce_chunks(C, chunks, part, s, sx, c)) return;
   if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)s : (float)s;
   coef[c] = (float)(s / M);
   coef[C + c] = (float)(sx / M);
@@ -210,7 +233,7 @@ int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps,
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(rs.chunks), dim3(256), 0, st, M, C, z, nullptr, 0, 0, nullptr,
                      nullptr, nullptr, 0, rs.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, M, C, rs.chunks, part, eps,
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, M, C, rs.chunks, part, eps,
                      decay, bessel, moving_mean, moving_var, save_mean, save_invstd);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid((long)M * C / 4)), dim3(256), 0, st, M, C, z, save_mean,
                      save_invstd, beta, relu, y, y_cstride, y_coff);
@@ -239,7 +262,7 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
   float* coef = reinterpret_cast<float*>(part + (size_t)rs.chunks * 2 * C);
   hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(rs.chunks), dim3(256), 0, st, M, C, z, dy, dy_cstride, dy_coff,
                      save_mean, save_invstd, beta, relu, rs.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, M, C, rs.chunks, part, dbeta,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, M, C, rs.chunks, part, dbeta,
                      accumulate_dbeta, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((long)M * C / 4)), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                      dy_coff, save_mean, save_invstd, beta, coef, relu, dz);

@@ -387,7 +387,11 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
     splits = (int)((target + tiles - 1) / tiles);
     splits = splits > nkt / 8 ? nkt / 8 : splits;
     if (splits < 1) splits = 1;
-    if (splits > 64) splits = 64;
+    if (splits > 512) splits = 512;
+    // keep the fp32 partial slabs under 128 MB
+    long rows = mode == MODE_DGRAD ? (long)d.N * d.H * d.W : M;
+    long cols = mode == MODE_DGRAD ? d.C : Nn;
+    while (splits > 1 && (long)splits * rows * cols * 4 > (128l << 20)) splits /= 2;
   }
   pl.kt_per = tde_cdiv(nkt, splits);
   pl.splits = tde_cdiv(nkt, pl.kt_per);

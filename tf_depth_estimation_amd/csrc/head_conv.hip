@@ -100,50 +100,88 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const HeadArgs p) {
 // Per-chunk partial dW / db: part[chunk][e*KC + k] for e = (tap, c) in [0, KH*KW*wcin), then KC bias sums.
 constexpr int HW_PIX = 128;  // pixels per chunk (staged dz in LDS)
 
+// One block per pixel chunk (<= HW_CHUNKS chunks).  Threads = (entry e, pixel lane g): when the weight
+// has E < 256 entries, 256/E lanes split each staged sub-chunk's pixels and are combined through LDS.
+constexpr int HW_CHUNKS = 256;
+
 template <int KC>
-__global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs p, float* part) {
+__global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs p, float* part, int pix_per_chunk) {
   __shared__ float sdz[HW_PIX * KC];
-  __shared__ int spix[HW_PIX];
+  __shared__ float sred[256 * KC];
   const long M = (long)p.N * p.OH * p.OW;
-  const long p0 = (long)blockIdx.x * HW_PIX;
-  const int np = (int)min((long)HW_PIX, M - p0);
-  for (int t = threadIdx.x; t < HW_PIX * KC; t += blockDim.x) {
-    const int pi = t / KC, k = t - pi * KC;
-    float v = 0.f;
-    if (pi < np) {
-      const long o = (p0 + pi) * p.ycs + p.yco + k;
-      v = head_dz(p.yin[o], p.dy[o], p.act, p.scale, p.offset);
-    }
-    sdz[t] = v;
-  }
-  __syncthreads();
+  const long cbeg = (long)blockIdx.x * pix_per_chunk;
+  const long cend = min(M, cbeg + pix_per_chunk);
   const int E = p.KH * p.KW * p.wcin;
+  const int G = E >= 256 ? 1 : 256 / E;          // pixel lanes
+  const int lane = (int)threadIdx.x / (E >= 256 ? 256 : E);
+  const bool active = lane < G;
+  const int ohw = p.OH * p.OW;
+  // each thread owns entries e = e0, e0 + 256, ... (G == 1) or exactly one entry (G > 1)
+  const int e0 = E >= 256 ? (int)threadIdx.x : (int)threadIdx.x % E;
+  const int ne = E >= 256 ? (E - e0 + 255) / 256 : 1;
+  constexpr int MAXE = 8;                        // E <= 2048 entries
+  float acc[MAXE][KC];
+#pragma unroll
+  for (int j = 0; j < MAXE; ++j)
+#pragma unroll
+    for (int k = 0; k < KC; ++k) acc[j][k] = 0.f;
+  float bacc[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) bacc[k] = 0.f;
+  for (long p0 = cbeg; p0 < cend; p0 += HW_PIX) {
+    const int np = (int)min((long)HW_PIX, cend - p0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < HW_PIX * KC; t += blockDim.x) {
+      const int pi = t / KC, k = t - pi * KC;
+      float v = 0.f;
+      if (pi < np) {
+        const long o = (p0 + pi) * p.ycs + p.yco + k;
+        v = head_dz(p.yin[o], p.dy[o], p.act, p.scale, p.offset);
+      }
+      sdz[t] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < KC)
+      for (int pi = 0; pi < np; ++pi) bacc[threadIdx.x] += sdz[pi * KC + threadIdx.x];
+    if (!active) continue;
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+      if (j >= ne) break;
+      const int e = e0 + j * 256;
+      const int tap = e / p.wcin, c = e - tap * p.wcin, kh = tap / p.KW, kw = tap - kh * p.KW;
+      for (int pi = lane; pi < np; pi += G) {
+        const long pix = p0 + pi;
+        const int n = (int)(pix / ohw), r = (int)(pix - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
+        const int ih = oh * p.S - p.PT + kh, iw = ow * p.S - p.PL + kw;
+        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+          const float xv = p.x[((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + c];
+#pragma unroll
+          for (int k = 0; k < KC; ++k) acc[j][k] = fmaf(xv, sdz[pi * KC + k], acc[j][k]);
+        }
+      }
+    }
+  }
   const int stride_out = E * KC + KC;
   float* out = part + (long)blockIdx.x * stride_out;
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    const int tap = e / p.wcin, c = e - tap * p.wcin, kh = tap / p.KW, kw = tap - kh * p.KW;
-    float acc[KC];
+  if (G == 1) {
+    for (int j = 0; j < ne; ++j)
 #pragma unroll
-    for (int k = 0; k < KC; ++k) acc[k] = 0.f;
-    const int ohw = p.OH * p.OW;
-    int n = (int)(p0 / ohw), r = (int)(p0 - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
-    for (int pi = 0; pi < np; ++pi) {
-      const int ih = oh * p.S - p.PT + kh, iw = ow * p.S - p.PL + kw;
-      if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
-        const float xv = p.x[((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + c];
+      for (int k = 0; k < KC; ++k) out[(e0 + j * 256) * KC + k] = acc[j][k];
+  } else {
+    __syncthreads();
+    if (active)
 #pragma unroll
-        for (int k = 0; k < KC; ++k) acc[k] = fmaf(xv, sdz[pi * KC + k], acc[k]);
+      for (int k = 0; k < KC; ++k) sred[threadIdx.x * KC + k] = acc[0][k];
+    __syncthreads();
+    if ((int)threadIdx.x < E) {
+      for (int k = 0; k < KC; ++k) {
+        float s = 0.f;
+        for (int g = 0; g < G; ++g) s += sred[(g * E + threadIdx.x) * KC + k];
+        out[threadIdx.x * KC + k] = s;
       }
-      if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
     }
-#pragma unroll
-    for (int k = 0; k < KC; ++k) out[e * KC + k] = acc[k];
   }
-  if (threadIdx.x < KC) {
-    float s = 0.f;
-    for (int pi = 0; pi < np; ++pi) s += sdz[pi * KC + threadIdx.x];
-    out[E * KC + threadIdx.x] = s;
-  }
+  if (threadIdx.x < KC) out[E * KC + threadIdx.x] = bacc[threadIdx.x];
 }
 
 __global__ void __launch_bounds__(256) head_wgrad_reduce_kernel(const float* part, int chunks, int E, int KC,
@@ -155,6 +193,11 @@ __global__ void __launch_bounds__(256) head_wgrad_reduce_kernel(const float* par
   for (int ch = 0; ch < chunks; ++ch) s += part[(long)ch * total + i];
   float* dst = (i < E * KC) ? dw + i : db + (i - E * KC);
   *dst = accumulate ? *dst + (float)s : (float)s;
+}
+
+int head_chunks(long M) {
+  const long c = (M + HW_PIX - 1) / HW_PIX;
+  return (int)(c < HW_CHUNKS ? c : HW_CHUNKS);
 }
 
 bool head_desc_ok(const tde_conv_desc_t* d) {
@@ -192,7 +235,7 @@ extern "C" {
 size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
   const long M = (long)d->N * d->OH * d->OW;
-  const long chunks = (M + HW_PIX - 1) / HW_PIX;
+  const long chunks = head_chunks(M);
   return (size_t)chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
 }
 
@@ -226,8 +269,10 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
     if (ws_bytes < tde_head_workspace_size(d)) return TDE_ERR_WORKSPACE;
     float* part = static_cast<float*>(ws);
     const long M = (long)d->N * d->OH * d->OW;
-    const int chunks = (int)((M + HW_PIX - 1) / HW_PIX);
-    HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(chunks), a, part);
+    const int chunks = head_chunks(M);
+    const int ppc = (int)((M + chunks - 1) / chunks);
+    TDE_CHECK_ARG(d->KH * d->KW * d->w_cin <= 2048);
+    HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(chunks), a, part, ppc);
     const int E = d->KH * d->KW * d->w_cin;
     const int total = E * d->K + d->K;
     hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, chunks, E,

@@ -213,13 +213,13 @@ class NetRun:
         self.act = {}
         for b in prog.spec.bufs:
             shape = (N, b.H, b.W, b.cs)
-            self.act[b.name] = (torch.zeros(shape, device=device) if b.zero
-                                else torch.empty(shape, device=device))
+            self.act[b.name] = (torch.zeros(shape, device=device, dtype=torch.float32) if b.zero
+                                else torch.empty(shape, device=device, dtype=torch.float32))
         self.z, self.stats = {}, {}
         for i, op in enumerate(prog.spec.ops):
             if isinstance(op, ConvBN) and op.bn:
-                self.z[i] = torch.empty(op.zshape(N), device=device)
-                self.stats[i] = torch.empty((2, op.K), device=device)
+                self.z[i] = torch.empty(op.zshape(N), device=device, dtype=torch.float32)
+                self.stats[i] = torch.empty((2, op.K), device=device, dtype=torch.float32)
             elif isinstance(op, ConvBN):
                 self.z[i] = None
         self.grad = None
@@ -340,7 +340,7 @@ class NetProgram:
         st = _lib.stream_ptr()
         spec = self.spec
         if run.grad is None:
-            run.grad = {b.name: torch.empty((N, b.H, b.W, b.cs), device=run.device) for b in spec.bufs}
+            run.grad = {b.name: torch.empty((N, b.H, b.W, b.cs), device=run.device, dtype=torch.float32) for b in spec.bufs}
         written = {b.name: [] for b in spec.bufs}
 
         def mark(v):
@@ -357,7 +357,7 @@ class NetProgram:
         for v, g in zip(spec.outputs, grad_outputs):
             acc = mark(v)
             if g is None:
-                g = torch.empty((N, v.H, v.W, v.C), device=run.device)
+                g = torch.empty((N, v.H, v.W, v.C), device=run.device, dtype=torch.float32)
                 _lib.check(lib.tde_fill(g.numel(), ptr(g), 0.0, st), "zero grad_out")
             g = g.contiguous()
             _lib.check(lib.tde_copy_view(N * v.H * v.W, v.C, ptr(g), v.C, 0, run.vptr(v, True), v.buf.cs, v.coff,

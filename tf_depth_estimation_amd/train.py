@@ -20,7 +20,7 @@ class Adam:
 
     def __init__(self, chunk, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8):
         self.chunk, self.lr, self.b1, self.b2, self.eps = chunk, lr, beta1, beta2, eps
-        self.t = torch.zeros(1, device="cuda")
+        self.t = torch.zeros(1, device="cuda", dtype=torch.float32)
 
     def step(self):
         lib, st = _lib.load(), _lib.stream_ptr()
@@ -111,11 +111,11 @@ class DepthOnlyTrainer(Trainer):
         self.run = NetRun(self.prog, batch)
         self.opt = Adam(self.chunk, lr, beta1)
         dev = "cuda"
-        self.images = torch.zeros(batch, H, W, 3, device=dev)
-        self.label = torch.ones(batch, H, W, 1, device=dev)
-        self.label_pyr = [self.label] + [torch.empty(batch, H >> s, W >> s, 1, device=dev) for s in (1, 2, 3)]
+        self.images = torch.zeros(batch, H, W, 3, device=dev, dtype=torch.float32)
+        self.label = torch.ones(batch, H, W, 1, device=dev, dtype=torch.float32)
+        self.label_pyr = [self.label] + [torch.empty(batch, H >> s, W >> s, 1, device=dev, dtype=torch.float32) for s in (1, 2, 3)]
         outs = self.prog.spec.outputs
-        self.d_out = [torch.empty(batch, v.H, v.W, v.C, device=dev) for v in outs]
+        self.d_out = [torch.empty(batch, v.H, v.W, v.C, device=dev, dtype=torch.float32) for v in outs]
         self.loss = torch.zeros(1, dtype=torch.float64, device=dev)
         self.parts = torch.zeros(2, dtype=torch.float64, device=dev)   # [depth, smooth]
 
