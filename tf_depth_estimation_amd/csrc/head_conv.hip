@@ -102,12 +102,13 @@ constexpr int HW_PIX = 128;  // pixels per chunk (staged dz in LDS)
 
 // One block per pixel chunk (<= HW_CHUNKS chunks).  Threads = (entry e, pixel lane g): when the weight
 // has E < 256 entries, 256/E lanes split each staged sub-chunk's pixels and are combined through LDS.
-constexpr int HW_CHUNKS = 256;
+constexpr int HW_CHUNKS = 1024;
 
 template <int KC>
 __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs p, float* part, int pix_per_chunk) {
   __shared__ float sdz[HW_PIX * KC];
   __shared__ float sred[256 * KC];
+  __shared__ int3 spix[HW_PIX];
   const long M = (long)p.N * p.OH * p.OW;
   const long cbeg = (long)blockIdx.x * pix_per_chunk;
   const long cend = min(M, cbeg + pix_per_chunk);
@@ -140,6 +141,11 @@ __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs 
       }
       sdz[t] = v;
     }
+    for (int pi = threadIdx.x; pi < np; pi += blockDim.x) {   // pixel decode once per sub-chunk
+      const long pix = p0 + pi;
+      const int n = (int)(pix / ohw), r = (int)(pix - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
+      spix[pi] = make_int3(n * p.H, oh * p.S - p.PT, ow * p.S - p.PL);
+    }
     __syncthreads();
     if (threadIdx.x < KC)
       for (int pi = 0; pi < np; ++pi) bacc[threadIdx.x] += sdz[pi * KC + threadIdx.x];
@@ -150,11 +156,10 @@ __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs 
       const int e = e0 + j * 256;
       const int tap = e / p.wcin, c = e - tap * p.wcin, kh = tap / p.KW, kw = tap - kh * p.KW;
       for (int pi = lane; pi < np; pi += G) {
-        const long pix = p0 + pi;
-        const int n = (int)(pix / ohw), r = (int)(pix - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
-        const int ih = oh * p.S - p.PT + kh, iw = ow * p.S - p.PL + kw;
+        const int3 q = spix[pi];
+        const int ih = q.y + kh, iw = q.z + kw;
         if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
-          const float xv = p.x[((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + c];
+          const float xv = p.x[((long)(q.x + ih) * p.W + iw) * p.xcs + p.xco + c];
 #pragma unroll
           for (int k = 0; k < KC; ++k) acc[j][k] = fmaf(xv, sdz[pi * KC + k], acc[j][k]);
         }
@@ -164,9 +169,10 @@ __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs 
   const int stride_out = E * KC + KC;
   float* out = part + (long)blockIdx.x * stride_out;
   if (G == 1) {
-    for (int j = 0; j < ne; ++j)
+    if (active)
+      for (int j = 0; j < ne; ++j)
 #pragma unroll
-      for (int k = 0; k < KC; ++k) out[(e0 + j * 256) * KC + k] = acc[j][k];
+        for (int k = 0; k < KC; ++k) out[(e0 + j * 256) * KC + k] = acc[j][k];
   } else {
     __syncthreads();
     if (active)
@@ -184,13 +190,20 @@ __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs 
   if (threadIdx.x < KC) out[E * KC + threadIdx.x] = bacc[threadIdx.x];
 }
 
+// 64 outputs per block, 4 waves split the chunk range, fp64 combine through LDS.
 __global__ void __launch_bounds__(256) head_wgrad_reduce_kernel(const float* part, int chunks, int E, int KC,
                                                                  float* dw, float* db, int accumulate) {
+  __shared__ double sh[256];
   const int total = E * KC + KC;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
+  const int il = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + il;
   double s = 0.0;
-  for (int ch = 0; ch < chunks; ++ch) s += part[(long)ch * total + i];
+  if (i < total)
+    for (int ch = w; ch < chunks; ch += 4) s += part[(long)ch * total + i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  if (w != 0 || i >= total) return;
+  s = sh[il] + sh[il + 64] + sh[il + 128] + sh[il + 192];
   float* dst = (i < E * KC) ? dw + i : db + (i - E * KC);
   *dst = accumulate ? *dst + (float)s : (float)s;
 }
@@ -275,7 +288,7 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
     HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(chunks), a, part, ppc);
     const int E = d->KH * d->KW * d->w_cin;
     const int total = E * d->K + d->K;
-    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, chunks, E,
+    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, st, part, chunks, E,
                        d->K, dw, dbias, accumulate_dw);
   }
   return tde_launch_status();
