@@ -105,7 +105,7 @@ def main():
     x, lab = synthetic_batch(N, H, W, seed=rank)
     tr.set_batch(x.cuda(), lab.cuda())
     if world > 1:
-        tr.grad_sync = train.AllReduceGrads(tr.chunk, world)
+        tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
 
     # instrumented eager step: per-family HIP-event times for the roofline
     tr.step_eager()

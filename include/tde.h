@@ -145,6 +145,60 @@ int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, c
                 int nonfinite, float weight, double* loss, float* grad, int g_cstride, int g_coff,
                 void* stream);
 
+/* ---------------------------------------------------------------- projective warp loss head
+ * Fused forward + hand-derived backward of the per-scale self-supervised terms of
+ * train_depth_then_cam_lr.py:253-340 (config 4), train_optflow_combine.py:178-198 (config 3) and
+ * refine_depth.py:200-212 (config 5) over utils_lr.py:151-366 (pixel2cam, cam2pixel,
+ * projective_inverse_warp, bilinear_sampler) and :369-458 (consistent_depth_loss):
+ *   coords: (u,v,z) = cam2pixel(P @ pixel2cam(1/disp, Kinv))  or  grid + flow (optflow_warp, :258-274)
+ *   photo  : photo_w  * mean_{pix,3ch}(|bilinear(img_src,(u,v)) - img_tgt| * w_pix),
+ *            w_pix = softmax(logits)[1] (exp mask), wmask (data) or 1
+ *   exp    : exp_w    * mean_pix(CE(logits, [0,1]))               (compute_exp_reg_loss, :87-91)
+ *   consist: consist_w* mean_pix(|z - bilinear(1/disp_other,(u,v))| * softmax(logits)[1])
+ * loss[0..2] += (photo, exp, consist); gradients are ADDED into g_disp / g_flow / g_logits (same views
+ * as the inputs), scattered with float atomics into g_other, and reduced per batch element into
+ * g_P[b][12] = dL/dP (fp64, +=), from which tde_pose_grad chains to the 6-DoF pose vector. */
+typedef struct {
+  int B, H, W;
+  const float* disp; int disp_cs, disp_co;          /* projective mode: target disparity view */
+  const float* flow; int flow_cs, flow_co;          /* flow mode (disp == NULL) */
+  const float* P;                                    /* [B][12] rows 0..2 of K4 @ T */
+  const float* Kinv;                                 /* [B][9] */
+  const float* img_src;                              /* [B,H,W,3] dense, sampled */
+  const float* img_tgt;                              /* [B,H,W,3] dense */
+  const float* wmask;                                /* optional [B,H,W] photometric weight */
+  const float* logits; int logit_cs, logit_co;       /* optional 2-channel explainability logits */
+  const float* disp_other; int other_cs, other_co;   /* optional consistency source disparity */
+  float photo_w, exp_w, consist_w;
+  double* loss;                                      /* [3] */
+  float* g_disp; float* g_flow; float* g_logits; float* g_other;
+  double* g_P;                                       /* [B][12] or NULL (pose is data) */
+} tde_warp_loss_t;
+int tde_warp_loss(const tde_warp_loss_t* args, void* stream);
+
+/* Forward-only projective_inverse_warp (utils_lr.py:222-256) / bilinear_sampler (:276-366): coords from
+ * depth (or 1/disp when depth_is_disp) through P and Kinv, or given coords_in [B,H,W,2] when depth is
+ * NULL.  Any output may be NULL: out [B,H,W,C] (samples img [B,Hs,Ws,C]), coords [B,H,W,2],
+ * flow_x/flow_y = coords - grid (depth_optflow, :472-489), wmask [B,H,W], z [B,H,W]. */
+int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_disp, const float* P,
+                 const float* Kinv, const float* coords_in, const float* img, int Hs, int Ws, float* out,
+                 float* coords, float* flow_x, float* flow_y, float* wmask, float* z, void* stream);
+
+/* pose_vec2mat(vec,'angleaxis') (utils_lr.py:106-149; NaN at r = 0 as in the reference) or a given 4x4
+ * (format='matrix'), then P = (K4 @ T)[0:3] (:245-251) and Kinv = matrix_inverse(K) (:165).
+ * T may be NULL.  K is [B][9]. */
+int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const float* K, float* T,
+                  float* P, float* Kinv, void* stream);
+/* d loss / d pose_vec from gP [nscales][B][12] (each scale's K_s at K + b*k_stride_b + 9*s) plus an
+ * optional direct dL/dT [B][16]; Rodrigues backward. */
+int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, long k_stride_b,
+                  const double* gP, const float* gT_extra, float* g_pose_vec, int accumulate,
+                  void* stream);
+/* Config 4 cam loss (train_depth_then_cam_lr.py:278-286): w*mean((T_gt-T_lr)^2) +
+ * w*mean((inv(T_gt)-T_rl)^2); loss += value, gT_lr/gT_rl += gradients. */
+int tde_cam_loss(int B, const float* gt_vec, const float* T_lr, const float* T_rl, float weight,
+                 double* loss, float* gT_lr, float* gT_rl, void* stream);
+
 /* ---------------------------------------------------------------- optimizer
  * tf.train.AdamOptimizer (train_depth_then_cam_lr.py:413-417), TF epsilon-hat form, one launch over
  * a flat parameter buffer.  `step` is a device counter (incremented on device by tde_adam_step_begin)

@@ -25,7 +25,26 @@ class ConvDesc(ctypes.Structure):
 
 
 P = c_void_p
+
+
+class WarpLossArgs(ctypes.Structure):
+    """Mirror of tde_warp_loss_t (include/tde.h)."""
+    _fields_ = [("B", c_int), ("H", c_int), ("W", c_int),
+                ("disp", P), ("disp_cs", c_int), ("disp_co", c_int),
+                ("flow", P), ("flow_cs", c_int), ("flow_co", c_int),
+                ("P", P), ("Kinv", P), ("img_src", P), ("img_tgt", P), ("wmask", P),
+                ("logits", P), ("logit_cs", c_int), ("logit_co", c_int),
+                ("disp_other", P), ("other_cs", c_int), ("other_co", c_int),
+                ("photo_w", c_float), ("exp_w", c_float), ("consist_w", c_float),
+                ("loss", P), ("g_disp", P), ("g_flow", P), ("g_logits", P), ("g_other", P), ("g_P", P)]
+
+
 _SIGS = {
+    "tde_warp_loss": (c_int, [P, P]),
+    "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),
+    "tde_pose_prep": (c_int, [c_int, P, P, P, P, P, P, P]),
+    "tde_pose_grad": (c_int, [c_int, c_int, P, P, ctypes.c_long, P, P, P, c_int, P]),
+    "tde_cam_loss": (c_int, [c_int, P, P, P, c_float, P, P, P, P]),
     "tde_abi_version": (c_int, []),
     "tde_status_string": (ctypes.c_char_p, [c_int]),
     "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),

@@ -1,0 +1,86 @@
+"""Loss-head launch helpers (fused forward + gradient kernels of libtde.so).
+
+Every helper ADDS weight * term into a device fp64 accumulator and ADDS the term's gradient into the
+given gradient tensors, so a trainer zeroes its accumulators once per step and calls these in any
+order.  Reference loss code: train_depth_then_cam_lr.py:59-91,211-355, train_depth_only.py:162-219,
+train_optflow_combine.py:138-240, refine_depth.py:185-215.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import WarpLossArgs, ptr
+
+W_CONFIG2 = dict(smooth=1.0, depth=1.0)                                   # train_depth_only.py:33-37
+W_CONFIG3 = dict(smooth=0.5, data=0.5, optflow=1.0, depth=50.0)           # train_optflow_combine.py:33-37
+W_CONFIG4 = dict(smooth=1.0, data=10.0, depth=20.0, exp=1.0, cam=5.0)     # train_depth_then_cam_lr.py:44-51
+W_CONFIG5 = dict(smooth=2.0, data=0.2)                                    # refine_depth.py:34-36
+
+
+def dptr(t, idx=0):
+    """Pointer to element `idx` of an fp64 accumulator tensor."""
+    return ctypes.c_void_p(t.data_ptr() + 8 * idx)
+
+
+def vptr(t, coff=0):
+    """Pointer to channel `coff` of the first pixel of an NHWC tensor (channel views)."""
+    return ctypes.c_void_p(t.data_ptr() + 4 * coff)
+
+
+def zero(*ts):
+    lib, st = _lib.load(), _lib.stream_ptr()
+    for t in ts:
+        _lib.check(lib.tde_zero_bytes(t.numel() * t.element_size(), ptr(t), st), "zero")
+
+
+def smooth(pred, g, weight, acc, slot, recip=False, coff=0):
+    """compute_smooth_loss of channel `coff` of pred (or of 1/pred) (train_depth_then_cam_lr.py:59-68)."""
+    N, H, W, C = pred.shape
+    _lib.call("tde_loss_smooth2", N, H, W, ptr(pred), C, coff, int(recip), float(weight), dptr(acc, slot), ptr(g), C,
+              coff, _lib.stream_ptr())
+
+
+def l1(pred, label, g, weight, acc, slot, nonfinite=False, coff=0):
+    """mean|nf(label - pred[..., coff])| * weight; label dense [N,H,W] or [N,H,W,1]."""
+    N, H, W, C = pred.shape
+    _lib.call("tde_loss_l1", N, H, W, ptr(pred), C, coff, ptr(label), int(nonfinite), float(weight),
+              dptr(acc, slot), ptr(g), C, coff, _lib.stream_ptr())
+
+
+def area(src, dst):
+    N, H, W, C = src.shape
+    _lib.call("tde_resize_area_fwd", N, H, W, C, ptr(src), dst.shape[1], dst.shape[2], ptr(dst), _lib.stream_ptr())
+
+
+def warp_loss(acc, slot0, img_src, img_tgt, P=None, Kinv=None, disp=None, flow=None, wmask=None, logits=None,
+              disp_other=None, photo_w=0.0, exp_w=0.0, consist_w=0.0, g_disp=None, g_flow=None, g_logits=None,
+              g_other=None, g_P=None):
+    """One direction of the fused projective-warp loss head (include/tde.h tde_warp_loss).  All NHWC
+    tensors are dense; acc[slot0 .. slot0+2] += (photo, exp, consist)."""
+    B, H, W, _ = img_tgt.shape
+    a = WarpLossArgs()
+    a.B, a.H, a.W = B, H, W
+    if disp is not None:
+        a.disp, a.disp_cs, a.disp_co = ptr(disp), disp.shape[-1], 0
+    if flow is not None:
+        a.flow, a.flow_cs, a.flow_co = ptr(flow), flow.shape[-1], 0
+    a.P, a.Kinv = ptr(P), ptr(Kinv)
+    a.img_src, a.img_tgt, a.wmask = ptr(img_src), ptr(img_tgt), ptr(wmask)
+    if logits is not None:
+        a.logits, a.logit_cs, a.logit_co = ptr(logits), logits.shape[-1], 0
+    if disp_other is not None:
+        a.disp_other, a.other_cs, a.other_co = ptr(disp_other), disp_other.shape[-1], 0
+    a.photo_w, a.exp_w, a.consist_w = photo_w, exp_w, consist_w
+    a.loss = dptr(acc, slot0)
+    a.g_disp, a.g_flow, a.g_logits, a.g_other, a.g_P = ptr(g_disp), ptr(g_flow), ptr(g_logits), ptr(g_other), ptr(g_P)
+    _lib.call("tde_warp_loss", ctypes.byref(a), _lib.stream_ptr())
+
+
+def pose_prep(K, T=None, P=None, Kinv=None, vec=None, mat=None):
+    B = K.shape[0]
+    _lib.call("tde_pose_prep", B, ptr(vec), ptr(mat), ptr(K), ptr(T), ptr(P), ptr(Kinv), _lib.stream_ptr())
+
+
+def new(shape, dtype=torch.float32):
+    return torch.empty(shape, device="cuda", dtype=dtype)

@@ -108,6 +108,7 @@ class DepthOnlyTrainer(Trainer):
             self.prog = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
                                          offset=0.0)
         self.chunk = self.prog.chunk
+        self.chunks = [self.chunk]
         self.run = NetRun(self.prog, batch)
         self.opt = Adam(self.chunk, lr, beta1)
         dev = "cuda"
@@ -159,3 +160,304 @@ class DepthOnlyTrainer(Trainer):
 def ctypes_double_ptr(t, idx):
     import ctypes
     return ctypes.c_void_p(t.data_ptr() + 8 * idx)
+
+
+class MultiAdam:
+    def __init__(self, chunks, lr=2e-4, beta1=0.9):
+        self.opts = [Adam(c, lr, beta1) for c in chunks]
+
+    def step(self):
+        for o in self.opts:
+            o.step()
+
+
+class MultiAllReduce:
+    """One RCCL all-reduce per parameter chunk (flat, contiguous) + 1/world scale."""
+
+    def __init__(self, chunks, world):
+        self.parts = [AllReduceGrads(c, world) for c in chunks]
+
+    def __call__(self):
+        for p in self.parts:
+            p()
+
+
+def _scale_shapes(B, H, W, C, n=4):
+    return [(B, H >> s, W >> s, C) for s in range(n)]
+
+
+class DepthThenCamTrainer(Trainer):
+    """Config 4: `train_depth_then_cam_lr.py` (canonical interpretation):
+    single `disp_net` on each image (shared variables, separate BN batches, :123-136), 4-scale pair
+    `depth_net` (nets_optflow_depth_pairtest) on concat(L,R) and concat(R,L) (:142-154), and per scale
+    (:211-340): smoothness of 1/disp on the 4 maps, depth L1 with replace_nonfinite on the single left
+    net, explainability-masked photometric warp + exp CE + left-right depth consistency in both
+    directions, cam loss at s = 0; total (:355); Adam over both nets (:413-417)."""
+
+    SLOTS = dict(smooth=0, depth=1, photo=2, exp=3, consist=4, cam=5)
+
+    def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
+        from .losses import W_CONFIG4, new, zero
+        self.N, self.H, self.W = batch, H, W
+        self.w = weights or W_CONFIG4
+        with variables.variable_scope("model_singledepth"):
+            self.single = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
+                                           offset=0.0)
+        with variables.variable_scope("model_pairdepth"):
+            self.pair = _api.get_program("depth_cam_net", _netlib.depth_net_spec, H, W, 6, levels=4)
+        self.chunks = [self.single.chunk, self.pair.chunk]
+        self.opt = MultiAdam(self.chunks, lr, beta1)
+        B = batch
+        self.runs = {k: NetRun(p, B) for k, p in (("sl", self.single), ("sr", self.single), ("pl", self.pair),
+                                                   ("pr", self.pair))}
+        self.img = {"l": new((B, H, W, 3)), "r": new((B, H, W, 3))}
+        self.label = new((B, H, W, 1))
+        self.K = new((B, 4, 3, 3))
+        self.gt_cam = new((B, 6))
+        self.pair_in = {"lr": new((B, H, W, 6)), "rl": new((B, H, W, 6))}
+        self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
+        self.label_pyr = [self.label] + [new(s) for s in _scale_shapes(B, H, W, 1)[1:]]
+        self.Ks = [new((B, 9)) for _ in range(4)]
+        so, po = self.single.spec.outputs, self.pair.spec.outputs
+        self.d_out = {k: [new((B, v.H, v.W, v.C)) for v in (so if k[0] == "s" else po)] for k in self.runs}
+        self.pose = {"lr": new((B, 6)), "rl": new((B, 6))}
+        self.g_pose = {"lr": new((B, 6)), "rl": new((B, 6))}
+        self.T = {"lr": new((B, 16)), "rl": new((B, 16))}
+        self.gT = {"lr": new((B, 16)), "rl": new((B, 16))}
+        self.P = {d: [new((B, 12)) for _ in range(4)] for d in ("lr", "rl")}
+        self.Kinv = [new((B, 9)) for _ in range(4)]
+        self.gP = {d: new((4, B, 12), torch.float64) for d in ("lr", "rl")}
+        self.acc = new((8,), torch.float64)
+        self._zero = zero
+
+    def set_batch(self, img_l, img_r, label, K, gt_cam):
+        """img_* [B,H,W,3] in [-0.5,0.5]; label = inverse depth [B,H,W,1] (NaN holes allowed);
+        K [B,4,3,3] per-scale intrinsics (Demon_Data_loader.py:135-138); gt_cam [B,6] = (t, r)."""
+        self.img["l"].copy_(img_l)
+        self.img["r"].copy_(img_r)
+        self.label.copy_(label)
+        self.K.copy_(K)
+        self.gt_cam.copy_(gt_cam)
+        for s in range(4):
+            self.Ks[s].copy_(self.K[:, s].reshape(-1, 9))
+
+    def phase_update(self):
+        self.opt.step()
+
+    def phase_compute(self):
+        from . import losses as Ls
+        lib, st = _lib.load(), _lib.stream_ptr()
+        B, H, W, w = self.N, self.H, self.W, self.w
+        M = B * H * W
+        for c in self.chunks:
+            _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
+        self._zero(self.acc, self.gP["lr"], self.gP["rl"], self.gT["lr"], self.gT["rl"],
+                   *[g for v in self.d_out.values() for g in v])
+        # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
+        for key, (a, b) in (("lr", ("l", "r")), ("rl", ("r", "l"))):
+            dst = self.pair_in[key]
+            _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[a]), 3, 0, ptr(dst), 6, 0, 0, st), "concat")
+            _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[b]), 3, 0, ptr(dst), 6, 3, 0, st), "concat")
+        out = {"sl": self.single.forward(self.runs["sl"], self.img["l"]),
+               "sr": self.single.forward(self.runs["sr"], self.img["r"]),
+               "pl": self.pair.forward(self.runs["pl"], self.pair_in["lr"]),
+               "pr": self.pair.forward(self.runs["pr"], self.pair_in["rl"])}
+        # pose_final = reduce_mean(pose_pred, [1,2]) (nets_optflow_depth.py:183-186)
+        for run_key, d in (("pl", "lr"), ("pr", "rl")):
+            pp = out[run_key][4]
+            _lib.check(lib.tde_spatial_mean_fwd(B, pp.shape[1] * pp.shape[2], 6, ptr(pp), 6, ptr(self.pose[d]), st),
+                       "pose mean")
+        for s in range(1, 4):
+            Ls.area(self.img["l"], self.pyr["l"][s])
+            Ls.area(self.img["r"], self.pyr["r"][s])
+            Ls.area(self.label, self.label_pyr[s])
+        for s in range(4):
+            for d in ("lr", "rl"):
+                Ls.pose_prep(self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
+                             vec=self.pose[d])
+        S = self.SLOTS
+        _lib.check(lib.tde_cam_loss(B, ptr(self.gt_cam), ptr(self.T["lr"]), ptr(self.T["rl"]), w["cam"],
+                                    Ls.dptr(self.acc, S["cam"]), ptr(self.gT["lr"]), ptr(self.gT["rl"]), st), "cam")
+        for s in range(4):
+            for k in ("pl", "pr", "sl", "sr"):     # :216-225
+                Ls.smooth(out[k][s], self.d_out[k][s], w["smooth"] / 2 ** s, self.acc, S["smooth"], recip=True)
+            Ls.l1(out["sl"][s], self.label_pyr[s], self.d_out["sl"][s], w["depth"], self.acc, S["depth"],
+                  nonfinite=True)                 # :241-243
+            for tgt, src, run, oth, d in (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl")):
+                Ls.warp_loss(self.acc, S["photo"], self.pyr[src][s], self.pyr[tgt][s], P=self.P[d][s],
+                             Kinv=self.Kinv[s], disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s],
+                             photo_w=w["data"], exp_w=w["exp"], consist_w=w["depth"], g_disp=self.d_out[run][s],
+                             g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s])
+        # pose gradients -> pose_pred (spatial mean backward)
+        for run_key, d in (("pl", "lr"), ("pr", "rl")):
+            _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
+                                         ptr(self.g_pose[d]), 0, st), "pose grad")
+            gpp = self.d_out[run_key][4]
+            _lib.check(lib.tde_spatial_mean_bwd(B, gpp.shape[1] * gpp.shape[2], 6, ptr(gpp), 6, 0,
+                                                ptr(self.g_pose[d]), st), "pose mean bwd")
+        for k, prog in (("pr", self.pair), ("pl", self.pair), ("sr", self.single), ("sl", self.single)):
+            prog.backward(self.runs[k], self.d_out[k])
+
+    def loss_parts(self):
+        v = self.acc.cpu().tolist()
+        return {k: v[i] for k, i in self.SLOTS.items()}
+
+    def total_loss(self):
+        return float(sum(self.loss_parts().values()))
+
+
+class OptflowCombineTrainer(Trainer):
+    """Config 3: `train_optflow_combine.py` (canonical interpretation): joint
+    depth + flow `nets_depth.disp_net` on concat(L,R) (:97-109); per scale (:138-237) smoothness of disp,
+    flow-x, flow-y; depth L1; a ground-truth-depth warp giving wmask and the flow target (:169-176,205);
+    wmask-weighted photometric L1 of the predicted-depth warp (:178-188) and of the flow warp
+    (:191-198); flow L1 to depth_optflow (:205-210); pose is the given 4x4 tgt2src (format='matrix')."""
+
+    SLOTS = dict(smooth=0, depth=1, photo=2, optflow=5)
+
+    def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
+        from .losses import W_CONFIG3, new, zero
+        self.N, self.H, self.W = batch, H, W
+        self.w = weights or W_CONFIG3
+        with variables.variable_scope("model"):
+            self.prog = _api.get_program("depth_net", _netlib.depthflow_net_spec, H, W, 6)
+        self.chunks = [self.prog.chunk]
+        self.opt = MultiAdam(self.chunks, lr, beta1)
+        B = batch
+        self.run = NetRun(self.prog, B)
+        self.img = {"l": new((B, H, W, 3)), "r": new((B, H, W, 3))}
+        self.pair_in = new((B, H, W, 6))
+        self.label = new((B, H, W, 1))
+        self.K = new((B, 4, 3, 3))
+        self.tgt2src = new((B, 4, 4))
+        self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
+        self.label_pyr = [self.label] + [new(s) for s in _scale_shapes(B, H, W, 1)[1:]]
+        self.Ks = [new((B, 9)) for _ in range(4)]
+        self.P = [new((B, 12)) for _ in range(4)]
+        self.Kinv = [new((B, 9)) for _ in range(4)]
+        self.wmask = [new((B, H >> s, W >> s)) for s in range(4)]
+        self.gflow = [(new((B, H >> s, W >> s)), new((B, H >> s, W >> s))) for s in range(4)]
+        self.d_out = [new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
+        self.acc = new((8,), torch.float64)
+        self._zero = zero
+
+    def set_batch(self, img_l, img_r, label, K, tgt2src):
+        self.img["l"].copy_(img_l)
+        self.img["r"].copy_(img_r)
+        self.label.copy_(label)
+        self.K.copy_(K)
+        self.tgt2src.copy_(tgt2src)
+        for s in range(4):
+            self.Ks[s].copy_(self.K[:, s].reshape(-1, 9))
+
+    def phase_update(self):
+        self.opt.step()
+
+    def phase_compute(self):
+        from . import losses as Ls
+        lib, st = _lib.load(), _lib.stream_ptr()
+        B, H, W, w = self.N, self.H, self.W, self.w
+        M = B * H * W
+        c = self.prog.chunk
+        _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
+        self._zero(self.acc, *self.d_out)
+        _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["l"]), 3, 0, ptr(self.pair_in), 6, 0, 0, st), "concat")
+        _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["r"]), 3, 0, ptr(self.pair_in), 6, 3, 0, st), "concat")
+        out = self.prog.forward(self.run, self.pair_in)
+        for s in range(1, 4):
+            Ls.area(self.img["l"], self.pyr["l"][s])
+            Ls.area(self.img["r"], self.pyr["r"][s])
+            Ls.area(self.label, self.label_pyr[s])
+        S = self.SLOTS
+        for s in range(4):
+            disp, flow = out[s], out[4 + s]
+            gd, gf = self.d_out[s], self.d_out[4 + s]
+            ws = 1.0 / 2 ** s
+            Ls.smooth(disp, gd, w["smooth"] * ws, self.acc, S["smooth"])                  # :143-144
+            Ls.smooth(flow, gf, w["smooth"] * ws, self.acc, S["smooth"], coff=0)          # :147-148
+            Ls.smooth(flow, gf, w["smooth"] * ws, self.acc, S["smooth"], coff=1)          # :149-150
+            Ls.l1(disp, self.label_pyr[s], gd, w["depth"] * ws, self.acc, S["depth"])    # :163-164
+            Ls.pose_prep(self.Ks[s], P=self.P[s], Kinv=self.Kinv[s], mat=self.tgt2src)
+            h, wd = H >> s, W >> s
+            _lib.check(lib.tde_warp_fwd(B, h, wd, 3, ptr(self.label_pyr[s]), 1, ptr(self.P[s]), ptr(self.Kinv[s]),
+                                        None, None, 0, 0, None, None, ptr(self.gflow[s][0]), ptr(self.gflow[s][1]),
+                                        ptr(self.wmask[s]), None, st), "gt warp")      # :169-176
+            Ls.warp_loss(self.acc, S["photo"], self.pyr["r"][s], self.pyr["l"][s], P=self.P[s], Kinv=self.Kinv[s],
+                         disp=disp, wmask=self.wmask[s], photo_w=w["data"] * ws, g_disp=gd)   # :178-188
+            Ls.warp_loss(self.acc, S["photo"], self.pyr["r"][s], self.pyr["l"][s], flow=flow, wmask=self.wmask[s],
+                         photo_w=w["data"] * ws, g_flow=gf)                              # :191-198
+            Ls.l1(flow, self.gflow[s][0], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=0)   # :205-207
+            Ls.l1(flow, self.gflow[s][1], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=1)   # :209-210
+        self.prog.backward(self.run, self.d_out)
+
+    def total_loss(self):
+        return float(self.acc.sum().item())
+
+
+class RefineTrainer(Trainer):
+    """Config 5: `refine_depth.py` canonical interpretation: 1-channel sigmoid
+    disp_net at 640x480; per scale (:185-213) smoothness of disp, |src - warp(tgt, 1/disp, pose)| and a
+    depth L1 to the area-downsampled ground truth; fixed 4x4 pose, scale_factor = 1."""
+
+    SLOTS = dict(smooth=0, depth=1, photo=2)
+
+    def __init__(self, batch, H=480, W=640, lr=2e-5, beta1=0.9, weights=None):
+        from .losses import W_CONFIG5, new, zero
+        self.N, self.H, self.W = batch, H, W
+        self.w = weights or W_CONFIG5
+        with variables.variable_scope("model"):
+            self.prog = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
+                                         offset=0.0)
+        self.chunks = [self.prog.chunk]
+        self.opt = MultiAdam(self.chunks, lr, beta1)
+        B = batch
+        self.run = NetRun(self.prog, B)
+        self.x1, self.x2 = new((B, H, W, 3)), new((B, H, W, 3))
+        self.gt = new((B, H, W, 1))
+        self.K = new((B, 4, 3, 3))
+        self.pose = new((B, 4, 4))
+        self.pyr1 = [self.x1] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]]
+        self.pyr2 = [self.x2] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]]
+        self.gt_pyr = [self.gt] + [new(s) for s in _scale_shapes(B, H, W, 1)[1:]]
+        self.Ks = [new((B, 9)) for _ in range(4)]
+        self.P = [new((B, 12)) for _ in range(4)]
+        self.Kinv = [new((B, 9)) for _ in range(4)]
+        self.d_out = [new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
+        self.acc = new((4,), torch.float64)
+        self._zero = zero
+
+    def set_batch(self, x1, x2, gt_disp, K, pose4):
+        self.x1.copy_(x1)
+        self.x2.copy_(x2)
+        self.gt.copy_(gt_disp)
+        self.K.copy_(K)
+        self.pose.copy_(pose4)
+        for s in range(4):
+            self.Ks[s].copy_(self.K[:, s].reshape(-1, 9))
+
+    def phase_update(self):
+        self.opt.step()
+
+    def phase_compute(self):
+        from . import losses as Ls
+        lib, st = _lib.load(), _lib.stream_ptr()
+        c = self.prog.chunk
+        _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
+        self._zero(self.acc, *self.d_out)
+        out = self.prog.forward(self.run, self.x1)
+        for s in range(1, 4):
+            Ls.area(self.x1, self.pyr1[s])
+            Ls.area(self.x2, self.pyr2[s])
+            Ls.area(self.gt, self.gt_pyr[s])
+        S, w = self.SLOTS, self.w
+        for s in range(4):
+            disp, g = out[s], self.d_out[s]
+            Ls.smooth(disp, g, w["smooth"] / 2 ** s, self.acc, S["smooth"])                # :186-187
+            Ls.pose_prep(self.Ks[s], P=self.P[s], Kinv=self.Kinv[s], mat=self.pose)
+            Ls.warp_loss(self.acc, S["photo"], self.pyr2[s], self.pyr1[s], P=self.P[s], Kinv=self.Kinv[s],
+                         disp=disp, photo_w=1.0, g_disp=g)                                  # :200-212
+            Ls.l1(disp, self.gt_pyr[s], g, w["data"] / 2 ** s, self.acc, S["depth"])         # :210-213
+        self.prog.backward(self.run, self.d_out)
+
+    def total_loss(self):
+        return float(self.acc.sum().item())
