@@ -51,6 +51,19 @@ def check_grads(gpu, ref64, ref32):
         assert e_gpu <= max(GRAD_TOL, 4 * e_cpu32), f"{name}: gpu {e_gpu:.2e} vs cpu-fp32 {e_cpu32:.2e}"
 
 
+def check_grads_global(gpu, ref64, ref32):
+    """Whole-gradient criterion: relative L2 error of the concatenated gradient vector,
+    |g_gpu - g64| / |g64| <= max(GRAD_TOL, 4 * |g_cpu32 - g64| / |g64|)."""
+    names = sorted(ref64)
+    g = torch.cat([gpu[n].detach().double().cpu().reshape(-1) for n in names])
+    r = torch.cat([ref64[n].detach().double().cpu().reshape(-1) for n in names])
+    c = torch.cat([ref32[n].detach().double().cpu().reshape(-1) for n in names])
+    e_gpu = ((g - r).norm() / r.norm()).item()
+    e_cpu = ((c - r).norm() / r.norm()).item()
+    assert e_gpu <= max(GRAD_TOL, 4 * e_cpu), f"global grad: gpu {e_gpu:.2e} vs cpu-fp32 {e_cpu:.2e}"
+    return e_gpu, e_cpu
+
+
 def images(N, H, W, C, seed):
     g = np.random.default_rng(seed)
     return torch.tensor(g.uniform(-0.5, 0.5, size=(N, H, W, C)), dtype=torch.float32)
