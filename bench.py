@@ -1,22 +1,25 @@
 #!/usr/bin/env python3
 """Training-throughput benchmark (BASELINE.json metric: training image-pairs/sec at 256x192).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2] [--no-graph]
-                    [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config3|config4|config5]
+                    [--batch B] [--no-graph] [--no-cpu-baseline]
 For N > 1 launch with `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`:
 one process per GPU, per-GPU batch fixed (weak scaling), gradients averaged with one RCCL
-all-reduce of the flat gradient buffer per step.
+all-reduce per flat parameter chunk per step.
 
-A step = one pass of the hot path over one synthetic batch already resident in HBM: disp_net
-forward, fused loss head (value + gradient), backward, Adam (BASELINE config 2, train_depth_only.py,
-per-GPU batch 8 = configs[1]).  The step is recorded once into a hipGraph and replayed.
+A step = one pass of the hot path over one synthetic batch already resident in HBM: network
+forward(s), fused loss head (values + gradients), backward(s), Adam.  The default workload is
+BASELINE configs[1] (config 2, train_depth_only.py, per-GPU batch 8); config 4 (the 8-GPU DDP
+photometric config, per-GPU batch 8 = 64/8), config 3 (batch 32) and config 5 (640x480, per-GPU
+batch 2 = 16/8) are selectable.  The step is recorded once into a hipGraph and replayed.
 
-Prints ONE JSON line on rank 0 (contract in the task brief), with
-  roofline    : the MFMA implicit-GEMM conv family (fwd + dgrad + wgrad), algorithmic FLOPs of the
-                step's convs / their summed HIP-event time, measured live on an instrumented step,
-                against the fp32 MFMA dense peak (157.3 TFLOP/s, MI355X_MICROARCH.md);
+Prints ONE JSON line on rank 0 with
+  roofline    : the MFMA implicit-GEMM conv family (fwd + dgrad + wgrad): algorithmic FLOPs of the
+                step's convs / their summed HIP-event time, measured live on an instrumented step on
+                the stream the kernels run on, against the fp32 MFMA dense peak (157.3 TFLOP/s,
+                MI355X_MICROARCH.md);
   cpu_baseline: the oracle's PyTorch-CPU fp32 restatement of the same step ("port": TF-1 cannot
-                run here), timed on a bounded sample on this host's cores.
+                run here), timed on a bounded sample on this host's cores, rank 0 at N = 1 only.
 """
 import argparse
 import json
@@ -32,38 +35,136 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
-TRAIN_GFLOP_PER_IMAGE = 20.05        # disp_net train GFLOP/image at 256x192
+METRIC = "training image-pairs/sec at 256x192, 1/2/4/8 MI355X; depth L1 vs ref"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def synthetic_batch(N, H, W, seed):
-    """images U(-0.5,0.5), label disparity U(0.25,4)."""
-    g = np.random.default_rng(seed)
-    x = torch.tensor(g.uniform(-0.5, 0.5, (N, H, W, 3)), dtype=torch.float32)
-    lab = torch.tensor(g.uniform(0.25, 4.0, (N, H, W, 1)), dtype=torch.float32)
-    return x, lab
+# ---------------------------------------------------------------- synthetic inputs
+def texture(rng, B, H, W):
+    """Smooth random texture: sum of 8 random sinusoids + 0.02 N(0,1), clipped to +-0.5."""
+    yy, xx = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+    out = np.zeros((B, H, W, 3), np.float32)
+    for b in range(B):
+        for c in range(3):
+            for _ in range(8):
+                fx, fy = rng.uniform(0.02, 0.25, 2)
+                out[b, :, :, c] += rng.uniform(0.05, 0.15) * np.sin(fx * xx + fy * yy + rng.uniform(0, 6.28))
+    out += 0.02 * rng.standard_normal(out.shape).astype(np.float32)
+    return torch.from_numpy(np.clip(out, -0.5, 0.5))
 
 
-def cpu_baseline(N, H, W, budget_s=12.0):
-    """Oracle restatement (PyTorch-CPU fp32) of the same config-2 step, bounded sample."""
+def intrinsics(B, H, W):
+    """Normalized (fx,fy,cx,cy) = (0.89,1.19,0.5,0.5) x (W,H), per-scale / 2^s (Demon_Data_loader.py:25-39)."""
+    K = np.zeros((B, 4, 3, 3), np.float32)
+    for s in range(4):
+        f = 2.0 ** s
+        K[:, s] = [[0.89 * W / f, 0, 0.5 * W / f], [0, 1.19 * H / f, 0.5 * H / f], [0, 0, 1]]
+    return torch.from_numpy(K)
+
+
+def small_pose(rng, B):
+    t = rng.standard_normal((B, 3))
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    ax = rng.standard_normal((B, 3))
+    ax /= np.linalg.norm(ax, axis=1, keepdims=True)
+    return torch.tensor(np.concatenate([t, ax * rng.uniform(0.02, 0.2, (B, 1))], 1), dtype=torch.float32)
+
+
+def rodrigues_np(v):
+    """pose vector (t, angle-axis r) -> 4x4 (data prep for the configs whose pose is a given matrix)."""
+    T = np.tile(np.eye(4, dtype=np.float32), (v.shape[0], 1, 1))
+    for b, (tx, ty, tz, rx, ry, rz) in enumerate(v.numpy().astype(np.float64)):
+        th = np.sqrt(rx * rx + ry * ry + rz * rz)
+        a = np.array([rx, ry, rz]) / th
+        Kx = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        T[b, :3, :3] = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+        T[b, :3, 3] = [tx, ty, tz]
+    return torch.from_numpy(T)
+
+
+WORKLOADS = {
+    # name: (H, W, default per-GPU batch, train GFLOP per unit (SURVEY §8d), description)
+    "config2": (192, 256, 8, 20.05, "config2: train_depth_only.py path -- nets_optflow_depth.disp_net fwd + "
+                                    "smooth/depth-L1 loss head + bwd + Adam (BASELINE configs[1])"),
+    "config3": (192, 256, 32, 30.22, "config3: train_optflow_combine.py path -- nets_depth joint depth+flow net + "
+                                     "GT-warp wmask, depth/flow warps, flow L1, smooth + Adam"),
+    "config4": (192, 256, 8, 89.37, "config4: train_depth_then_cam_lr.py path -- 2x disp_net + 2x 4-scale "
+                                    "depth_net, photometric/exp/consistency/cam loss + Adam (per-GPU shard of 64)"),
+    "config5": (480, 640, 2, 125.9, "config5: refine_depth.py path -- disp_net at 640x480 + warp/depth/smooth "
+                                    "loss + Adam (per-GPU shard of 16)"),
+}
+
+
+def make_trainer(name, N):
+    from tf_depth_estimation_amd import train
+    H, W = WORKLOADS[name][:2]
+    cls = dict(config2=train.DepthOnlyTrainer, config3=train.OptflowCombineTrainer,
+               config4=train.DepthThenCamTrainer, config5=train.RefineTrainer)[name]
+    return cls(N, H, W)
+
+
+def make_batch(name, N, seed):
+    H, W = WORKLOADS[name][:2]
+    rng = np.random.default_rng(seed)
+    if name == "config2":
+        x = torch.tensor(rng.uniform(-0.5, 0.5, (N, H, W, 3)), dtype=torch.float32)
+        lab = torch.tensor(rng.uniform(0.25, 4.0, (N, H, W, 1)), dtype=torch.float32)
+        return (x, lab)
+    if name == "config3":
+        il, ir = texture(rng, N, H, W), texture(rng, N, H, W)
+        lab = torch.tensor(rng.uniform(0.25, 4.0, (N, H, W, 1)), dtype=torch.float32)
+        T = rodrigues_np(small_pose(rng, N) * torch.tensor([0.1, 0.1, 0.1, 1, 1, 1]))
+        return (il, ir, lab, intrinsics(N, H, W), T)
+    if name == "config4":
+        il, ir = texture(rng, N, H, W), texture(rng, N, H, W)
+        lab = rng.uniform(0.1, 2.0, (N, H, W, 1)).astype(np.float32)
+        lab[rng.uniform(size=lab.shape) < 0.05] = np.nan
+        return (il, ir, torch.from_numpy(lab), intrinsics(N, H, W), small_pose(rng, N))
+    x1, x2 = texture(rng, N, H, W), texture(rng, N, H, W)
+    gt = torch.tensor(rng.uniform(0.25, 4.0, (N, H, W, 1)), dtype=torch.float32)
+    T = rodrigues_np(small_pose(rng, N) * torch.tensor([0.1, 0.1, 0.1, 1, 1, 1]))
+    return (x1, x2, gt, intrinsics(N, H, W), T)
+
+
+# ---------------------------------------------------------------- CPU baseline (oracle restatement)
+def cpu_baseline(name, N, budget_s=12.0):
     from oracle import losses as OL
     from oracle import nets as ON
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    x, lab = synthetic_batch(N, H, W, 0)
-    P = ON.Params(dtype=torch.float32)
+    H, W = WORKLOADS[name][:2]
+    batch = make_batch(name, N, 0)
+    Ps = ON.Params(dtype=torch.float32)
+    Pp = ON.Params(dtype=torch.float32)
     opt = OL.AdamTF(lr=2e-4)
 
     def step():
-        for v in P.vars.values():
-            v.grad = None
-        ref = ON.disp_net(P, x, True, scope="model/depth_net")
-        loss, _ = OL.loss_depth_only(ref, lab)
+        for P in (Ps, Pp):
+            for v in P.vars.values():
+                v.grad = None
+        if name == "config2":
+            x, lab = batch
+            loss, _ = OL.loss_depth_only(ON.disp_net(Ps, x, True, scope="model/depth_net"), lab)
+        elif name == "config3":
+            il, ir, lab, K, T = batch
+            outs = ON.disp_net_depthflow(Ps, torch.cat([il, ir], -1), True, scope="model/depth_net")
+            loss, _ = OL.loss_optflow_combine(outs, il, ir, lab, K, T)
+        elif name == "config4":
+            il, ir, lab, K, gt = batch
+            dsl = ON.disp_net(Ps, il, True, scope="model_singledepth/depth_net")
+            dsr = ON.disp_net(Ps, ir, True, scope="model_singledepth/depth_net")
+            dpl, pr, ml = ON.depth_net(Pp, torch.cat([il, ir], -1), True, scope="model_pairdepth/depth_cam_net")
+            dpr, pl, mr = ON.depth_net(Pp, torch.cat([ir, il], -1), True, scope="model_pairdepth/depth_cam_net")
+            loss, _ = OL.loss_depth_then_cam_lr(dsl, dsr, dpl, dpr, pr, pl, ml, mr, il, ir, lab, K, gt)
+        else:
+            x1, x2, gt, K, T = batch
+            loss, _ = OL.loss_refine(ON.disp_net(Ps, x1, True, scope="model/depth_net"), x1, x2, gt, T, K)
         loss.backward()
-        opt.step(P.vars, {k: v.grad for k, v in P.vars.items()})
+        params = dict(Ps.vars, **Pp.vars)
+        opt.step(params, {k: v.grad for k, v in params.items()})
 
     step()  # warm-up (creates variables)
     n, t0 = 0, time.perf_counter()
@@ -74,8 +175,8 @@ def cpu_baseline(N, H, W, budget_s=12.0):
         if el >= budget_s or n >= 20:
             break
     return dict(value=round(N * n / el, 3), unit="image-pairs/s", cores=threads, kind="port",
-                sample=f"{n} config-2 training steps x {N} images at {W}x{H}, PyTorch-CPU fp32 restatement "
-                       f"(oracle/), {el:.1f}s")
+                sample=f"{n} {name} training steps x {N} samples at {W}x{H}, PyTorch-CPU fp32 restatement "
+                       f"(oracle/), {el:.1f}s wall")
 
 
 def main():
@@ -83,8 +184,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (config 4: 64 global / 8 GPUs)")
-    ap.add_argument("--workload", default="config2", choices=["config2"])
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -92,27 +193,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from tf_depth_estimation_amd import train
     from tf_depth_estimation_amd.program import KernelTimer
 
-    H, W, N = 192, 256, args.batch
-    tr = train.DepthOnlyTrainer(N, H, W)
-    x, lab = synthetic_batch(N, H, W, seed=rank)
-    tr.set_batch(x.cuda(), lab.cuda())
+    H, W, Nd, gflop_unit, desc = WORKLOADS[args.workload]
+    N = args.batch or Nd
+    tr = make_trainer(args.workload, N)
+    tr.set_batch(*[t.cuda() for t in make_batch(args.workload, N, seed=1000 + rank)])
     if world > 1:
         tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
+    progs = [p for p in (getattr(tr, "prog", None), getattr(tr, "single", None), getattr(tr, "pair", None)) if p]
 
-    # instrumented eager step: per-family HIP-event times for the roofline
+    # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
     tr.step_eager()
     timer = KernelTimer()
-    tr.prog.timer = timer
+    for p in progs:
+        p.timer = timer
     tr.step_eager()
-    tr.prog.timer = None
+    for p in progs:
+        p.timer = None
     fam = timer.totals()
     conv = [fam[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad") if k in fam]
     conv_ms = sum(c[0] for c in conv)
@@ -147,7 +250,7 @@ def main():
         value = world * N * args.steps / el
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         out = {
-            "metric": "training image-pairs/sec at 256x192, 1/2/4/8 MI355X; depth L1 vs ref",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "image-pairs/s",
             "n_gpus": world,
@@ -158,25 +261,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY.md §8d: images U(-0.5,0.5), label disparity U(0.25,4)); random-init "
-                    "Glorot weights",
-            "config": {"workload": "config2: train_depth_only.py path -- nets_optflow_depth.disp_net fwd + "
-                                   "smooth/depth-L1 loss head + bwd + Adam (configs[1])",
-                       "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
+            "data": "synthetic (SURVEY.md §8d shapes/distributions); random-init Glorot weights",
+            "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
-                       "unit_note": "config 2 trains on the left image of each loaded pair: 1 pair = 1 sample"},
+                       "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": "igemm_kernel (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)",
                          "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                          "flops_per_step": conv_flops, "conv_ms_per_step": round(conv_ms, 4),
                          "launches_per_step": conv_launches,
-                         "survey_flops_per_step": TRAIN_GFLOP_PER_IMAGE * 1e9 * N},
+                         "survey_flops_per_step": gflop_unit * 1e9 * N},
             "kernel_breakdown_ms": {k: round(v[0], 4) for k, v in sorted(fam.items())},
             "final_loss": loss,
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] timing CPU baseline ...")
-            out["cpu_baseline"] = cpu_baseline(N, H, W)
+            out["cpu_baseline"] = cpu_baseline(args.workload, N)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
