@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+BF16_MFMA_PEAK = 2500.0              # MI355X_MICROARCH.md: Peak BF16 MFMA, dense (~2.5 PF)
 METRIC = "training image-pairs/sec at 256x192, 1/2/4/8 MI355X; depth L1 vs ref"
 
 
@@ -187,6 +188,8 @@ def main():
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--math", default="fp32", choices=["fp32", "bf16x3"],
+                    help="conv arithmetic: exact fp32 MFMA, or bf16x3 split precision (include/tde.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -202,6 +205,8 @@ def main():
 
     H, W, Nd, gflop_unit, desc = WORKLOADS[args.workload]
     N = args.batch or Nd
+    from tf_depth_estimation_amd import _lib
+    _lib.check(_lib.load().tde_set_conv_math(1 if args.math == "bf16x3" else 0), "conv math")
     tr = make_trainer(args.workload, N)
     tr.set_batch(*[t.cuda() for t in make_batch(args.workload, N, seed=1000 + rank)])
     if world > 1:
@@ -247,6 +252,11 @@ def main():
     loss = tr.total_loss()
 
     if rank == 0:
+        if args.math == "bf16x3":
+            # 3 bf16 MFMAs per fp32 product: priced against the dense bf16 MFMA peak, FLOPs counted once
+            kernel_name, peak = "igemm3_kernel (conv fwd+dgrad+wgrad, bf16x3 on MFMA 16x16x32 bf16)", BF16_MFMA_PEAK
+        else:
+            kernel_name, peak = "igemm_kernel (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
         value = world * N * args.steps / el
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         out = {
@@ -265,9 +275,9 @@ def main():
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
-            "roofline": {"bound": "mfma", "kernel": "igemm_kernel (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)",
-                         "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
+                         "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
                          "flops_per_step": conv_flops, "conv_ms_per_step": round(conv_ms, 4),
                          "launches_per_step": conv_launches,
                          "survey_flops_per_step": gflop_unit * 1e9 * N},

@@ -60,6 +60,12 @@ const char* tde_status_string(int status);
  * slim.conv2d (no bias; the BN that follows owns the shift), nets_optflow_depth.py:88-101,107-142
  * -> TF Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter.
  * Requires C, K, cstrides and coffs to be multiples of 4 (16-byte vectors). */
+/* Process-wide conv arithmetic (set before graph capture; not per-stream):
+ *   0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32; bit-for-bit an fp32 fma chain), default;
+ *   1 = bf16x3: each fp32 operand split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi on
+ *       v_mfma_f32_16x16x32_bf16 with fp32 accumulation (~2^-16 relative per product, 5.3x rate). */
+int tde_set_conv_math(int mode);
+int tde_get_conv_math(void);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
 int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y,
                    int accumulate, void* ws, size_t ws_bytes, void* stream);

@@ -84,8 +84,19 @@ CONV_CASES = [
 ]
 
 
+@pytest.fixture(params=[0, 1], ids=["fp32", "bf16x3"])
+def conv_tol(request, L):
+    """Conv arithmetic mode (include/tde.h tde_set_conv_math) -> tolerance: exact fp32 MFMA 1e-5;
+    bf16x3 (~2^-16 per product, fp32 accumulation) 1e-4 relative-to-max."""
+    lib = L.load()
+    L.check(lib.tde_set_conv_math(request.param))
+    yield TOL if request.param == 0 else 1e-4
+    L.check(lib.tde_set_conv_math(0))
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_fwd_bwd(L, case):
+def test_conv2d_fwd_bwd(L, case, conv_tol):
+    tol = conv_tol
     N, H, W, cin, C, K, k, s, xcs, xco = case
     lib = L.load()
     st = L.stream_ptr()
@@ -103,7 +114,7 @@ def test_conv2d_fwd_bwd(L, case):
     xr = xfull[..., xco:xco + cin].clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = T.conv2d_same(xr, wr, s)
-    close(gy, yr, what="conv fwd")
+    close(gy, yr, tol=tol, what="conv fwd")
     dy = rnd(N, OH, OW, K, seed=3)
     yr.backward(dy)
     # bwd data with accumulate into a pre-filled view
@@ -113,13 +124,13 @@ def test_conv2d_fwd_bwd(L, case):
                                     ws.numel() * 4, st))
     exp = base.clone()
     exp[..., xco:xco + cin] += xr.grad
-    close(gdx[..., xco:xco + cin], exp[..., xco:xco + cin], what="conv dgrad")
+    close(gdx[..., xco:xco + cin], exp[..., xco:xco + cin], tol=tol, what="conv dgrad")
     close(gdx[..., :xco], base[..., :xco], what="dgrad untouched lo")
     close(gdx[..., xco + C:], base[..., xco + C:], what="dgrad untouched hi")
     gdw = torch.empty_like(gw)
     L.check(lib.tde_conv2d_bwd_filter(ctypes.byref(d), L.ptr(gx), L.ptr(dev(dy)), L.ptr(gdw), 0, L.ptr(ws),
                                       ws.numel() * 4, st))
-    close(gdw, wr.grad, what="conv wgrad")
+    close(gdw, wr.grad, tol=tol, what="conv wgrad")
 
 
 DECONV_CASES = [
@@ -133,7 +144,8 @@ DECONV_CASES = [
 
 
 @pytest.mark.parametrize("case", DECONV_CASES)
-def test_deconv2d_fwd_bwd(L, case):
+def test_deconv2d_fwd_bwd(L, case, conv_tol):
+    tol = conv_tol
     N, h, w_, cin, cout, k = case
     lib = L.load()
     st = L.stream_ptr()
@@ -150,17 +162,17 @@ def test_deconv2d_fwd_bwd(L, case):
                                  ws.numel() * 4, st))
     xr, wr = x.clone().requires_grad_(True), wt.clone().requires_grad_(True)
     yr = T.conv2d_transpose_same(xr, wr, 2)
-    close(gy, yr, what="deconv fwd")
+    close(gy, yr, tol=tol, what="deconv fwd")
     dy = rnd(N, H, W, cout, seed=7)
     yr.backward(dy)
     gdx = torch.empty(N, h, w_, cin, device="cuda")
     L.check(lib.tde_deconv2d_bwd_data(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(dev(wt)), L.ptr(gdx), 0, L.ptr(ws),
                                       ws.numel() * 4, st))
-    close(gdx, xr.grad, what="deconv dgrad")
+    close(gdx, xr.grad, tol=tol, what="deconv dgrad")
     gdw = torch.empty(k, k, cout, cin, device="cuda")
     L.check(lib.tde_deconv2d_bwd_filter(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(dev(x)), L.ptr(gdw), 0, L.ptr(ws),
                                         ws.numel() * 4, st))
-    close(gdw, wr.grad, what="deconv wgrad")
+    close(gdw, wr.grad, tol=tol, what="deconv wgrad")
 
 
 HEAD_CASES = [

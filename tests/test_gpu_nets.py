@@ -77,8 +77,17 @@ def fresh_store():
     yield
 
 
+@pytest.fixture(params=[0, 1], ids=["fp32", "bf16x3"])
+def conv_math(request):
+    from tf_depth_estimation_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.tde_set_conv_math(request.param))
+    yield request.param
+    _lib.check(lib.tde_set_conv_math(0))
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 64, 96), (1, 192, 256)])
-def test_disp_net_forward_parity(N, H, W):
+def test_disp_net_forward_parity(N, H, W, conv_math):
     from tf_depth_estimation_amd import nets_optflow_depth as nod
     from tf_depth_estimation_amd import variables
     x = images(N, H, W, 3, 0)
@@ -172,7 +181,7 @@ def test_autograd_api_gradients():
     check_grads(gpu, grads[torch.float64], grads[torch.float32])
 
 
-def test_config2_train_step_parity():
+def test_config2_train_step_parity(conv_math):
     """One full config-2 step (train_depth_only.py): loss, parameter gradients, Adam update."""
     from tf_depth_estimation_amd import train
     N, H, W = 2, 64, 96
@@ -191,7 +200,7 @@ def test_config2_train_step_parity():
         lr.backward()
         grads[dt] = {k: v.grad for k, v in P.vars.items()}
         if dt == torch.float64:
-            assert abs(tr.total_loss() - lr.item()) <= 1e-5 * abs(lr.item())
+            assert abs(tr.total_loss() - lr.item()) <= (1e-5 if conv_math == 0 else 1e-4) * abs(lr.item())
     check_grads({k: tr.chunk.grad_view(k) for k in p0}, grads[torch.float64], grads[torch.float32])
     # Adam: TF's first step is ~lr*sign(g), sign-sensitive where g ~ 0, so the update is checked
     # against the oracle optimizer applied to the GPU's own gradient buffer.

@@ -47,6 +47,8 @@ _SIGS = {
     "tde_cam_loss": (c_int, [c_int, P, P, P, c_float, P, P, P, P]),
     "tde_abi_version": (c_int, []),
     "tde_status_string": (ctypes.c_char_p, [c_int]),
+    "tde_set_conv_math": (c_int, [c_int]),
+    "tde_get_conv_math": (c_int, []),
     "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_deconv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),

@@ -320,6 +320,318 @@ __global__ void __launch_bounds__(NT) igemm_kernel(const ConvArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ bf16x3 split-precision variant
+// Same three gather modes, but each fp32 operand element x is split at staging time into
+// hi = bf16_rne(x), lo = bf16_rne(x - hi) and the product is formed by three
+// v_mfma_f32_16x16x32_bf16 (lo*hi + hi*lo + hi*hi, fp32 accumulate).  The dropped lo*lo term and the
+// two roundings leave ~2^-16 relative error per product (vs 2^-24 for fp32) at 16/3 = 5.3x the
+// fp32-MFMA rate.  LDS holds hi/lo planes as [row][BK=32 (+8 pad)] bf16; an operand whose 16-byte
+// global vectors run along rows is transposed in registers (4 rows x 4 k per thread).
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16;
+constexpr int BK3 = 32;
+constexpr int LDR = BK3 + 8;   // 80-byte rows: ds_read_b128 fragments hit distinct 16-B slots
+
+__device__ __forceinline__ unsigned bf16_rne_bits(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+__device__ __forceinline__ void split4(f4 v, uint2& hi, uint2& lo) {
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = bf16_rne_bits(v[j]);
+    l[j] = bf16_rne_bits(v[j] - __uint_as_float(h[j] << 16));
+  }
+  hi = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+  lo = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+}
+
+template <int ROWS>
+struct Img3 {
+  static constexpr int PLANE = ROWS * LDR;     // u16 elements per plane
+  static constexpr int SIZE = 2 * PLANE;       // hi + lo
+  __device__ static __forceinline__ void put(u16* s, int row, int k, f4 v) {
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(s + row * LDR + k) = hi;
+    *reinterpret_cast<uint2*>(s + PLANE + row * LDR + k) = lo;
+  }
+  __device__ static __forceinline__ bf8 hi(const u16* s, int row, int q) {
+    return *reinterpret_cast<const bf8*>(s + row * LDR + 8 * q);
+  }
+  __device__ static __forceinline__ bf8 lo(const u16* s, int row, int q) {
+    return *reinterpret_cast<const bf8*>(s + PLANE + row * LDR + 8 * q);
+  }
+};
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT) igemm3_kernel(const ConvArgs p) {
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
+  constexpr bool A_T = (MODE == MODE_WGRAD);   // A global vectors along rows -> register transpose
+  constexpr bool B_T = (MODE != MODE_DGRAD);   // B global vectors along rows (n) -> transpose
+  using IA = Img3<BM>;
+  using IB = Img3<BN>;
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * (IA::SIZE + IB::SIZE)];
+  u16* const As0 = smem;
+  u16* const Bs0 = smem + 2 * IA::SIZE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  int M, Nn, Kd;
+  DgClass g{};
+  int zsplit;
+  if constexpr (MODE == MODE_DGRAD) {
+    const int ncls = p.S * p.S;
+    const int cls = blockIdx.z % ncls;
+    zsplit = blockIdx.z / ncls;
+    g = dg_class(p, cls);
+    M = g.M; Nn = p.C; Kd = g.Kd;
+  } else if constexpr (MODE == MODE_FWD) {
+    zsplit = blockIdx.z;
+    M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
+  } else {
+    zsplit = blockIdx.z;
+    M = p.KH * p.KW * p.C; Nn = p.K; Kd = p.N * p.OH * p.OW;
+  }
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (m0 >= M || n0 >= Nn) return;
+  const int nkt = (Kd + BK3 - 1) / BK3;
+  const int kt0 = zsplit * p.kt_per;
+  const int kt1 = min(nkt, kt0 + p.kt_per);
+
+  // A slots: plain -> (row = s >> 3, kq = s & 7); transposed -> (rq = s % (BM/4), kq = s / (BM/4))
+  constexpr int A_SLOTS = A_T ? (BM / 4) * (BK3 / 4) : BM * (BK3 / 4);
+  constexpr int B_SLOTS = B_T ? (BN / 4) * (BK3 / 4) : BN * (BK3 / 4);
+  constexpr int A_PER = (A_SLOTS + NT - 1) / NT, B_PER = (B_SLOTS + NT - 1) / NT;
+  constexpr int A_V = A_T ? 4 : 1, B_V = B_T ? 4 : 1;   // f4 loads per slot
+  int a_i0[A_PER], a_i1[A_PER], a_i2[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int s = tid + i * NT;
+    a_ok[i] = false; a_i0[i] = a_i1[i] = a_i2[i] = 0;
+    if (s >= A_SLOTS) continue;
+    if constexpr (MODE == MODE_FWD) {
+      const int m = m0 + (s >> 3);
+      if (m < M) {
+        const int ohw = p.OH * p.OW;
+        const int n = m / ohw, r = m - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+        a_ok[i] = true; a_i0[i] = n; a_i1[i] = oh * p.S - p.PT; a_i2[i] = ow * p.S - p.PL;
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int m = m0 + (s >> 3);
+      if (m < M) {
+        const int hw = g.HH * g.WW;
+        const int n = m / hw, r = m - n * hw, ihh = r / g.WW, iww = r - ihh * g.WW;
+        a_ok[i] = true; a_i0[i] = n; a_i1[i] = ihh + g.dh; a_i2[i] = iww + g.dw;
+      }
+    } else {
+      const int m = m0 + 4 * (s % (BM / 4));
+      if (m < M) {
+        const int tap = m / p.C, c = m - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
+        a_ok[i] = true; a_i0[i] = c; a_i1[i] = kh - p.PT; a_i2[i] = kw - p.PL;
+      }
+    }
+  }
+
+  f4 ra[A_PER][A_V], rb[B_PER][B_V];
+
+  auto load_tiles = [&](int kt) {
+    const int kbase = kt * BK3;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int s = tid + i * NT;
+#pragma unroll
+      for (int j = 0; j < A_V; ++j) ra[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      if (s < A_SLOTS && a_ok[i]) {
+        if constexpr (MODE == MODE_FWD) {
+          const int k = kbase + 4 * (s & 7);
+          if (k < Kd) {
+            const int tap = k / p.C, c = k - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
+            const int ih = a_i1[i] + kh, iw = a_i2[i] + kw;
+            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+              ra[i][0] = ld4(p.x + ((long)(a_i0[i] * p.H + ih) * p.W + iw) * p.xcs + p.xco + c);
+          }
+        } else if constexpr (MODE == MODE_DGRAD) {
+          const int k = kbase + 4 * (s & 7);
+          if (k < Kd) {
+            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
+            const int oh = a_i1[i] - th, ow = a_i2[i] - tw;
+            if ((unsigned)oh < (unsigned)p.OH && (unsigned)ow < (unsigned)p.OW)
+              ra[i][0] = ld4(p.dy + ((long)(a_i0[i] * p.OH + oh) * p.OW + ow) * p.ycs + p.yco + co);
+          }
+        } else {
+          const int ohw = p.OH * p.OW;
+          const int pix0 = kbase + 4 * (s / (BM / 4));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int pix = pix0 + j;
+            if (pix < Kd) {
+              const int n = pix / ohw, r = pix - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+              const int ih = oh * p.S + a_i1[i], iw = ow * p.S + a_i2[i];
+              if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
+                ra[i][j] = ld4(p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + a_i0[i]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int s = tid + i * NT;
+#pragma unroll
+      for (int j = 0; j < B_V; ++j) rb[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+      if (s < B_SLOTS) {
+        if constexpr (MODE == MODE_FWD) {
+          const int n = n0 + 4 * (s % (BN / 4)), k0 = kbase + 4 * (s / (BN / 4));
+          if (n < Nn && k0 < Kd) {
+            const int tap = k0 / p.C, c0 = k0 - tap * p.C;   // k0..k0+3 share the tap (C % 4 == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (c0 + j < p.wcin) rb[i][j] = ld4(p.w + (long)(tap * p.wcin + c0 + j) * p.K + n);
+          }
+        } else if constexpr (MODE == MODE_DGRAD) {
+          const int ci = n0 + (s >> 3), k = kbase + 4 * (s & 7);
+          if (k < Kd && ci < p.wcin) {
+            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
+            const int kh = g.khs + p.S * th, kw = g.kws + p.S * tw;
+            rb[i][0] = ld4(p.w + ((long)(kh * p.KW + kw) * p.wcin + ci) * p.K + co);
+          }
+        } else {
+          const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
+          if (n < Nn) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (pix0 + j < Kd) rb[i][j] = ld4(p.dy + (long)(pix0 + j) * p.ycs + p.yco + n);
+          }
+        }
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    u16* A = As0 + buf * IA::SIZE;
+    u16* Bm = Bs0 + buf * IB::SIZE;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int s = tid + i * NT;
+      if (s >= A_SLOTS) continue;
+      if constexpr (A_T) {
+        const int r0 = 4 * (s % (BM / 4)), k0 = 4 * (s / (BM / 4));
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          IA::put(A, r0 + rr, k0, f4{ra[i][0][rr], ra[i][1][rr], ra[i][2][rr], ra[i][3][rr]});
+      } else {
+        IA::put(A, s >> 3, 4 * (s & 7), ra[i][0]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int s = tid + i * NT;
+      if (s >= B_SLOTS) continue;
+      if constexpr (B_T) {
+        const int r0 = 4 * (s % (BN / 4)), k0 = 4 * (s / (BN / 4));
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          IB::put(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
+      } else {
+        IB::put(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
+      }
+    }
+  };
+
+  f4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wrow0 = wm * TM * 16, wcol0 = wn * TN * 16;
+
+  if (kt0 < kt1) {
+    load_tiles(kt0);
+    store_tiles(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = (kt + 1 < kt1);
+      if (more) load_tiles(kt + 1);
+      const u16* A = As0 + cur * IA::SIZE;
+      const u16* Bm = Bs0 + cur * IB::SIZE;
+      bf8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+        al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+        bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
+      if (more) store_tiles(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---- epilogue (16x16 C/D map is dtype-independent on gfx950)
+  const bool direct = (p.splits == 1);
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wrow0 + a * 16 + 4 * q + r;
+      if (m >= M) continue;
+      long rowaddr;
+      bool rowok = true;
+      if constexpr (MODE == MODE_FWD) {
+        rowaddr = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const int hw = g.HH * g.WW;
+        const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
+        const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
+        rowaddr = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
+      } else {
+        if (direct) {
+          const int tap = m / p.C, c = m - tap * p.C;
+          rowok = c < p.wcin;
+          rowaddr = (long)(tap * p.wcin + c) * p.K;
+        } else {
+          rowaddr = ((long)zsplit * M + m) * Nn;
+        }
+      }
+      if (!rowok) continue;
+      float* base;
+      if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
+      else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
+      else base = direct ? p.dw : p.ws;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wcol0 + b * 16 + r16;
+        if (n < Nn) {
+          float* dst = base + rowaddr + n;
+          const float v = acc[a][b][r];
+          *dst = (direct && p.accumulate) ? (*dst + v) : v;
+        }
+      }
+    }
+  }
+}
+
 // Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col]
 template <int MODE>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols) {
@@ -368,7 +680,10 @@ static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, lon
   }
 }
 
+static int g_conv_math = 0;   // 0: exact fp32 MFMA, 1: bf16x3 (process-wide, see tde_set_conv_math)
+
 static Plan make_plan(const tde_conv_desc_t& d, int mode) {
+  const int BK = g_conv_math == 1 ? BK3 : ::BK;
   long M, Nn, Kd; int ncls;
   gemm_dims(d, mode, M, Nn, Kd, ncls);
   Plan pl{};
@@ -409,7 +724,8 @@ template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   constexpr int WN = BN >= 32 ? 2 : 1;
   constexpr int WM = 4 / WN;
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+  if (g_conv_math == 1) hipLaunchKernelGGL((igemm3_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
 }
 
 template <int MODE>
@@ -472,6 +788,14 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, void* ws, s
 }  // namespace
 
 extern "C" {
+
+int tde_set_conv_math(int mode) {
+  if (mode != 0 && mode != 1) return TDE_ERR_ARG;
+  g_conv_math = mode;
+  return TDE_OK;
+}
+
+int tde_get_conv_math(void) { return g_conv_math; }
 
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op) {
   if (!desc_ok(d) || op < 0 || op > 2) return 0;

@@ -288,6 +288,8 @@ class NetProgram:
         ws, _ = self._scratch(N)
         wsb = ws.numel() * 4
         for i, op in enumerate(spec.ops):
+            if self.timer is not None:
+                self.timer.tag = getattr(op, "layer", type(op).__name__)
             if isinstance(op, ConvBN):
                 d = op.desc(N)
                 w = self.P(f"{op.layer}/weights")
@@ -367,6 +369,8 @@ class NetProgram:
         iv = spec.input_view
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
+            if self.timer is not None:
+                self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
             if isinstance(op, ConvBN):
                 d = op.desc(N)
@@ -435,7 +439,8 @@ class KernelTimer:
     instrumented eager step; never active inside a captured graph)."""
 
     def __init__(self):
-        self.spans = []   # (family, start_event, end_event, flops)
+        self.spans = []   # (family, start_event, end_event, flops, tag)
+        self.tag = None   # set by the executor to the current layer name
 
     def span(self, family, flops=0.0):
         return _Span(self, family, flops)
@@ -443,10 +448,14 @@ class KernelTimer:
     def totals(self):
         torch.cuda.synchronize()
         out = {}
-        for fam, a, b, fl in self.spans:
+        for fam, a, b, fl, _ in self.spans:
             t, f, n = out.get(fam, (0.0, 0.0, 0))
             out[fam] = (t + a.elapsed_time(b), f + fl, n + 1)
         return out   # family -> (ms, flops, launches)
+
+    def by_tag(self):
+        torch.cuda.synchronize()
+        return [(fam, tag, a.elapsed_time(b), fl) for fam, a, b, fl, tag in self.spans]
 
 
 class _Span:
@@ -461,7 +470,7 @@ class _Span:
 
     def __exit__(self, *exc):
         self.b.record()
-        self.timer.spans.append((self.family, self.a, self.b, self.flops))
+        self.timer.spans.append((self.family, self.a, self.b, self.flops, self.timer.tag))
         return False
 
 
