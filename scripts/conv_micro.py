@@ -1,0 +1,84 @@
+"""Micro-benchmark of the implicit-GEMM conv kernels on fixed shapes (diagnostic).
+
+    python scripts/conv_micro.py [--math fp32|bf16x3|both] [--reps 20]
+For each shape and mode (fwd / dgrad / wgrad) prints the mean HIP-event time and TFLOP/s."""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from tf_depth_estimation_amd import _lib  # noqa: E402
+from tf_depth_estimation_amd.program import same_pad  # noqa: E402
+
+SHAPES = [
+    # name, N, H, W, C, K, k, s
+    ("gemm1x1_big", 8, 64, 64, 512, 512, 1, 1),
+    ("cnv1b", 8, 96, 128, 32, 32, 7, 1),
+    ("cnv2b", 8, 48, 64, 64, 64, 5, 1),
+    ("icnv4", 8, 24, 32, 256, 128, 3, 1),
+    ("icnv5", 8, 12, 16, 512, 256, 3, 1),
+    ("icnv6", 8, 6, 8, 1024, 512, 3, 1),
+    ("cnv4b", 8, 12, 16, 256, 256, 3, 1),
+    ("icnv1", 8, 192, 256, 20, 16, 3, 1),
+]
+
+
+def run(lib, name, N, H, W, C, K, k, s, reps):
+    OH, pt = same_pad(H, k, s)
+    OW, pl = same_pad(W, k, s)
+    d = _lib.ConvDesc(N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
+                      w_cin=C, x_cstride=C, x_coff=0, y_cstride=K, y_coff=0)
+    x = torch.randn(N, H, W, C, device="cuda")
+    w = torch.randn(k, k, C, K, device="cuda") * 0.1
+    y = torch.randn(N, OH, OW, K, device="cuda")
+    dx, dw = torch.empty_like(x), torch.empty_like(w)
+    wsz = max(lib.tde_conv2d_workspace_size(ctypes.byref(d), o) for o in range(3))
+    ws = torch.empty(wsz // 4 + 16, device="cuda")
+    st = _lib.stream_ptr()
+    flops = 2.0 * N * OH * OW * K * k * k * C
+    calls = {
+        "fwd": lambda: lib.tde_conv2d_fwd(ctypes.byref(d), _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), 0, _lib.ptr(ws),
+                                          ws.numel() * 4, st),
+        "dgrad": lambda: lib.tde_conv2d_bwd_data(ctypes.byref(d), _lib.ptr(y), _lib.ptr(w), _lib.ptr(dx), 0,
+                                                 _lib.ptr(ws), ws.numel() * 4, st),
+        "wgrad": lambda: lib.tde_conv2d_bwd_filter(ctypes.byref(d), _lib.ptr(x), _lib.ptr(y), _lib.ptr(dw), 0,
+                                                   _lib.ptr(ws), ws.numel() * 4, st),
+    }
+    out = []
+    for mode, fn in calls.items():
+        for _ in range(3):
+            _lib.check(fn(), mode)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / reps
+        out.append((mode, ms, flops / ms / 1e9))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--math", default="both")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    lib = _lib.load()
+    modes = {"fp32": [0], "bf16x3": [1], "both": [0, 1]}[a.math]
+    for m in modes:
+        _lib.check(lib.tde_set_conv_math(m))
+        print(f"== math {'fp32' if m == 0 else 'bf16x3'}")
+        for sh in SHAPES:
+            res = run(lib, *sh, a.reps)
+            print(f"{sh[0]:12s} " + "  ".join(f"{mode} {ms * 1e3:7.1f}us {tf:6.1f}TF" for mode, ms, tf in res),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

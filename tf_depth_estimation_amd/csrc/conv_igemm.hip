@@ -9,18 +9,20 @@
 //          stride-S problems split into S*S output-parity classes, each a dense stride-1 GEMM
 //          over only the taps that hit it (sub-pixel decomposition, no zero-insertion).
 //   WGRAD: C[m=(kh,kw,c)][k]      = sum_{pixels}     x(...) dy           (conv/deconv bwd-filter)
-// Tiles: BM x BN x 16 per 256-thread block (4 waves), each wave TM x TN 16x16 accumulators driven by
-// v_mfma_f32_16x16x4_f32 (exact f32: bit-for-bit an fma chain, so results match the fp32 oracle to
-// rounding).  Operands are register-staged into a double-buffered LDS image whose layout follows the
-// operand's natural 16-byte vector direction in HBM (m-major [row][k] or k-major [k][row]), so every
-// global load is a coalesced dwordx4 and every LDS store a ds_write_b128.  Split-K partials go to a
-// caller workspace and are reduced by a second kernel (deterministic; no float atomics).
+// Tiles: BM x BN x 32 per 256-thread block (4 waves), each wave TM x TN 16x16 accumulators.  Both
+// operands live m-major in a double-buffered LDS image ([row][k], padded rows); an operand whose
+// 16-byte global vectors run along rows (not k) is transposed in registers (4 rows x 4 k per thread),
+// so every global load is a coalesced dwordx4, every LDS store a ds_write_b128 (fp32) and every
+// fragment read a ds_read_b128 issued up front for the whole k-tile.  Two math modes:
+//   fp32   : 8 v_mfma_f32_16x16x4_f32 per tile pair (exact f32 products, fp32 accumulate);
+//   bf16x3 : 3 v_mfma_f32_16x16x32_bf16 per tile pair on a hi/lo split of each operand.
+// Split-K partials go to a caller workspace and are reduced by a second kernel (deterministic; no
+// float atomics).
 #include "tde_common.h"
 
 namespace {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
-constexpr int BK = 16;
 constexpr int NT = 256;
 
 struct ConvArgs {
@@ -54,271 +56,7 @@ __device__ __forceinline__ DgClass dg_class(const ConvArgs& p, int cls) {
   return g;
 }
 
-// LDS operand images. MMAJ: [rows][LDK] (k contiguous, read with one ds_read_b128 per fragment);
-// KMAJ: [BK][rows+4] (rows contiguous, 4 ds_read_b32 per fragment; conflict-free for 16-row groups).
-constexpr int LDK = BK + 4;
-
-template <int ROWS, bool KMAJ>
-struct LdsImg {
-  static constexpr int LD = KMAJ ? (ROWS + 4) : LDK;
-  static constexpr int SIZE = KMAJ ? BK * (ROWS + 4) : ROWS * LDK;
-  __device__ static __forceinline__ f4 frag(const float* s, int row, int q) {
-    if constexpr (KMAJ) {
-      f4 r;
-      r[0] = s[(4 * q + 0) * LD + row];
-      r[1] = s[(4 * q + 1) * LD + row];
-      r[2] = s[(4 * q + 2) * LD + row];
-      r[3] = s[(4 * q + 3) * LD + row];
-      return r;
-    } else {
-      return *reinterpret_cast<const f4*>(s + row * LDK + 4 * q);
-    }
-  }
-  // store 4 consecutive elements: along k (MMAJ, at [row][k..k+3]) or along rows (KMAJ, [k][row..row+3])
-  __device__ static __forceinline__ void put(float* s, int row, int k, f4 v) {
-    if constexpr (KMAJ) *reinterpret_cast<f4*>(s + k * LD + row) = v;
-    else *reinterpret_cast<f4*>(s + row * LDK + k) = v;
-  }
-};
-
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
-
-template <int MODE, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT) igemm_kernel(const ConvArgs p) {
-  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(TM >= 1 && TN >= 1, "tile");
-  // A/B LDS image orientation per mode (see header)
-  constexpr bool A_KMAJ = (MODE == MODE_WGRAD);
-  constexpr bool B_KMAJ = (MODE != MODE_DGRAD);
-  using IA = LdsImg<BM, A_KMAJ>;
-  using IB = LdsImg<BN, B_KMAJ>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::SIZE + IB::SIZE)];
-  float* const As0 = smem;
-  float* const Bs0 = smem + 2 * IA::SIZE;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
-
-  // ---- problem geometry for this block
-  int M, Nn, Kd;
-  DgClass g{};
-  int zsplit;
-  if constexpr (MODE == MODE_DGRAD) {
-    const int ncls = p.S * p.S;
-    const int cls = blockIdx.z % ncls;
-    zsplit = blockIdx.z / ncls;
-    g = dg_class(p, cls);
-    M = g.M; Nn = p.C; Kd = g.Kd;
-  } else if constexpr (MODE == MODE_FWD) {
-    zsplit = blockIdx.z;
-    M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
-  } else {
-    zsplit = blockIdx.z;
-    M = p.KH * p.KW * p.C; Nn = p.K; Kd = p.N * p.OH * p.OW;
-  }
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  if (m0 >= M || n0 >= Nn) return;
-  const int nkt = (Kd + BK - 1) / BK;
-  const int kt0 = zsplit * p.kt_per;
-  const int kt1 = min(nkt, kt0 + p.kt_per);
-
-  // ---- staging slot bookkeeping
-  // A slots: MMAJ -> (row = s>>2, kq = s&3); KMAJ -> (kk = s / (BM/4), rq = s % (BM/4))
-  constexpr int A_SLOTS = BM * BK / 4, B_SLOTS = BN * BK / 4;
-  constexpr int A_PER = (A_SLOTS + NT - 1) / NT, B_PER = (B_SLOTS + NT - 1) / NT;
-  int a_i0[A_PER], a_i1[A_PER], a_i2[A_PER];  // per-slot precomputed row geometry
-  bool a_ok[A_PER];
-#pragma unroll
-  for (int i = 0; i < A_PER; ++i) {
-    const int s = tid + i * NT;
-    a_ok[i] = false; a_i0[i] = a_i1[i] = a_i2[i] = 0;
-    if (s >= A_SLOTS) continue;
-    if constexpr (MODE == MODE_FWD) {
-      const int m = m0 + (s >> 2);
-      if (m < M) {
-        const int ohw = p.OH * p.OW;
-        const int n = m / ohw, r = m - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
-        a_ok[i] = true; a_i0[i] = n; a_i1[i] = oh * p.S - p.PT; a_i2[i] = ow * p.S - p.PL;
-      }
-    } else if constexpr (MODE == MODE_DGRAD) {
-      const int m = m0 + (s >> 2);
-      if (m < M) {
-        const int hw = g.HH * g.WW;
-        const int n = m / hw, r = m - n * hw, ihh = r / g.WW, iww = r - ihh * g.WW;
-        a_ok[i] = true; a_i0[i] = n; a_i1[i] = ihh + g.dh; a_i2[i] = iww + g.dw;
-      }
-    } else {
-      const int m = m0 + 4 * (s % (BM / 4));
-      if (m < M) {
-        const int tap = m / p.C, c = m - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
-        a_ok[i] = true; a_i0[i] = c; a_i1[i] = kh - p.PT; a_i2[i] = kw - p.PL;
-      }
-    }
-  }
-
-  f4 ra[A_PER], rb[B_PER];
-
-  auto load_tiles = [&](int kt) {
-    const int kbase = kt * BK;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int s = tid + i * NT;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (s < A_SLOTS && a_ok[i]) {
-        if constexpr (MODE == MODE_FWD) {
-          const int k = kbase + 4 * (s & 3);
-          if (k < Kd) {
-            const int tap = k / p.C, c = k - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
-            const int ih = a_i1[i] + kh, iw = a_i2[i] + kw;
-            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-              v = ld4(p.x + ((long)(a_i0[i] * p.H + ih) * p.W + iw) * p.xcs + p.xco + c);
-          }
-        } else if constexpr (MODE == MODE_DGRAD) {
-          const int k = kbase + 4 * (s & 3);
-          if (k < Kd) {
-            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
-            const int oh = a_i1[i] - th, ow = a_i2[i] - tw;
-            if ((unsigned)oh < (unsigned)p.OH && (unsigned)ow < (unsigned)p.OW)
-              v = ld4(p.dy + ((long)(a_i0[i] * p.OH + oh) * p.OW + ow) * p.ycs + p.yco + co);
-          }
-        } else {
-          const int pix = kbase + s / (BM / 4);
-          if (pix < Kd) {
-            const int ohw = p.OH * p.OW;
-            const int n = pix / ohw, r = pix - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
-            const int ih = oh * p.S + a_i1[i], iw = ow * p.S + a_i2[i];
-            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-              v = ld4(p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + a_i0[i]);
-          }
-        }
-      }
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int s = tid + i * NT;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (s < B_SLOTS) {
-        if constexpr (MODE == MODE_FWD) {
-          const int k = kbase + s / (BN / 4), n = n0 + 4 * (s % (BN / 4));
-          if (k < Kd && n < Nn) {
-            const int tap = k / p.C, c = k - tap * p.C;
-            if (c < p.wcin) v = ld4(p.w + (long)(tap * p.wcin + c) * p.K + n);
-          }
-        } else if constexpr (MODE == MODE_DGRAD) {
-          const int ci = n0 + (s >> 2), k = kbase + 4 * (s & 3);
-          if (k < Kd && ci < p.wcin) {
-            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
-            const int kh = g.khs + p.S * th, kw = g.kws + p.S * tw;
-            v = ld4(p.w + ((long)(kh * p.KW + kw) * p.wcin + ci) * p.K + co);
-          }
-        } else {
-          const int pix = kbase + s / (BN / 4), n = n0 + 4 * (s % (BN / 4));
-          if (pix < Kd && n < Nn) v = ld4(p.dy + (long)pix * p.ycs + p.yco + n);
-        }
-      }
-      rb[i] = v;
-    }
-  };
-
-  auto store_tiles = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int s = tid + i * NT;
-      if (s < A_SLOTS) {
-        if constexpr (A_KMAJ) IA::put(As0 + buf * IA::SIZE, 4 * (s % (BM / 4)), s / (BM / 4), ra[i]);
-        else IA::put(As0 + buf * IA::SIZE, s >> 2, 4 * (s & 3), ra[i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int s = tid + i * NT;
-      if (s < B_SLOTS) {
-        if constexpr (B_KMAJ) IB::put(Bs0 + buf * IB::SIZE, 4 * (s % (BN / 4)), s / (BN / 4), rb[i]);
-        else IB::put(Bs0 + buf * IB::SIZE, s >> 2, 4 * (s & 3), rb[i]);
-      }
-    }
-  };
-
-  f4 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-
-  const int r16 = lane & 15, q = lane >> 4;
-  const int wrow0 = wm * TM * 16, wcol0 = wn * TN * 16;
-
-  if (kt0 < kt1) {
-    load_tiles(kt0);
-    store_tiles(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = (kt + 1 < kt1);
-      if (more) load_tiles(kt + 1);
-      f4 fa[TM], fb[TN];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) fa[a] = IA::frag(As0 + cur * IA::SIZE, wrow0 + a * 16 + r16, q);
-#pragma unroll
-      for (int b = 0; b < TN; ++b) fb[b] = IB::frag(Bs0 + cur * IB::SIZE, wcol0 + b * 16 + r16, q);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][j], fb[b][j], acc[a][b], 0, 0, 0);
-      if (more) store_tiles(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  // ---- epilogue: C/D map of 16x16x4: col = lane&15, row = 4*(lane>>4) + reg
-  const bool direct = (p.splits == 1);
-#pragma unroll
-  for (int a = 0; a < TM; ++a) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wrow0 + a * 16 + 4 * q + r;
-      if (m >= M) continue;
-      long rowaddr;
-      bool rowok = true;
-      if constexpr (MODE == MODE_FWD) {
-        rowaddr = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
-      } else if constexpr (MODE == MODE_DGRAD) {
-        const int hw = g.HH * g.WW;
-        const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
-        const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
-        rowaddr = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
-      } else {
-        if (direct) {
-          const int tap = m / p.C, c = m - tap * p.C;
-          rowok = c < p.wcin;
-          rowaddr = (long)(tap * p.wcin + c) * p.K;
-        } else {
-          rowaddr = ((long)zsplit * M + m) * Nn;
-        }
-      }
-      if (!rowok) continue;
-      float* base;
-      if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
-      else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
-      else base = direct ? p.dw : p.ws;
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wcol0 + b * 16 + r16;
-        if (n < Nn) {
-          float* dst = base + rowaddr + n;
-          const float v = acc[a][b][r];
-          *dst = (direct && p.accumulate) ? (*dst + v) : v;
-        }
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------ bf16x3 split-precision variant
 // Same three gather modes, but each fp32 operand element x is split at staging time into
@@ -366,17 +104,42 @@ struct Img3 {
   }
 };
 
-template <int MODE, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT) igemm3_kernel(const ConvArgs p) {
+// fp32 image: [row][BK3 + 4] floats (144-byte rows: the 16 rows of a fragment read land on 16
+// distinct 16-B bank slots), read as f4 = the 4 k of one v_mfma_f32_16x16x4_f32 lane.
+constexpr int LDF = BK3 + 4;
+
+template <int ROWS>
+struct Img1 {
+  using T = float;
+  static constexpr int SIZE = ROWS * LDF;
+  __device__ static __forceinline__ void put(float* s, int row, int k, f4 v) {
+    *reinterpret_cast<f4*>(s + row * LDF + k) = v;
+  }
+  __device__ static __forceinline__ f4 frag(const float* s, int row, int k) {
+    return *reinterpret_cast<const f4*>(s + row * LDF + k);
+  }
+};
+
+template <int MATH, int ROWS>
+struct ImgSel;
+template <int ROWS>
+struct ImgSel<0, ROWS> { using type = Img1<ROWS>; using T = float; };
+template <int ROWS>
+struct ImgSel<1, ROWS> { using type = Img3<ROWS>; using T = u16; };
+
+// MATH 0: exact fp32 (2 x 4 v_mfma_f32_16x16x4_f32 per 32-deep k-tile); MATH 1: bf16x3.
+template <int MATH, int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
   constexpr bool A_T = (MODE == MODE_WGRAD);   // A global vectors along rows -> register transpose
   constexpr bool B_T = (MODE != MODE_DGRAD);   // B global vectors along rows (n) -> transpose
-  using IA = Img3<BM>;
-  using IB = Img3<BN>;
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * (IA::SIZE + IB::SIZE)];
-  u16* const As0 = smem;
-  u16* const Bs0 = smem + 2 * IA::SIZE;
+  using IA = typename ImgSel<MATH, BM>::type;
+  using IB = typename ImgSel<MATH, BN>::type;
+  using ET = typename ImgSel<MATH, BM>::T;
+  __shared__ __attribute__((aligned(16))) ET smem[2 * (IA::SIZE + IB::SIZE)];
+  ET* const As0 = smem;
+  ET* const Bs0 = smem + 2 * IA::SIZE;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
@@ -514,8 +277,8 @@ __global__ void __launch_bounds__(NT) igemm3_kernel(const ConvArgs p) {
   };
 
   auto store_tiles = [&](int buf) {
-    u16* A = As0 + buf * IA::SIZE;
-    u16* Bm = Bs0 + buf * IB::SIZE;
+    ET* A = As0 + buf * IA::SIZE;
+    ET* Bm = Bs0 + buf * IB::SIZE;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int s = tid + i * NT;
@@ -561,27 +324,48 @@ __global__ void __launch_bounds__(NT) igemm3_kernel(const ConvArgs p) {
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = (kt + 1 < kt1);
       if (more) load_tiles(kt + 1);
-      const u16* A = As0 + cur * IA::SIZE;
-      const u16* Bm = Bs0 + cur * IB::SIZE;
-      bf8 ah[TM], al[TM], bh[TN], bl[TN];
+      const ET* A = As0 + cur * IA::SIZE;
+      const ET* Bm = Bs0 + cur * IB::SIZE;
+      if constexpr (MATH == 1) {
+        bf8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
-        al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
-      }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
-        bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
-      }
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
+        for (int a = 0; a < TM; ++a) {
+          ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+          al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
+        }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+          bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
         }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      } else {
+        // lane (r16, q) holds k = 16*kc + 4*q + j of MFMA (kc, j): same permutation for A and B
+        f4 fa[2][TM], fb[2][TN];
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+#pragma unroll
+          for (int a = 0; a < TM; ++a) fa[kc][a] = IA::frag(A, wrow0 + a * 16 + r16, 16 * kc + 4 * q);
+#pragma unroll
+          for (int b = 0; b < TN; ++b) fb[kc][b] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 * kc + 4 * q);
+        }
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kc][a][j], fb[kc][b][j], acc[a][b], 0, 0, 0);
+      }
       if (more) store_tiles(cur ^ 1);
       __syncthreads();
       cur ^= 1;
@@ -683,7 +467,7 @@ static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, lon
 static int g_conv_math = 0;   // 0: exact fp32 MFMA, 1: bf16x3 (process-wide, see tde_set_conv_math)
 
 static Plan make_plan(const tde_conv_desc_t& d, int mode) {
-  const int BK = g_conv_math == 1 ? BK3 : ::BK;
+  const int BK = BK3;
   long M, Nn, Kd; int ncls;
   gemm_dims(d, mode, M, Nn, Kd, ncls);
   Plan pl{};
@@ -724,8 +508,8 @@ template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   constexpr int WN = BN >= 32 ? 2 : 1;
   constexpr int WM = 4 / WN;
-  if (g_conv_math == 1) hipLaunchKernelGGL((igemm3_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+  if (g_conv_math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
 }
 
 template <int MODE>
