@@ -191,6 +191,9 @@ def main():
     ap.add_argument("--math", default="fp32", choices=["fp32", "bf16x3"],
                     help="conv arithmetic: exact fp32 MFMA, or bf16x3 split precision (include/tde.h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
+                    help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,7 +213,10 @@ def main():
     tr = make_trainer(args.workload, N)
     tr.set_batch(*[t.cuda() for t in make_batch(args.workload, N, seed=1000 + rank)])
     if world > 1:
-        tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
+        if args.ddp == "overlap":
+            tr.enable_ddp(world, bucket_mb=args.bucket_mb)
+        else:
+            tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     progs = [p for p in (getattr(tr, "prog", None), getattr(tr, "single", None), getattr(tr, "pair", None)) if p]
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
@@ -254,9 +260,9 @@ def main():
     if rank == 0:
         if args.math == "bf16x3":
             # 3 bf16 MFMAs per fp32 product: priced against the dense bf16 MFMA peak, FLOPs counted once
-            kernel_name, peak = "igemm3_kernel (conv fwd+dgrad+wgrad, bf16x3 on MFMA 16x16x32 bf16)", BF16_MFMA_PEAK
+            kernel_name, peak = "igemmx_kernel<1,...> (conv fwd+dgrad+wgrad, bf16x3 on MFMA 16x16x32 bf16)", BF16_MFMA_PEAK
         else:
-            kernel_name, peak = "igemm_kernel (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
+            kernel_name, peak = "igemmx_kernel<0,...> (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
         value = world * N * args.steps / el
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         out = {
@@ -274,6 +280,7 @@ def main():
             "data": "synthetic (SURVEY.md §8d shapes/distributions); random-init Glorot weights",
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
+                       "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",

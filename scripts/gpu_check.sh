@@ -7,6 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r01}
 STEPS=${STEPS:-50}
+WL=${WL:-config2}
 
 ok_or_stop() {  # rc 0 (pass) and 1 (test failures) keep going; anything else is a fault/timeout
   local rc=$1 what=$2
@@ -15,18 +16,22 @@ ok_or_stop() {  # rc 0 (pass) and 1 (test failures) keep going; anything else is
 }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 700 python -m pytest tests -q -m gpu ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
   ok_or_stop $? "pytest -m gpu"
-  tail -3 gpurun_out/gpu_tests.log
+  grep -E "passed|failed|FAILED|ERROR" gpurun_out/gpu_tests.log | tail -20
 fi
 
-timeout -k 10 400 python bench.py --steps "$STEPS" --warmup 10 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
-ok_or_stop $? "bench"
-cat gpurun_out/bench_$TAG.json
+if [ "${SKIP_BENCH:-0}" != "1" ]; then
+  timeout -k 10 400 python bench.py --workload "$WL" --steps "$STEPS" --warmup 10 ${BENCH_ARGS:-} \
+    > gpurun_out/bench_${TAG}_$WL.json 2> gpurun_out/bench_${TAG}_$WL.err
+  ok_or_stop $? "bench"
+  cat gpurun_out/bench_${TAG}_$WL.json
+fi
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof_$TAG" -o run --output-format csv \
-    -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof_${TAG}_$WL" -o run --output-format csv \
+    -- python3 bench.py --workload "$WL" --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} \
+    > gpurun_out/prof_${TAG}_$WL.log 2>&1
   ok_or_stop $? "rocprofv3"
-  find gpurun_out/prof_$TAG -name "*stats*" | head
+  find gpurun_out/prof_${TAG}_$WL -name "*stats*"
 fi

@@ -81,6 +81,9 @@ CONV_CASES = [
     (2, 2, 2, 512, 512, 512, 3, 1, 1024, 512),
     (1, 9, 11, 129, 132, 64, 3, 1, 132, 0),
     (3, 3, 4, 512, 512, 256, 3, 2, 512, 0),
+    (2, 8, 12, 258, 260, 128, 3, 1, 260, 0),        # nets_depth icnv4_opt at 64x96 (padded concat)
+    (8, 48, 64, 30, 32, 32, 3, 1, 36, 4),           # split-K wgrad over 24576 pixels, w_cin < C, offset view
+    (4, 24, 32, 256, 256, 128, 3, 1, 384, 128),     # split-K fwd/dgrad (Kd = 2304), offset view
 ]
 
 

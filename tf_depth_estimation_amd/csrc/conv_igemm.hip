@@ -479,12 +479,12 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
   const int nkt = tde_cdiv(Kd, BK);
-  // split K until ~2 blocks per CU, keeping >= 8 k-tiles per split
+  // split K until ~2 blocks per CU, keeping >= 4 k-tiles (128 reduction elements) per split
   int splits = 1;
   const long target = 512;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
-    splits = splits > nkt / 8 ? nkt / 8 : splits;
+    splits = splits > nkt / 4 ? nkt / 4 : splits;
     if (splits < 1) splits = 1;
     if (splits > 512) splits = 512;
     // keep the fp32 partial slabs under 128 MB

@@ -334,9 +334,11 @@ class NetProgram:
         return [run.view_tensor(v) for v in spec.outputs]
 
     # ---------------------------------------------------------------- backward
-    def backward(self, run, grad_outputs, need_input_grad=False):
+    def backward(self, run, grad_outputs, need_input_grad=False, on_grads=None):
         """grad_outputs: list (aligned with spec.outputs) of tensors or None.  Accumulates parameter
-        gradients into chunk.grad.  Returns d(input) if requested."""
+        gradients into chunk.grad.  Returns d(input) if requested.  on_grads(names), if given, is
+        called after each op with the full variable names whose gradient that op just wrote (the
+        data-parallel exchange launches a bucket once all its parameters are final, ddp.py)."""
         N = run.N
         lib = _lib.load()
         st = _lib.stream_ptr()
@@ -403,6 +405,8 @@ class NetProgram:
                         with self._span("conv_dgrad", fl):
                             _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
                                                                acc, ptr(ws), wsb, st), op.layer + " dgrad")
+                if on_grads is not None:
+                    on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Head):
                 d = op.desc(N)
                 acc = mark(op.src) if src_needs else 0
@@ -412,6 +416,8 @@ class NetProgram:
                                                 run.vptr(op.src, True) if src_needs else None, acc,
                                                 ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")),
                                                 1, op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
+                if on_grads is not None:
+                    on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Resize):
                 s, t = op.src, op.dst
                 acc = mark(s)

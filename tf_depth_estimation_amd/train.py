@@ -49,16 +49,34 @@ class AllReduceGrads:
 class Trainer:
     """Common capture/replay machinery.  A step is phase_compute (zero grads, fwd, loss, bwd),
     the optional gradient exchange, then phase_update (Adam).  Without an exchange the whole step is
-    one hipGraph; with one, compute and update are two graphs and the RCCL all-reduce runs between
-    their replays on the same stream."""
+    one hipGraph.  With a ddp.GradSync, backward reports finished parameters and each full bucket's
+    RCCL all-reduce is launched on a side stream while backward continues; under capture, every
+    launch point closes a graph segment, and replay interleaves segments with the bucket launches
+    (RCCL itself is never captured), then one graph for Adam after the comm stream joins."""
 
     graphs = None
+    segments = None          # [(graph, buckets launched after it)] when capturing with a GradSync
     grad_sync = None
+    BACKWARD_USES = 1        # backward calls per chunk per step (shared-variable nets call it twice)
+
+    def enable_ddp(self, world, bucket_mb=32.0, group=None):
+        from .ddp import GradSync
+        uses = {id(c): self.BACKWARD_USES for c in self.chunks}
+        self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
+        return self.grad_sync
+
+    def hook(self, chunk):
+        """on_grads callback for NetProgram.backward (None without an overlapped exchange)."""
+        gs = self.grad_sync
+        return gs.hook(chunk) if gs is not None and hasattr(gs, "hook") else None
 
     def step_eager(self):
+        gs = self.grad_sync
+        if gs is not None and hasattr(gs, "begin_step"):
+            gs.begin_step()
         self.phase_compute()
-        if self.grad_sync is not None:
-            self.grad_sync()
+        if gs is not None:
+            gs()
         self.phase_update()
 
     def capture(self, warmup=2):
@@ -69,24 +87,68 @@ class Trainer:
             for _ in range(warmup):
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(s)
-        if self.grad_sync is None:
+        gs = self.grad_sync
+        if gs is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.phase_compute()
                 self.phase_update()
             self.graphs = [g]
-        else:
+            return self.graphs
+        if not hasattr(gs, "begin_step"):       # plain exchange after backward
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self.phase_compute()
             with torch.cuda.graph(g2):
                 self.phase_update()
             self.graphs = [g1, g2]
+            return self.graphs
+        # segmented capture: graph boundaries at bucket launch points
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        cs = torch.cuda.Stream()
+        segs = []
+        state = {"g": torch.cuda.CUDAGraph()}
+
+        def cut(buckets):
+            state["g"].capture_end()
+            segs.append((state["g"], list(buckets)))
+            state["g"] = torch.cuda.CUDAGraph()
+            state["g"].capture_begin(pool=pool)
+
+        gs.begin_step()
+        gs.capturing = cut
+        try:
+            with torch.cuda.stream(cs):
+                state["g"].capture_begin(pool=pool)
+                self.phase_compute()
+                state["g"].capture_end()
+                segs.append((state["g"], gs.leftovers()))
+                upd = torch.cuda.CUDAGraph()
+                upd.capture_begin(pool=pool)
+                self.phase_update()
+                upd.capture_end()
+        finally:
+            gs.capturing = None
+        torch.cuda.synchronize()
+        self.segments = segs
+        self.graphs = [g for g, _ in segs] + [upd]
         return self.graphs
 
     def step(self):
         if self.graphs is None:
             self.step_eager()
+        elif self.segments is not None:
+            gs = self.grad_sync
+            gs.begin_step()
+            for g, buckets in self.segments:
+                g.replay()
+                if buckets:
+                    for b in buckets:
+                        b.launched = True
+                    gs.launch(buckets)
+            gs.finish()
+            self.graphs[-1].replay()
         elif len(self.graphs) == 1:
             self.graphs[0].replay()
         else:
@@ -148,7 +210,7 @@ class DepthOnlyTrainer(Trainer):
                                             1, 0, st), "smooth")
             _lib.check(lib.tde_loss_l1(N, h, w, ptr(pred), 1, 0, ptr(self.label_pyr[s]), 0, self.w["depth"] / 2 ** s,
                                        p_depth, ptr(g), 1, 0, st), "depth l1")
-        self.prog.backward(self.run, self.d_out)
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
 
     def total_loss(self):
         return float(self.parts.sum().item())
@@ -195,6 +257,7 @@ class DepthThenCamTrainer(Trainer):
     directions, cam loss at s = 0; total (:355); Adam over both nets (:413-417)."""
 
     SLOTS = dict(smooth=0, depth=1, photo=2, exp=3, consist=4, cam=5)
+    BACKWARD_USES = 2        # each net runs on both images (shared variables)
 
     def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
         from .losses import W_CONFIG4, new, zero
@@ -296,7 +359,7 @@ class DepthThenCamTrainer(Trainer):
             _lib.check(lib.tde_spatial_mean_bwd(B, gpp.shape[1] * gpp.shape[2], 6, ptr(gpp), 6, 0,
                                                 ptr(self.g_pose[d]), st), "pose mean bwd")
         for k, prog in (("pr", self.pair), ("pl", self.pair), ("sr", self.single), ("sl", self.single)):
-            prog.backward(self.runs[k], self.d_out[k])
+            prog.backward(self.runs[k], self.d_out[k], on_grads=self.hook(prog.chunk))
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
@@ -388,7 +451,7 @@ class OptflowCombineTrainer(Trainer):
                          photo_w=w["data"] * ws, g_flow=gf)                              # :191-198
             Ls.l1(flow, self.gflow[s][0], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=0)   # :205-207
             Ls.l1(flow, self.gflow[s][1], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=1)   # :209-210
-        self.prog.backward(self.run, self.d_out)
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
 
     def total_loss(self):
         return float(self.acc.sum().item())
@@ -457,7 +520,7 @@ class RefineTrainer(Trainer):
             Ls.warp_loss(self.acc, S["photo"], self.pyr2[s], self.pyr1[s], P=self.P[s], Kinv=self.Kinv[s],
                          disp=disp, photo_w=1.0, g_disp=g)                                  # :200-212
             Ls.l1(disp, self.gt_pyr[s], g, w["data"] / 2 ** s, self.acc, S["depth"])         # :210-213
-        self.prog.backward(self.run, self.d_out)
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
 
     def total_loss(self):
         return float(self.acc.sum().item())
