@@ -185,6 +185,9 @@ HEAD_CASES = [
     (2, 2, 2, 256, 6, 1, 0, 1.0, 0.0, 256, 0),
     (1, 16, 20, 16, 2, 7, 0, 1.0, 0.0, 16, 0),
     (2, 6, 8, 128, 1, 3, 1, 10.0, 0.001, 128, 0),
+    (4, 96, 128, 16, 1, 3, 1, 4.0, 0.0, 20, 4),      # many wgrad chunks, offset view
+    (2, 48, 64, 32, 2, 5, 0, 1.0, 0.0, 32, 0),       # exp/mask2 shape: 25 taps = 5 tap groups
+    (2, 48, 64, 16, 2, 7, 0, 1.0, 0.0, 16, 0),       # exp/mask1 shape: 49 taps = 10 tap groups
 ]
 
 

@@ -25,26 +25,38 @@ RowSplit row_split(int M, int C) {
   return r;
 }
 
-// Sum the per-chunk fp64 partials [chunks][2][C] for 64 channels per block: 4 waves split the
-// chunk range, one LDS combine.  Returns (in wave 0) the two totals for channel c.
+// Sum the per-chunk fp64 partials [chunks][2][C] for 64 channels per 1024-thread block: 16 waves
+// split the chunk range, each keeping 4 chunks' loads in flight (the loop is L2-latency bound, not
+// bandwidth bound), then one fixed-order LDS combine.  Returns (in wave 0) the totals for channel c.
+constexpr int FIN_WAVES = 16;
 __device__ __forceinline__ bool reduce_chunks(int C, int chunks, const double* part, double& s0, double& s1,
                                               int& c) {
-  __shared__ double sh[2][256];
+  __shared__ double sh[2][FIN_WAVES * 64];
   const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
   c = blockIdx.x * 64 + cl;
-  double a = 0.0, b = 0.0;
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
   if (c < C) {
-    for (int k = w; k < chunks; k += 4) {
-      a += part[(long)k * 2 * C + c];
-      b += part[(long)k * 2 * C + C + c];
+    const long st = 2l * C;
+    int k = w;
+    for (; k + 3 * FIN_WAVES < chunks; k += 4 * FIN_WAVES) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += part[(k + u * FIN_WAVES) * st + c];
+        b[u] += part[(k + u * FIN_WAVES) * st + C + c];
+      }
+    }
+    for (int u = 0; k < chunks; k += FIN_WAVES, ++u) {
+      a[u & 3] += part[k * st + c];
+      b[u & 3] += part[k * st + C + c];
     }
   }
-  sh[0][threadIdx.x] = a;
-  sh[1][threadIdx.x] = b;
+  sh[0][threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
+  sh[1][threadIdx.x] = (b[0] + b[1]) + (b[2] + b[3]);
   __syncthreads();
   if (w != 0 || c >= C) return false;
-  s0 = sh[0][cl] + sh[0][cl + 64] + sh[0][cl + 128] + sh[0][cl + 192];
-  s1 = sh[1][cl] + sh[1][cl + 64] + sh[1][cl + 128] + sh[1][cl + 192];
+  s0 = 0.0; s1 = 0.0;
+#pragma unroll
+  for (int v = 0; v < FIN_WAVES; ++v) { s0 += sh[0][cl + 64 * v]; s1 += sh[1][cl + 64 * v]; }
   return true;
 }
 
@@ -70,30 +82,30 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(int M, int C, const flo
         is = *reinterpret_cast<const f4*>(invstd + 4 * c4);
         bt = *reinterpret_cast<const f4*>(beta + 4 * c4);
       }
-      float f0[4] = {0, 0, 0, 0}, f1[4] = {0, 0, 0, 0};
-      int cnt = 0;
-      for (int r = r0 + ty; r < r1; r += ty_n) {
-        const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + 4 * c4);
-        if (MODE == 0) {
+      // fp32 partials over <= 64 rows per thread, flushed into fp64; unrolled so 8 rows' loads are
+      // in flight at once (one load per iteration would expose the full memory latency each time)
+      for (int rb = r0 + ty; rb < r1; rb += 64 * ty_n) {
+        const int rend = min(r1, rb + 64 * ty_n);
+        float f0[4] = {0, 0, 0, 0}, f1[4] = {0, 0, 0, 0};
+#pragma unroll 8
+        for (int r = rb; r < rend; r += ty_n) {
+          const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + 4 * c4);
+          if (MODE == 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { f0[j] += zv[j]; f1[j] += zv[j] * zv[j]; }
-        } else {
-          const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + 4 * c4);
+            for (int j = 0; j < 4; ++j) { f0[j] += zv[j]; f1[j] += zv[j] * zv[j]; }
+          } else {
+            const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + 4 * c4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float xh = (zv[j] - mu[j]) * is[j];
-            const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
-            f0[j] += g; f1[j] += g * xh;
+            for (int j = 0; j < 4; ++j) {
+              const float xh = (zv[j] - mu[j]) * is[j];
+              const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
+              f0[j] += g; f1[j] += g * xh;
+            }
           }
         }
-        if (++cnt == 64) {  // flush fp32 partials into fp64 every 64 rows
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { s0[j] += f0[j]; s1[j] += f1[j]; f0[j] = 0; f1[j] = 0; }
-          cnt = 0;
-        }
+        for (int j = 0; j < 4; ++j) { s0[j] += f0[j]; s1[j] += f1[j]; }
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { s0[j] += f0[j]; s1[j] += f1[j]; }
     }
   }
   // reduce over ty within the block (cq <= 256 case; for cq > 256 each thread owns distinct channels)
@@ -112,7 +124,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(int M, int C, const flo
   }
 }
 
-__global__ void bn_stats_finalize_kernel(int M, int C, int chunks, const double* part, float eps, float decay,
+__global__ void __launch_bounds__(1024) bn_stats_finalize_kernel(int M, int C, int chunks, const double* part, float eps, float decay,
                                          int bessel, float* mm, float* mv, float* save_mean, float* save_invstd) {
   double s, ss;
   int c;
@@ -170,7 +182,7 @@ __global__ void __launch_bounds__(256) bn_infer_kernel(int M, int C, const float
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(int M, int C, int chunks, const double* part, float* dbeta, int acc,
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int M, int C, int chunks, const double* part, float* dbeta, int acc,
                                        float* coef /*[2][C]: mean(g), mean(g*xhat)*/) {
   double s, sx;
   int c;
@@ -233,7 +245,7 @@ int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps,
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(rs.chunks), dim3(256), 0, st, M, C, z, nullptr, 0, 0, nullptr,
                      nullptr, nullptr, 0, rs.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, M, C, rs.chunks, part, eps,
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, st, M, C, rs.chunks, part, eps,
                      decay, bessel, moving_mean, moving_var, save_mean, save_invstd);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid((long)M * C / 4)), dim3(256), 0, st, M, C, z, save_mean,
                      save_invstd, beta, relu, y, y_cstride, y_coff);
@@ -262,7 +274,7 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
   float* coef = reinterpret_cast<float*>(part + (size_t)rs.chunks * 2 * C);
   hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(rs.chunks), dim3(256), 0, st, M, C, z, dy, dy_cstride, dy_coff,
                      save_mean, save_invstd, beta, relu, rs.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, M, C, rs.chunks, part, dbeta,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0, st, M, C, rs.chunks, part, dbeta,
                      accumulate_dbeta, coef);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((long)M * C / 4)), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                      dy_coff, save_mean, save_invstd, beta, coef, relu, dz);

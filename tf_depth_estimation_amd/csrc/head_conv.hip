@@ -1,8 +1,15 @@
 // Few-output-channel conv heads (K <= 8): disparity heads (nets_optflow_depth.py:122-144,
 // DISP_SCALING*sigmoid(conv+b) [+MIN_DISP]), flow heads (nets_depth.py:169-191, 2-ch linear), exp-mask
-// logits (nets_optflow_depth.py:193-198) and pose/pred 1x1 (:181).  These GEMMs have N = 1..6 and are
-// HBM/L2-bound (arithmetic intensity ~K flop/B), so they are direct convolutions on the vector ALU
-// with the activation and its derivative fused, not MFMA tiles padded to 16 columns.
+// logits (nets_optflow_depth.py:193-198, k 3/5/7) and pose/pred 1x1 (:181).  These GEMMs have N = 1..6
+// and are HBM/L2-bound (arithmetic intensity ~K flop/B), so they are direct convolutions on the vector
+// ALU with the activation and its derivative fused, not MFMA tiles padded to 16 columns.
+//
+//   fwd   : L lanes per output pixel split the (tap, channel-quad) reduction, xor-shuffle combine.
+//   dz    : dz = dL/d(pre-activation) once per output element (workspace), reused by dgrad and wgrad.
+//   dgrad : one thread per (input pixel, channel quad) gathers dz over the taps (stride 1).
+//   wgrad : block = (pixel chunk, tap group); thread = (channel quad, pixel lane) keeps a
+//           TT-tap x 4-channel x K register tile over its pixels, LDS combine over pixel lanes, then a
+//           deterministic fixed-order reduction over chunks.
 #include "tde_common.h"
 
 namespace {
@@ -13,6 +20,7 @@ struct HeadArgs {
   const float* w; const float* b;
   float* y; const float* yin; const float* dy; int ycs, yco;
   float* dx; int acc_dx;
+  const float* dz;   // [M][K] dense (backward)
   int act; float scale, offset;
 };
 
@@ -27,38 +35,59 @@ __device__ __forceinline__ float head_dz(float y, float dy, int act, float scale
   return dy * scale * s * (1.f - s);
 }
 
-template <int KC>
+template <int KC, int L>
 __global__ void __launch_bounds__(256) head_fwd_kernel(const HeadArgs p) {
+  constexpr int PPB = 256 / L;
+  const int lane = threadIdx.x & (L - 1);
   const long M = (long)p.N * p.OH * p.OW;
-  for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
-    const int ohw = p.OH * p.OW;
-    const int n = (int)(m / ohw), r = (int)(m - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
+  const int ohw = p.OH * p.OW;
+  for (long m0 = (long)blockIdx.x * PPB; m0 < M; m0 += (long)gridDim.x * PPB) {
+    const long m = m0 + threadIdx.x / L;
     float acc[KC];
 #pragma unroll
     for (int k = 0; k < KC; ++k) acc[k] = 0.f;
-    for (int kh = 0; kh < p.KH; ++kh) {
-      const int ih = oh * p.S - p.PT + kh;
-      if ((unsigned)ih >= (unsigned)p.H) continue;
-      for (int kw = 0; kw < p.KW; ++kw) {
-        const int iw = ow * p.S - p.PL + kw;
-        if ((unsigned)iw >= (unsigned)p.W) continue;
-        const float* xp = p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco;
-        const float* wp = p.w + (long)(kh * p.KW + kw) * p.wcin * KC;
-        for (int c = 0; c < p.wcin; c += 4) {
-          const f4 xv = *reinterpret_cast<const f4*>(xp + c);
+    if (m < M) {
+      const int n = (int)(m / ohw), r = (int)(m - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
+      for (int kh = 0; kh < p.KH; ++kh) {
+        const int ih = oh * p.S - p.PT + kh;
+        if ((unsigned)ih >= (unsigned)p.H) continue;
+        for (int kw = 0; kw < p.KW; ++kw) {
+          const int iw = ow * p.S - p.PL + kw;
+          if ((unsigned)iw >= (unsigned)p.W) continue;
+          const float* xp = p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco;
+          const float* wp = p.w + (long)(kh * p.KW + kw) * p.wcin * KC;
+          for (int c = 4 * lane; c < p.wcin; c += 4 * L) {
+            const f4 xv = *reinterpret_cast<const f4*>(xp + c);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (c + j < p.wcin) {
+            for (int j = 0; j < 4; ++j)
+              if (c + j < p.wcin) {
 #pragma unroll
-              for (int k = 0; k < KC; ++k) acc[k] = fmaf(xv[j], wp[(c + j) * KC + k], acc[k]);
-            }
+                for (int k = 0; k < KC; ++k) acc[k] = fmaf(xv[j], wp[(c + j) * KC + k], acc[k]);
+              }
           }
         }
       }
     }
-    float* yp = p.y + m * p.ycs + p.yco;
 #pragma unroll
-    for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[k] + p.b[k], p.act, p.scale, p.offset);
+    for (int off = L / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+    if (m < M && lane == 0) {
+      float* yp = p.y + m * p.ycs + p.yco;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[k] + p.b[k], p.act, p.scale, p.offset);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) head_dz_kernel(long M, int K, const float* y, const float* dy, int ycs,
+                                                      int yco, int act, float scale, float offset, float* dz) {
+  const long total = M * K;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / K;
+    const int k = (int)(i - m * K);
+    const long o = m * ycs + yco + k;
+    dz[i] = head_dz(y[o], dy[o], act, scale, offset);
   }
 }
 
@@ -73,20 +102,22 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const HeadArgs p) {
     const int hw = p.H * p.W;
     const int n = (int)(pix / hw), r = (int)(pix - (long)n * hw), ih = r / p.W, iw = r - ih * p.W;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int kh = 0; kh < p.KH; ++kh) {
-      const int oh = ih + p.PT - kh;
-      if ((unsigned)oh >= (unsigned)p.OH) continue;
-      for (int kw = 0; kw < p.KW; ++kw) {
-        const int ow = iw + p.PL - kw;
-        if ((unsigned)ow >= (unsigned)p.OW) continue;
-        const long o = ((long)(n * p.OH + oh) * p.OW + ow) * p.ycs + p.yco;
-        const float* wp = p.w + (long)(kh * p.KW + kw) * p.wcin * KC;
+    if (c < p.wcin) {
+      for (int kh = 0; kh < p.KH; ++kh) {
+        const int oh = ih + p.PT - kh;
+        if ((unsigned)oh >= (unsigned)p.OH) continue;
+        for (int kw = 0; kw < p.KW; ++kw) {
+          const int ow = iw + p.PL - kw;
+          if ((unsigned)ow >= (unsigned)p.OW) continue;
+          const float* dzp = p.dz + ((long)(n * p.OH + oh) * p.OW + ow) * KC;
+          const float* wp = p.w + (long)(kh * p.KW + kw) * p.wcin * KC;
 #pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          const float dz = head_dz(p.yin[o + k], p.dy[o + k], p.act, p.scale, p.offset);
+          for (int k = 0; k < KC; ++k) {
+            const float dz = dzp[k];
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (c + j < p.wcin) acc[j] = fmaf(dz, wp[(c + j) * KC + k], acc[j]);
+            for (int j = 0; j < 4; ++j)
+              if (c + j < p.wcin) acc[j] = fmaf(dz, wp[(c + j) * KC + k], acc[j]);
+          }
         }
       }
     }
@@ -97,125 +128,154 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const HeadArgs p) {
   }
 }
 
-// Per-chunk partial dW / db: part[chunk][e*KC + k] for e = (tap, c) in [0, KH*KW*wcin), then KC bias sums.
-constexpr int HW_PIX = 128;  // pixels per chunk (staged dz in LDS)
+// taps per wgrad block: TT * 4 * KC accumulators per thread
+template <int KC>
+struct WgTaps { static constexpr int TT = KC == 1 ? 9 : (KC == 2 ? 5 : 2); };
 
-// One block per pixel chunk (<= HW_CHUNKS chunks).  Threads = (entry e, pixel lane g): when the weight
-// has E < 256 entries, 256/E lanes split each staged sub-chunk's pixels and are combined through LDS.
-constexpr int HW_CHUNKS = 1024;
+constexpr int WG_MAX_CHUNKS = 1024;
 
+// part[chunk][e * KC + k] for e = tap * wcin + c (only this block's taps), plus part[chunk][E*KC + k]
+// = bias sums (tap group 0).
 template <int KC>
 __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs p, float* part, int pix_per_chunk) {
-  __shared__ float sdz[HW_PIX * KC];
-  __shared__ float sred[256 * KC];
-  __shared__ int3 spix[HW_PIX];
+  constexpr int TT = WgTaps<KC>::TT;
+  constexpr int NV = TT * 4 * KC;
+  __shared__ float sred[256 * NV];
   const long M = (long)p.N * p.OH * p.OW;
+  const int CQ = p.C / 4;
+  const int P = 256 / CQ;                     // pixel lanes (CQ <= 64)
+  const int q = (int)threadIdx.x % CQ, pl = (int)threadIdx.x / CQ;
+  const int ntaps = p.KH * p.KW;
+  const int t0 = blockIdx.y * TT;
+  const int nt = min(TT, ntaps - t0);
   const long cbeg = (long)blockIdx.x * pix_per_chunk;
   const long cend = min(M, cbeg + pix_per_chunk);
-  const int E = p.KH * p.KW * p.wcin;
-  const int G = E >= 256 ? 1 : 256 / E;          // pixel lanes
-  const int lane = (int)threadIdx.x / (E >= 256 ? 256 : E);
-  const bool active = lane < G;
   const int ohw = p.OH * p.OW;
-  // each thread owns entries e = e0, e0 + 256, ... (G == 1) or exactly one entry (G > 1)
-  const int e0 = E >= 256 ? (int)threadIdx.x : (int)threadIdx.x % E;
-  const int ne = E >= 256 ? (E - e0 + 255) / 256 : 1;
-  constexpr int MAXE = 8;                        // E <= 2048 entries
-  float acc[MAXE][KC];
+  int tkh[TT], tkw[TT];
 #pragma unroll
-  for (int j = 0; j < MAXE; ++j)
+  for (int t = 0; t < TT; ++t) {
+    const int tap = min(t0 + t, ntaps - 1);
+    tkh[t] = tap / p.KW - p.PT;
+    tkw[t] = tap - (tap / p.KW) * p.KW - p.PL;
+  }
+  float acc[TT][4][KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) acc[j][k] = 0.f;
+  for (int t = 0; t < TT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) acc[t][j][k] = 0.f;
   float bacc[KC];
 #pragma unroll
   for (int k = 0; k < KC; ++k) bacc[k] = 0.f;
-  for (long p0 = cbeg; p0 < cend; p0 += HW_PIX) {
-    const int np = (int)min((long)HW_PIX, cend - p0);
-    __syncthreads();
-    for (int t = threadIdx.x; t < HW_PIX * KC; t += blockDim.x) {
-      const int pi = t / KC, k = t - pi * KC;
-      float v = 0.f;
-      if (pi < np) {
-        const long o = (p0 + pi) * p.ycs + p.yco + k;
-        v = head_dz(p.yin[o], p.dy[o], p.act, p.scale, p.offset);
-      }
-      sdz[t] = v;
-    }
-    for (int pi = threadIdx.x; pi < np; pi += blockDim.x) {   // pixel decode once per sub-chunk
-      const long pix = p0 + pi;
+  if (pl < P) {
+    for (long pix = cbeg + pl; pix < cend; pix += P) {
+      float dz[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) dz[k] = p.dz[pix * KC + k];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) bacc[k] += dz[k];
       const int n = (int)(pix / ohw), r = (int)(pix - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
-      spix[pi] = make_int3(n * p.H, oh * p.S - p.PT, ow * p.S - p.PL);
-    }
-    __syncthreads();
-    if (threadIdx.x < KC)
-      for (int pi = 0; pi < np; ++pi) bacc[threadIdx.x] += sdz[pi * KC + threadIdx.x];
-    if (!active) continue;
+      const float* xb = p.x + (long)n * p.H * p.W * p.xcs + p.xco + 4 * q;
 #pragma unroll
-    for (int j = 0; j < MAXE; ++j) {
-      if (j >= ne) break;
-      const int e = e0 + j * 256;
-      const int tap = e / p.wcin, c = e - tap * p.wcin, kh = tap / p.KW, kw = tap - kh * p.KW;
-      for (int pi = lane; pi < np; pi += G) {
-        const int3 q = spix[pi];
-        const int ih = q.y + kh, iw = q.z + kw;
-        if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
-          const float xv = p.x[((long)(q.x + ih) * p.W + iw) * p.xcs + p.xco + c];
+      for (int t = 0; t < TT; ++t) {
+        const int ih = oh * p.S + tkh[t], iw = ow * p.S + tkw[t];
+        if (t < nt && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W) {
+          const f4 xv = *reinterpret_cast<const f4*>(xb + ((long)ih * p.W + iw) * p.xcs);
 #pragma unroll
-          for (int k = 0; k < KC; ++k) acc[j][k] = fmaf(xv, sdz[pi * KC + k], acc[j][k]);
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < KC; ++k) acc[t][j][k] = fmaf(xv[j], dz[k], acc[t][j][k]);
         }
       }
     }
   }
-  const int stride_out = E * KC + KC;
-  float* out = part + (long)blockIdx.x * stride_out;
-  if (G == 1) {
-    if (active)
-      for (int j = 0; j < ne; ++j)
+  // combine the P pixel lanes: sred[thread][t][j][k]
+  float* mine = sred + threadIdx.x * NV;
 #pragma unroll
-        for (int k = 0; k < KC; ++k) out[(e0 + j * 256) * KC + k] = acc[j][k];
-  } else {
-    __syncthreads();
-    if (active)
+  for (int t = 0; t < TT; ++t)
 #pragma unroll
-      for (int k = 0; k < KC; ++k) sred[threadIdx.x * KC + k] = acc[0][k];
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) mine[(t * 4 + j) * KC + k] = acc[t][j][k];
+  __syncthreads();
+  const int E = ntaps * p.wcin;
+  float* out = part + (long)blockIdx.x * (E * KC + KC);
+  const int nout = nt * CQ * 4 * KC;
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    const int k = o % KC, cj = (o / KC) % (CQ * 4), t = o / (KC * CQ * 4);
+    const int qq = cj >> 2, j = cj & 3;
+    const int c = 4 * qq + j;
+    if (c >= p.wcin) continue;
+    float s = 0.f;
+    for (int l = 0; l < P; ++l) s += sred[(l * CQ + qq) * NV + (t * 4 + j) * KC + k];
+    out[((t0 + t) * p.wcin + c) * KC + k] = s;
+  }
+  if (blockIdx.y == 0) {
     __syncthreads();
-    if ((int)threadIdx.x < E) {
-      for (int k = 0; k < KC; ++k) {
-        float s = 0.f;
-        for (int g = 0; g < G; ++g) s += sred[(g * E + threadIdx.x) * KC + k];
-        out[threadIdx.x * KC + k] = s;
-      }
+    if (q == 0 && pl < P)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) sred[pl * KC + k] = bacc[k];
+    __syncthreads();
+    if (threadIdx.x < KC) {
+      float s = 0.f;
+      for (int l = 0; l < P; ++l) s += sred[l * KC + threadIdx.x];
+      out[E * KC + threadIdx.x] = s;
     }
   }
-  if (threadIdx.x < KC) out[E * KC + threadIdx.x] = bacc[threadIdx.x];
 }
 
-// 64 outputs per block, 4 waves split the chunk range, fp64 combine through LDS.
-__global__ void __launch_bounds__(256) head_wgrad_reduce_kernel(const float* part, int chunks, int E, int KC,
-                                                                 float* dw, float* db, int accumulate) {
-  __shared__ double sh[256];
-  const int total = E * KC + KC;
+// 64 outputs per block, 16 waves split the chunk range with 4 loads in flight each, fp64 fixed-order
+// combine through LDS.
+__global__ void __launch_bounds__(1024) head_wgrad_reduce_kernel(const float* part, int chunks, int total,
+                                                                  int nw, float* dw, float* db, int accumulate) {
+  __shared__ double sh[1024];
   const int il = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + il;
-  double s = 0.0;
-  if (i < total)
-    for (int ch = w; ch < chunks; ch += 4) s += part[(long)ch * total + i];
-  sh[threadIdx.x] = s;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (i < total) {
+    int ch = w;
+    for (; ch + 48 < chunks; ch += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += part[(long)(ch + 16 * u) * total + i];
+    }
+    for (int u = 0; ch < chunks; ch += 16, ++u) a[u & 3] += part[(long)ch * total + i];
+  }
+  sh[threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (w != 0 || i >= total) return;
-  s = sh[il] + sh[il + 64] + sh[il + 128] + sh[il + 192];
-  float* dst = (i < E * KC) ? dw + i : db + (i - E * KC);
+  double s = 0.0;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) s += sh[il + 64 * v];
+  float* dst = (i < nw) ? dw + i : db + (i - nw);
   *dst = accumulate ? *dst + (float)s : (float)s;
 }
 
-int head_chunks(long M) {
-  const long c = (M + HW_PIX - 1) / HW_PIX;
-  return (int)(c < HW_CHUNKS ? c : HW_CHUNKS);
+struct WgPlan {
+  int chunks, ppc, tgroups;
+};
+
+WgPlan wg_plan(const tde_conv_desc_t* d) {
+  WgPlan w;
+  const long M = (long)d->N * d->OH * d->OW;
+  const int TT = d->K == 1 ? 9 : (d->K == 2 ? 5 : 2);
+  w.tgroups = (d->KH * d->KW + TT - 1) / TT;
+  const int P = 256 / (d->C / 4);
+  // >= 8 pixels per thread lane, ~2048 blocks in total, <= WG_MAX_CHUNKS partial rows
+  long chunks = (2048 + w.tgroups - 1) / w.tgroups;
+  const long maxc = (M + 8l * P - 1) / (8l * P);
+  if (chunks > maxc) chunks = maxc;
+  if (chunks > WG_MAX_CHUNKS) chunks = WG_MAX_CHUNKS;
+  if (chunks < 1) chunks = 1;
+  w.ppc = (int)((M + chunks - 1) / chunks);
+  w.chunks = (int)((M + w.ppc - 1) / w.ppc);
+  return w;
 }
 
 bool head_desc_ok(const tde_conv_desc_t* d) {
   if (!d) return false;
   if (d->K < 1 || d->K > 8 || d->C % 4 || d->w_cin > d->C || d->w_cin <= 0) return false;
+  if (d->C > 256) return false;   // wgrad: one channel quad per thread, >= 1 pixel lane per block
   if (d->x_coff + d->C > d->x_cstride || d->y_coff + d->K > d->y_cstride) return false;
   return d->N > 0 && d->H > 0 && d->W > 0 && d->OH > 0 && d->OW > 0;
 }
@@ -233,6 +293,23 @@ int grid_for(long n) {
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
 
+size_t dz_bytes(const tde_conv_desc_t* d) {
+  const size_t n = (size_t)d->N * d->OH * d->OW * d->K * sizeof(float);
+  return (n + 255) / 256 * 256;
+}
+
+template <int KC>
+int launch_fwd(const HeadArgs& a, long M, hipStream_t st) {
+  const int cq = (a.wcin + 3) / 4;
+  const int L = cq <= 4 ? 4 : (cq <= 8 ? 8 : 16);
+  const long blocks = (M * L + 255) / 256;
+  const dim3 g((unsigned)(blocks > 16384 ? 16384 : blocks));
+  if (L == 4) hipLaunchKernelGGL((head_fwd_kernel<KC, 4>), g, dim3(256), 0, st, a);
+  else if (L == 8) hipLaunchKernelGGL((head_fwd_kernel<KC, 8>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((head_fwd_kernel<KC, 16>), g, dim3(256), 0, st, a);
+  return TDE_OK;
+}
+
 #define HEAD_DISPATCH(KVAL, KERNEL, GRID, ...)                                              \
   switch (KVAL) {                                                                            \
     case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
@@ -247,9 +324,9 @@ extern "C" {
 
 size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
-  const long M = (long)d->N * d->OH * d->OW;
-  const long chunks = head_chunks(M);
-  return (size_t)chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
+  const WgPlan w = wg_plan(d);
+  const size_t part = (size_t)w.chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
+  return dz_bytes(d) + part;
 }
 
 int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, float* y,
@@ -259,7 +336,12 @@ int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   a.x = x; a.w = w; a.b = bias; a.y = y; a.act = act; a.scale = scale; a.offset = offset;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const long M = (long)d->N * d->OH * d->OW;
-  HEAD_DISPATCH(d->K, head_fwd_kernel, dim3(grid_for(M)), a);
+  switch (d->K) {
+    case 1: launch_fwd<1>(a, M, st); break;
+    case 2: launch_fwd<2>(a, M, st); break;
+    case 6: launch_fwd<6>(a, M, st); break;
+    default: return TDE_ERR_UNSUPPORTED;
+  }
   return tde_launch_status();
 }
 
@@ -268,10 +350,17 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
                  float offset, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(head_desc_ok(d) && d->stride == 1 && x && w && y && dy && tde_aligned16(x));
   TDE_CHECK_ARG(d->x_cstride % 4 == 0 && d->x_coff % 4 == 0);
+  TDE_CHECK_ARG(d->K == 1 || d->K == 2 || d->K == 6);
+  if (ws_bytes < tde_head_workspace_size(d) || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   HeadArgs a = make_head_args(d);
   a.x = x; a.w = w; a.yin = y; a.dy = dy; a.dx = dx; a.acc_dx = accumulate_dx;
   a.act = act; a.scale = scale; a.offset = offset;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const long M = (long)d->N * d->OH * d->OW;
+  float* dz = static_cast<float*>(ws);
+  a.dz = dz;
+  hipLaunchKernelGGL(head_dz_kernel, dim3(grid_for(M * d->K)), dim3(256), 0, st, M, d->K, y, dy, d->y_cstride,
+                     d->y_coff, act, scale, offset, dz);
   if (dx) {
     TDE_CHECK_ARG(tde_aligned16(dx));
     const long n = (long)d->N * d->H * d->W * (d->C / 4);
@@ -279,17 +368,13 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   }
   if (dw) {
     TDE_CHECK_ARG(dbias != nullptr);
-    if (ws_bytes < tde_head_workspace_size(d)) return TDE_ERR_WORKSPACE;
-    float* part = static_cast<float*>(ws);
-    const long M = (long)d->N * d->OH * d->OW;
-    const int chunks = head_chunks(M);
-    const int ppc = (int)((M + chunks - 1) / chunks);
-    TDE_CHECK_ARG(d->KH * d->KW * d->w_cin <= 2048);
-    HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(chunks), a, part, ppc);
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
+    const WgPlan wp = wg_plan(d);
+    HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(wp.chunks, wp.tgroups), a, part, wp.ppc);
     const int E = d->KH * d->KW * d->w_cin;
     const int total = E * d->K + d->K;
-    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, st, part, chunks, E,
-                       d->K, dw, dbias, accumulate_dw);
+    hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, st, part, wp.chunks, total,
+                       E * d->K, dw, dbias, accumulate_dw);
   }
   return tde_launch_status();
 }
