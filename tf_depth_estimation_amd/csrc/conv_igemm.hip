@@ -25,6 +25,25 @@ namespace {
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 constexpr int NT = 256;
 
+// Division by a runtime constant d >= 1 for 0 <= n < 2^31: q = (umulhi(n, m) + n) >> s with
+// s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1.  Replaces the ~30-instruction integer division
+// in the im2col decode of every k-tile by three instructions.
+struct FDiv {
+  unsigned m; int s;
+};
+
+__host__ __device__ inline FDiv make_fdiv(int d) {
+  FDiv f;
+  f.s = 0;
+  while ((1 << f.s) < d) ++f.s;
+  f.m = (unsigned)((((unsigned long long)1 << 32) * (((unsigned long long)1 << f.s) - (unsigned)d)) / (unsigned)d + 1);
+  return f;
+}
+
+__device__ __forceinline__ int fdiv(int n, FDiv f) {
+  return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s);
+}
+
 struct ConvArgs {
   int N, H, W, C, OH, OW, K, KH, KW, S, PT, PL, wcin;
   const float* x; float* dx; int xcs, xco;
@@ -32,6 +51,7 @@ struct ConvArgs {
   const float* w; float* dw;
   float* ws; int splits; int accumulate;
   int kt_per;  // k-tiles per split
+  FDiv fC, fK, fKW, fOW, fOHW;
 };
 
 // Per-class geometry of the DGRAD sub-pixel decomposition.
@@ -57,6 +77,18 @@ __device__ __forceinline__ DgClass dg_class(const ConvArgs& p, int cls) {
 }
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+// Raw buffer resource over n floats (byte range clamped below 2^31 so OOB is always out of range;
+// 0x00020000 = DATA_FORMAT 32 for gfx9-family raw buffers).
+constexpr int OOB = (int)0x80000000;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, long n) {
+  const long bytes = 4 * n;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0,
+                                           (int)(bytes < 0x7fffffffl ? bytes : 0x7fffffffl), 0x00020000);
+}
+__device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 // ------------------------------------------------------------------ bf16x3 split-precision variant
 // Same three gather modes, but each fp32 operand element x is split at staging time into
@@ -144,23 +176,30 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
 
+  // Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
+  // share a pixel slab -- was measured 5-20% SLOWER on config 2's layers: the round-robin order
+  // already lets neighbouring tiles, dispatched together, share the slab through the Infinity Cache.)
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+
   int M, Nn, Kd;
   DgClass g{};
   int zsplit;
   if constexpr (MODE == MODE_DGRAD) {
     const int ncls = p.S * p.S;
-    const int cls = blockIdx.z % ncls;
-    zsplit = blockIdx.z / ncls;
+    const int cls = bz % ncls;
+    zsplit = bz / ncls;
     g = dg_class(p, cls);
     M = g.M; Nn = p.C; Kd = g.Kd;
   } else if constexpr (MODE == MODE_FWD) {
-    zsplit = blockIdx.z;
+    zsplit = bz;
     M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
   } else {
-    zsplit = blockIdx.z;
+    zsplit = bz;
     M = p.KH * p.KW * p.C; Nn = p.K; Kd = p.N * p.OH * p.OW;
   }
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  FDiv fntw{};
+  if constexpr (MODE == MODE_DGRAD) fntw = make_fdiv(g.ntw);
+  const int m0 = bx * BM, n0 = by * BN;
   if (m0 >= M || n0 >= Nn) return;
   const int nkt = (Kd + BK3 - 1) / BK3;
   const int kt0 = zsplit * p.kt_per;
@@ -171,32 +210,41 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
   constexpr int B_SLOTS = B_T ? (BN / 4) * (BK3 / 4) : BN * (BK3 / 4);
   constexpr int A_PER = (A_SLOTS + NT - 1) / NT, B_PER = (B_SLOTS + NT - 1) / NT;
   constexpr int A_V = A_T ? 4 : 1, B_V = B_T ? 4 : 1;   // f4 loads per slot
-  int a_i0[A_PER], a_i1[A_PER], a_i2[A_PER];
-  bool a_ok[A_PER];
+
+  // Operands are read through raw buffer resources: an invalid element (padding tap, tile edge, k
+  // tail) gets offset OOB >= num_records and loads as zero -- no branches, no zero-fill moves.
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, (long)p.N * p.OH * p.OW * p.ycs);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, (long)p.KH * p.KW * p.wcin * p.K);
+
+  // per-slot row geometry (float offsets; `pb` = element offset of the row at tap/k origin)
+  int a_pb[A_PER], a_i1[A_PER], a_i2[A_PER];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int s = tid + i * NT;
-    a_ok[i] = false; a_i0[i] = a_i1[i] = a_i2[i] = 0;
-    if (s >= A_SLOTS) continue;
+    a_pb[i] = 0; a_i1[i] = -(1 << 28); a_i2[i] = -(1 << 28);   // invalid row -> every tap out of range
     if constexpr (MODE == MODE_FWD) {
       const int m = m0 + (s >> 3);
-      if (m < M) {
+      if (s < A_SLOTS && m < M) {
         const int ohw = p.OH * p.OW;
         const int n = m / ohw, r = m - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
-        a_ok[i] = true; a_i0[i] = n; a_i1[i] = oh * p.S - p.PT; a_i2[i] = ow * p.S - p.PL;
+        a_i1[i] = oh * p.S - p.PT; a_i2[i] = ow * p.S - p.PL;
+        a_pb[i] = ((n * p.H + a_i1[i]) * p.W + a_i2[i]) * p.xcs + p.xco;
       }
     } else if constexpr (MODE == MODE_DGRAD) {
       const int m = m0 + (s >> 3);
-      if (m < M) {
+      if (s < A_SLOTS && m < M) {
         const int hw = g.HH * g.WW;
         const int n = m / hw, r = m - n * hw, ihh = r / g.WW, iww = r - ihh * g.WW;
-        a_ok[i] = true; a_i0[i] = n; a_i1[i] = ihh + g.dh; a_i2[i] = iww + g.dw;
+        a_i1[i] = ihh + g.dh; a_i2[i] = iww + g.dw;
+        a_pb[i] = ((n * p.OH + a_i1[i]) * p.OW + a_i2[i]) * p.ycs + p.yco;
       }
     } else {
       const int m = m0 + 4 * (s % (BM / 4));
-      if (m < M) {
+      if (s < A_SLOTS && m < M) {
         const int tap = m / p.C, c = m - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
-        a_ok[i] = true; a_i0[i] = c; a_i1[i] = kh - p.PT; a_i2[i] = kw - p.PL;
+        a_i1[i] = kh - p.PT; a_i2[i] = kw - p.PL;
+        a_pb[i] = (a_i1[i] * p.W + a_i2[i]) * p.xcs + p.xco + c;
       }
     }
   }
@@ -205,73 +253,67 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
 
   auto load_tiles = [&](int kt) {
     const int kbase = kt * BK3;
+    // k decode shared by every A slot (and the DGRAD B slots): s & 7 == tid & 7 for all slots
+    const int kq = kbase + 4 * (tid & 7);
+    int t_h = 0, t_w = 0, koff = 0, kx = 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = fdiv(kq, p.fC), c = kq - tap * p.C;
+      t_h = fdiv(tap, p.fKW); t_w = tap - t_h * p.KW;
+      koff = (t_h * p.W + t_w) * p.xcs + c;
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int tap = fdiv(kq, p.fK);
+      kx = kq - tap * p.K;                       // output channel co
+      t_h = fdiv(tap, fntw); t_w = tap - t_h * g.ntw;
+      koff = -(t_h * p.OW + t_w) * p.ycs + kx;
+    }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      const int s = tid + i * NT;
+      if constexpr (MODE == MODE_FWD) {
+        const bool ok = kq < Kd && (unsigned)(a_i1[i] + t_h) < (unsigned)p.H &&
+                        (unsigned)(a_i2[i] + t_w) < (unsigned)p.W;
+        ra[i][0] = bload(rx, ok ? 4 * (a_pb[i] + koff) : OOB);
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const bool ok = kq < Kd && (unsigned)(a_i1[i] - t_h) < (unsigned)p.OH &&
+                        (unsigned)(a_i2[i] - t_w) < (unsigned)p.OW;
+        ra[i][0] = bload(rdy, ok ? 4 * (a_pb[i] + koff) : OOB);
+      } else {
+        const int s = tid + i * NT;
+        const int pix0 = kbase + 4 * (s / (BM / 4));
+        int n = fdiv(pix0, p.fOHW);
+        const int r = pix0 - n * p.OH * p.OW;
+        int oh = fdiv(r, p.fOW), ow = r - oh * p.OW;
 #pragma unroll
-      for (int j = 0; j < A_V; ++j) ra[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-      if (s < A_SLOTS && a_ok[i]) {
-        if constexpr (MODE == MODE_FWD) {
-          const int k = kbase + 4 * (s & 7);
-          if (k < Kd) {
-            const int tap = k / p.C, c = k - tap * p.C, kh = tap / p.KW, kw = tap - kh * p.KW;
-            const int ih = a_i1[i] + kh, iw = a_i2[i] + kw;
-            if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-              ra[i][0] = ld4(p.x + ((long)(a_i0[i] * p.H + ih) * p.W + iw) * p.xcs + p.xco + c);
-          }
-        } else if constexpr (MODE == MODE_DGRAD) {
-          const int k = kbase + 4 * (s & 7);
-          if (k < Kd) {
-            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
-            const int oh = a_i1[i] - th, ow = a_i2[i] - tw;
-            if ((unsigned)oh < (unsigned)p.OH && (unsigned)ow < (unsigned)p.OW)
-              ra[i][0] = ld4(p.dy + ((long)(a_i0[i] * p.OH + oh) * p.OW + ow) * p.ycs + p.yco + co);
-          }
-        } else {
-          const int ohw = p.OH * p.OW;
-          const int pix0 = kbase + 4 * (s / (BM / 4));
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int pix = pix0 + j;
-            if (pix < Kd) {
-              const int n = pix / ohw, r = pix - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
-              const int ih = oh * p.S + a_i1[i], iw = ow * p.S + a_i2[i];
-              if ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W)
-                ra[i][j] = ld4(p.x + ((long)(n * p.H + ih) * p.W + iw) * p.xcs + p.xco + a_i0[i]);
-            }
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int ih = oh * p.S, iw = ow * p.S;
+          const bool ok = pix0 + j < Kd && (unsigned)(ih + a_i1[i]) < (unsigned)p.H &&
+                          (unsigned)(iw + a_i2[i]) < (unsigned)p.W;
+          ra[i][j] = bload(rx, ok ? 4 * (a_pb[i] + ((n * p.H + ih) * p.W + iw) * p.xcs) : OOB);
+          if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int s = tid + i * NT;
+      const bool slot = s < B_SLOTS;
+      if constexpr (MODE == MODE_FWD) {
+        const int n = n0 + 4 * (s % (BN / 4)), k0 = kbase + 4 * (s / (BN / 4));
+        const int tap = fdiv(k0, p.fC), c0 = k0 - tap * p.C;   // k0..k0+3 share the tap (C % 4 == 0)
+        const bool ok = slot && n < Nn && k0 < Kd;
 #pragma unroll
-      for (int j = 0; j < B_V; ++j) rb[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-      if (s < B_SLOTS) {
-        if constexpr (MODE == MODE_FWD) {
-          const int n = n0 + 4 * (s % (BN / 4)), k0 = kbase + 4 * (s / (BN / 4));
-          if (n < Nn && k0 < Kd) {
-            const int tap = k0 / p.C, c0 = k0 - tap * p.C;   // k0..k0+3 share the tap (C % 4 == 0)
+        for (int j = 0; j < 4; ++j)
+          rb[i][j] = bload(rw, ok && c0 + j < p.wcin ? 4 * ((tap * p.wcin + c0 + j) * p.K + n) : OOB);
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const int ci = n0 + (s >> 3);
+        const int kh = g.khs + p.S * t_h, kw = g.kws + p.S * t_w;
+        const bool ok = slot && kq < Kd && ci < p.wcin;
+        rb[i][0] = bload(rw, ok ? 4 * (((kh * p.KW + kw) * p.wcin + ci) * p.K + kx) : OOB);
+      } else {
+        const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
+        const bool ok = slot && n < Nn;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (c0 + j < p.wcin) rb[i][j] = ld4(p.w + (long)(tap * p.wcin + c0 + j) * p.K + n);
-          }
-        } else if constexpr (MODE == MODE_DGRAD) {
-          const int ci = n0 + (s >> 3), k = kbase + 4 * (s & 7);
-          if (k < Kd && ci < p.wcin) {
-            const int tap = k / p.K, co = k - tap * p.K, th = tap / g.ntw, tw = tap - th * g.ntw;
-            const int kh = g.khs + p.S * th, kw = g.kws + p.S * tw;
-            rb[i][0] = ld4(p.w + ((long)(kh * p.KW + kw) * p.wcin + ci) * p.K + co);
-          }
-        } else {
-          const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
-          if (n < Nn) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (pix0 + j < Kd) rb[i][j] = ld4(p.dy + (long)(pix0 + j) * p.ycs + p.yco + n);
-          }
-        }
+        for (int j = 0; j < 4; ++j)
+          rb[i][j] = bload(rdy, ok && pix0 + j < Kd ? 4 * ((pix0 + j) * p.ycs + p.yco + n) : OOB);
       }
     }
   };
@@ -323,9 +365,10 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = (kt + 1 < kt1);
-      if (more) load_tiles(kt + 1);
       const ET* A = As0 + cur * IA::SIZE;
       const ET* Bm = Bs0 + cur * IB::SIZE;
+      // fragment reads first, then the next tile's global loads (their address arithmetic overlaps
+      // the LDS latency), then the MFMAs
       if constexpr (MATH == 1) {
         bf8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
@@ -338,6 +381,7 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
           bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
           bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
         }
+        if (more) load_tiles(kt + 1);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -356,6 +400,7 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
 #pragma unroll
           for (int b = 0; b < TN; ++b) fb[kc][b] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 * kc + 4 * q);
         }
+        if (more) load_tiles(kt + 1);
 #pragma unroll
         for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
@@ -424,8 +469,16 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
     const int row = (int)(i / (cols / 4));
     const int col = 4 * (int)(i - (long)row * (cols / 4));
-    f4 s = ld4(p.ws + (long)row * cols + col);
-    for (int z = 1; z < p.splits; ++z) s += ld4(p.ws + z * stride + (long)row * cols + col);
+    // 4 independent partial sums (fixed order -> deterministic) keep 4 slab loads in flight
+    const float* src = p.ws + (long)row * cols + col;
+    f4 s4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int z = 0;
+    for (; z + 3 < p.splits; z += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += ld4(src + (z + u) * stride);
+    }
+    for (int u = 0; z < p.splits; ++z, ++u) s4[u] += ld4(src + z * stride);
+    f4 s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     float* dst;
     if constexpr (MODE == MODE_FWD) {
       dst = p.y + (long)row * p.ycs + p.yco + col;
@@ -474,7 +527,9 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
   pl.bn = Nn <= 16 ? 16 : (Nn <= 32 ? 32 : (Nn <= 64 ? 64 : 128));
   pl.bm = 128;
   long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
-  if (tiles < 256 && M <= 4096) {
+  // WGRAD reduces over every pixel (Kd ~ 1e5): parallelism comes from split-K, so keep the
+  // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.
+  if (mode != MODE_WGRAD && tiles < 256 && M <= 4096) {
     pl.bm = 64;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
@@ -547,6 +602,8 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
   a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.OH = d.OH; a.OW = d.OW; a.K = d.K;
   a.KH = d.KH; a.KW = d.KW; a.S = d.stride; a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
   a.xcs = d.x_cstride; a.xco = d.x_coff; a.ycs = d.y_cstride; a.yco = d.y_coff;
+  a.fC = make_fdiv(d.C); a.fK = make_fdiv(d.K); a.fKW = make_fdiv(d.KW); a.fOW = make_fdiv(d.OW);
+  a.fOHW = make_fdiv(d.OH * d.OW);
   return a;
 }
 
