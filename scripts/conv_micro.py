@@ -28,7 +28,7 @@ SHAPES = [
 ]
 
 
-def run(lib, name, N, H, W, C, K, k, s, reps):
+def run(lib, name, N, H, W, C, K, k, s, reps, modes=("fwd", "dgrad", "wgrad")):
     OH, pt = same_pad(H, k, s)
     OW, pl = same_pad(W, k, s)
     d = _lib.ConvDesc(N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
@@ -51,6 +51,8 @@ def run(lib, name, N, H, W, C, K, k, s, reps):
     }
     out = []
     for mode, fn in calls.items():
+        if mode not in modes:
+            continue
         for _ in range(3):
             _lib.check(fn(), mode)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -68,6 +70,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--math", default="both")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--modes", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     lib = _lib.load()
     modes = {"fp32": [0], "bf16x3": [1], "both": [0, 1]}[a.math]
@@ -75,7 +79,9 @@ def main():
         _lib.check(lib.tde_set_conv_math(m))
         print(f"== math {'fp32' if m == 0 else 'bf16x3'}")
         for sh in SHAPES:
-            res = run(lib, *sh, a.reps)
+            if a.shapes and sh[0] not in a.shapes.split(","):
+                continue
+            res = run(lib, *sh, a.reps, a.modes.split(","))
             print(f"{sh[0]:12s} " + "  ".join(f"{mode} {ms * 1e3:7.1f}us {tf:6.1f}TF" for mode, ms, tf in res),
                   flush=True)
 

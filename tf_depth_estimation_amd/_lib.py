@@ -94,7 +94,7 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("TDE_LIBRARY") or LIB_PATH   # override: A/B of kernel build variants
     if not os.path.exists(path):
         raise TdeError(f"libtde.so not built at {path}: run `make -C tf_depth_estimation_amd/csrc` "
                        "or __graft_entry__.build()")
