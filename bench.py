@@ -291,6 +291,15 @@ def main():
             "kernel_breakdown_ms": {k: round(v[0], 4) for k, v in sorted(fam.items())},
             "final_loss": loss,
         }
+        tr_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.math}_b{N}.json")
+        if os.path.exists(tr_path):
+            # HBM bytes from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload (scripts/pmc.sh,
+            # a separate profiled run: counters cannot be read inside this timed process)
+            with open(tr_path) as fh:
+                conv_t = json.load(fh)["families"].get("conv", {})
+            out["roofline"]["traffic"] = conv_t.get("hbm_bytes_per_step")
+            out["roofline"]["traffic_unit"] = "bytes per step, conv family (igemm + split-K reduce)"
+            out["roofline"]["traffic_source"] = os.path.relpath(tr_path, ROOT)
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] timing CPU baseline ...")
             out["cpu_baseline"] = cpu_baseline(args.workload, N)
