@@ -20,6 +20,8 @@
 // float atomics).
 #include "tde_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
@@ -519,12 +521,31 @@ static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, lon
 
 static int g_conv_math = 0;   // 0: exact fp32 MFMA, 1: bf16x3 (process-wide, see tde_set_conv_math)
 
+// Split-K policy (environment overrides are for tuning experiments; read once at load time).
+static long env_long(const char* name, long dflt) {
+  const char* v = getenv(name);
+  return v ? atol(v) : dflt;
+}
+static const long g_split_target = env_long("TDE_SPLIT_TARGET", 512);   // blocks to aim for
+static const long g_split_minkt = env_long("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
+static const long g_split_slab = env_long("TDE_SPLIT_SLAB_MB", 128) << 20;
+
 static Plan make_plan(const tde_conv_desc_t& d, int mode) {
   const int BK = BK3;
   long M, Nn, Kd; int ncls;
   gemm_dims(d, mode, M, Nn, Kd, ncls);
   Plan pl{};
-  pl.bn = Nn <= 16 ? 16 : (Nn <= 32 ? 32 : (Nn <= 64 ? 64 : 128));
+  // N tile: minimise computed columns + a per-tile overhead (~24 columns' worth), so odd widths such
+  // as the decoder concats in DGRAD (68, 132, 260 channels) do not run half-empty 128-wide tiles
+  {
+    static const int cands[] = {16, 32, 48, 64, 96, 128};
+    long best = -1;
+    for (int bn : cands) {
+      const long t = tde_cdiv(Nn, bn);
+      const long cost = t * bn + 24 * t;
+      if (best < 0 || cost < best || (cost == best && bn > pl.bn)) { best = cost; pl.bn = bn; }
+    }
+  }
   pl.bm = 128;
   long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   // WGRAD reduces over every pixel (Kd ~ 1e5): parallelism comes from split-K, so keep the
@@ -536,16 +557,16 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
   const int nkt = tde_cdiv(Kd, BK);
   // split K until ~2 blocks per CU, keeping >= 4 k-tiles (128 reduction elements) per split
   int splits = 1;
-  const long target = 512;
+  const long target = g_split_target;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
-    splits = splits > nkt / 4 ? nkt / 4 : splits;
+    splits = splits > nkt / g_split_minkt ? (int)(nkt / g_split_minkt) : splits;
     if (splits < 1) splits = 1;
     if (splits > 512) splits = 512;
     // keep the fp32 partial slabs under 128 MB
     long rows = mode == MODE_DGRAD ? (long)d.N * d.H * d.W : M;
     long cols = mode == MODE_DGRAD ? d.C : Nn;
-    while (splits > 1 && (long)splits * rows * cols * 4 > (128l << 20)) splits /= 2;
+    while (splits > 1 && (long)splits * rows * cols * 4 > g_split_slab) splits /= 2;
   }
   pl.kt_per = tde_cdiv(nkt, splits);
   pl.splits = tde_cdiv(nkt, pl.kt_per);
@@ -561,7 +582,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
 
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
-  constexpr int WN = BN >= 32 ? 2 : 1;
+  constexpr int WN = BN % 32 == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   if (g_conv_math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
@@ -574,14 +595,18 @@ static void launch_mode(const Plan& pl, const ConvArgs& a, hipStream_t st) {
     switch (pl.bn) {
       case 16: launch_cfg<MODE, 128, 16>(a, grid, st); break;
       case 32: launch_cfg<MODE, 128, 32>(a, grid, st); break;
+      case 48: launch_cfg<MODE, 128, 48>(a, grid, st); break;
       case 64: launch_cfg<MODE, 128, 64>(a, grid, st); break;
+      case 96: launch_cfg<MODE, 128, 96>(a, grid, st); break;
       default: launch_cfg<MODE, 128, 128>(a, grid, st); break;
     }
   } else {
     switch (pl.bn) {
       case 16: launch_cfg<MODE, 64, 16>(a, grid, st); break;
       case 32: launch_cfg<MODE, 64, 32>(a, grid, st); break;
+      case 48: launch_cfg<MODE, 64, 48>(a, grid, st); break;
       case 64: launch_cfg<MODE, 64, 64>(a, grid, st); break;
+      case 96: launch_cfg<MODE, 64, 96>(a, grid, st); break;
       default: launch_cfg<MODE, 64, 128>(a, grid, st); break;
     }
   }
