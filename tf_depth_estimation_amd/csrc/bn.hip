@@ -219,6 +219,120 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
   }
 }
 
+
+// ------------------------------------------------------------------ small-M layers: one kernel each way
+// The deep encoder/decoder levels (12x16 down to 1x1 at batch 8: M <= 2048 rows) are launch-latency
+// bound as three kernels.  Here a block owns 16 channels over ALL rows (4 channel quads x 64 row lanes),
+// so statistics (fp64), finalize and apply happen in one launch with one LDS combine.
+constexpr int SMALL_M = 2048;
+
+__global__ void __launch_bounds__(256) bn_small_fwd_kernel(int M, int C, const float* z, const float* beta,
+                                                           float eps, float decay, int bessel, float* mm,
+                                                           float* mv, float* save_mean, float* save_invstd,
+                                                           float* y, int ycs, int yco, int relu) {
+  __shared__ double sh[2][64][17];
+  __shared__ float s_mu[16], s_is[16];
+  const int qd = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int c = blockIdx.x * 16 + 4 * qd;
+  const bool ok = c < C;
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  if (ok)
+    for (int r = rl; r < M; r += 64) {
+      const f4 v = *reinterpret_cast<const f4*>(z + (long)r * C + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { a[j] += v[j]; b[j] += (double)v[j] * v[j]; }
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { sh[0][rl][4 * qd + j] = a[j]; sh[1][rl][4 * qd + j] = b[j]; }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int cl = threadIdx.x, cc = blockIdx.x * 16 + cl;
+    double s = 0.0, ss = 0.0;
+    for (int l = 0; l < 64; ++l) { s += sh[0][l][cl]; ss += sh[1][l][cl]; }
+    const double mean = s / M;
+    double var = ss / M - mean * mean;
+    if (var < 0) var = 0;
+    const float mu = (float)mean, is = (float)(1.0 / sqrt(var + (double)eps));
+    s_mu[cl] = mu; s_is[cl] = is;
+    if (cc < C) {
+      save_mean[cc] = mu;
+      save_invstd[cc] = is;
+      if (mm) {
+        const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
+        mm[cc] -= (mm[cc] - mu) * (1.f - decay);
+        mv[cc] -= (mv[cc] - (float)vu) * (1.f - decay);
+      }
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  const f4 bt = *reinterpret_cast<const f4*>(beta + c);
+  for (int r = rl; r < M; r += 64) {
+    const f4 v = *reinterpret_cast<const f4*>(z + (long)r * C + c);
+    f4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = (v[j] - s_mu[4 * qd + j]) * s_is[4 * qd + j] + bt[j];
+      o[j] = (relu && t < 0.f) ? 0.f : t;
+    }
+    *reinterpret_cast<f4*>(y + (long)r * ycs + yco + c) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_small_bwd_kernel(int M, int C, const float* z, const float* mean,
+                                                           const float* invstd, const float* beta, const float* dy,
+                                                           int dycs, int dyco, float* dz, float* dbeta, int acc,
+                                                           int relu) {
+  __shared__ double sh[2][64][17];
+  __shared__ float s_mg[16], s_mgx[16];
+  const int qd = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int c = blockIdx.x * 16 + 4 * qd;
+  const bool ok = c < C;
+  f4 mu = {0, 0, 0, 0}, is = {0, 0, 0, 0}, bt = {0, 0, 0, 0};
+  if (ok) {
+    mu = *reinterpret_cast<const f4*>(mean + c);
+    is = *reinterpret_cast<const f4*>(invstd + c);
+    bt = *reinterpret_cast<const f4*>(beta + c);
+  }
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  if (ok)
+    for (int r = rl; r < M; r += 64) {
+      const f4 v = *reinterpret_cast<const f4*>(z + (long)r * C + c);
+      const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (v[j] - mu[j]) * is[j];
+        const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
+        a[j] += g; b[j] += (double)g * xh;
+      }
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { sh[0][rl][4 * qd + j] = a[j]; sh[1][rl][4 * qd + j] = b[j]; }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int cl = threadIdx.x, cc = blockIdx.x * 16 + cl;
+    double s = 0.0, sx = 0.0;
+    for (int l = 0; l < 64; ++l) { s += sh[0][l][cl]; sx += sh[1][l][cl]; }
+    s_mg[cl] = (float)(s / M);
+    s_mgx[cl] = (float)(sx / M);
+    if (cc < C && dbeta) dbeta[cc] = acc ? dbeta[cc] + (float)s : (float)s;
+  }
+  __syncthreads();
+  if (!ok) return;
+  for (int r = rl; r < M; r += 64) {
+    const f4 v = *reinterpret_cast<const f4*>(z + (long)r * C + c);
+    const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
+    f4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (v[j] - mu[j]) * is[j];
+      const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
+      o[j] = is[j] * (g - s_mg[4 * qd + j] - xh * s_mgx[4 * qd + j]);
+    }
+    *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
+  }
+}
+
 int ew_grid(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -241,6 +355,11 @@ int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps,
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) && tde_aligned16(y));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (M <= SMALL_M) {
+    hipLaunchKernelGGL(bn_small_fwd_kernel, dim3((C + 15) / 16), dim3(256), 0, st, M, C, z, beta, eps, decay, bessel,
+                       moving_mean, moving_var, save_mean, save_invstd, y, y_cstride, y_coff, relu);
+    return tde_launch_status();
+  }
   const RowSplit rs = row_split(M, C);
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(rs.chunks), dim3(256), 0, st, M, C, z, nullptr, 0, 0, nullptr,
@@ -269,6 +388,11 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (M <= SMALL_M) {
+    hipLaunchKernelGGL(bn_small_bwd_kernel, dim3((C + 15) / 16), dim3(256), 0, st, M, C, z, save_mean, save_invstd,
+                       beta, dy, dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu);
+    return tde_launch_status();
+  }
   const RowSplit rs = row_split(M, C);
   double* part = static_cast<double*>(ws);
   float* coef = reinterpret_cast<float*>(part + (size_t)rs.chunks * 2 * C);
