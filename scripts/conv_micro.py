@@ -25,10 +25,14 @@ SHAPES = [
     ("icnv6", 8, 6, 8, 1024, 512, 3, 1),
     ("cnv4b", 8, 12, 16, 256, 256, 3, 1),
     ("icnv1", 8, 192, 256, 20, 16, 3, 1),
+    ("cnv7", 8, 3, 4, 512, 512, 3, 2),
+    ("cnv7b", 8, 2, 2, 512, 512, 3, 1),
+    ("icnv7", 8, 2, 2, 1024, 512, 3, 1),
+    ("cnv6b", 8, 3, 4, 512, 512, 3, 1),
 ]
 
 
-def run(lib, name, N, H, W, C, K, k, s, reps, modes=("fwd", "dgrad", "wgrad")):
+def run(lib, name, N, H, W, C, K, k, s, reps, modes=("fwd", "dgrad", "wgrad"), acc=0):
     OH, pt = same_pad(H, k, s)
     OW, pl = same_pad(W, k, s)
     d = _lib.ConvDesc(N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
@@ -36,17 +40,17 @@ def run(lib, name, N, H, W, C, K, k, s, reps, modes=("fwd", "dgrad", "wgrad")):
     x = torch.randn(N, H, W, C, device="cuda")
     w = torch.randn(k, k, C, K, device="cuda") * 0.1
     y = torch.randn(N, OH, OW, K, device="cuda")
-    dx, dw = torch.empty_like(x), torch.empty_like(w)
+    dx, dw = torch.zeros_like(x), torch.zeros_like(w)
     wsz = max(lib.tde_conv2d_workspace_size(ctypes.byref(d), o) for o in range(3))
     ws = torch.empty(wsz // 4 + 16, device="cuda")
     st = _lib.stream_ptr()
     flops = 2.0 * N * OH * OW * K * k * k * C
     calls = {
-        "fwd": lambda: lib.tde_conv2d_fwd(ctypes.byref(d), _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), 0, _lib.ptr(ws),
+        "fwd": lambda: lib.tde_conv2d_fwd(ctypes.byref(d), _lib.ptr(x), _lib.ptr(w), _lib.ptr(y), acc, _lib.ptr(ws),
                                           ws.numel() * 4, st),
-        "dgrad": lambda: lib.tde_conv2d_bwd_data(ctypes.byref(d), _lib.ptr(y), _lib.ptr(w), _lib.ptr(dx), 0,
+        "dgrad": lambda: lib.tde_conv2d_bwd_data(ctypes.byref(d), _lib.ptr(y), _lib.ptr(w), _lib.ptr(dx), acc,
                                                  _lib.ptr(ws), ws.numel() * 4, st),
-        "wgrad": lambda: lib.tde_conv2d_bwd_filter(ctypes.byref(d), _lib.ptr(x), _lib.ptr(y), _lib.ptr(dw), 0,
+        "wgrad": lambda: lib.tde_conv2d_bwd_filter(ctypes.byref(d), _lib.ptr(x), _lib.ptr(y), _lib.ptr(dw), acc,
                                                    _lib.ptr(ws), ws.numel() * 4, st),
     }
     out = []
@@ -72,6 +76,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--modes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--accumulate", type=int, default=0)
     a = ap.parse_args()
     lib = _lib.load()
     modes = {"fp32": [0], "bf16x3": [1], "both": [0, 1]}[a.math]
@@ -81,7 +86,7 @@ def main():
         for sh in SHAPES:
             if a.shapes and sh[0] not in a.shapes.split(","):
                 continue
-            res = run(lib, *sh, a.reps, a.modes.split(","))
+            res = run(lib, *sh, a.reps, a.modes.split(","), a.accumulate)
             print(f"{sh[0]:12s} " + "  ".join(f"{mode} {ms * 1e3:7.1f}us {tf:6.1f}TF" for mode, ms, tf in res),
                   flush=True)
 

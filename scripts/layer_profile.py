@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--workload", default="config2")
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--loss-vs", type=float, default=0.0,
+                    help="also rank conv entries by ms lost against this TFLOP/s reference")
     a = ap.parse_args()
     N = a.batch or bench.WORKLOADS[a.workload][2]
     tr = bench.make_trainer(a.workload, N)
@@ -44,6 +46,13 @@ def main():
     for (fam, tag), (ms, fl, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.top]:
         tf = fl / (ms * 1e-3) / 1e12 if ms > 0 and fl > 0 else 0.0
         print(f"{ms:8.3f} ms {100 * ms / tot:5.1f}%  {fam:11s} {tag:28s} x{n}  {tf:7.2f} TF/s  {fl / 1e9:7.2f} GF")
+    if a.loss_vs > 0:
+        ref = a.loss_vs * 1e12
+        rows = [(ms - fl / ref * 1e3, ms, fam, tag, fl) for (fam, tag), (ms, fl, n) in agg.items()
+                if fam.startswith("conv")]
+        print(f"\nconv ms lost vs {a.loss_vs} TF/s: total {sum(r[0] for r in rows):.3f} ms")
+        for lost, ms, fam, tag, fl in sorted(rows, reverse=True)[:a.top]:
+            print(f"{lost:8.3f} lost {ms:8.3f} ms  {fam:11s} {tag:20s} {fl / (ms * 1e-3) / 1e12:7.2f} TF/s")
 
 
 if __name__ == "__main__":

@@ -419,48 +419,61 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
     }
   }
 
-  // ---- epilogue (16x16 C/D map is dtype-independent on gfx950)
+  // ---- epilogue (16x16 C/D map is dtype-independent on gfx950).  Row addresses first; when
+  // accumulating into the destination, ALL old values are loaded before any store (a store may alias a
+  // later load, so an interleaved read-modify-write would serialise one memory latency per element).
   const bool direct = (p.splits == 1);
+  float* base;
+  if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
+  else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
+  else base = direct ? p.dw : p.ws;
+  long rowaddr[TM][4];
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wrow0 + a * 16 + 4 * q + r;
-      if (m >= M) continue;
-      long rowaddr;
-      bool rowok = true;
-      if constexpr (MODE == MODE_FWD) {
-        rowaddr = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
-      } else if constexpr (MODE == MODE_DGRAD) {
-        const int hw = g.HH * g.WW;
-        const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
-        const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
-        rowaddr = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
-      } else {
-        if (direct) {
-          const int tap = m / p.C, c = m - tap * p.C;
-          rowok = c < p.wcin;
-          rowaddr = (long)(tap * p.wcin + c) * p.K;
+      long ra_ = -1;
+      if (m < M) {
+        if constexpr (MODE == MODE_FWD) {
+          ra_ = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
+        } else if constexpr (MODE == MODE_DGRAD) {
+          const int hw = g.HH * g.WW;
+          const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
+          const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
+          ra_ = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
         } else {
-          rowaddr = ((long)zsplit * M + m) * Nn;
+          if (direct) {
+            const int tap = m / p.C, c = m - tap * p.C;
+            if (c < p.wcin) ra_ = (long)(tap * p.wcin + c) * p.K;
+          } else {
+            ra_ = ((long)zsplit * M + m) * Nn;
+          }
         }
       }
-      if (!rowok) continue;
-      float* base;
-      if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
-      else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
-      else base = direct ? p.dw : p.ws;
+      rowaddr[a][r] = ra_;
+    }
+  }
+  if (direct && p.accumulate) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int n = n0 + wcol0 + b * 16 + r16;
+          if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + n];
+        }
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wcol0 + b * 16 + r16;
-        if (n < Nn) {
-          float* dst = base + rowaddr + n;
-          const float v = acc[a][b][r];
-          *dst = (direct && p.accumulate) ? (*dst + v) : v;
-        }
+        if (rowaddr[a][r] >= 0 && n < Nn) base[rowaddr[a][r] + n] = acc[a][b][r];
       }
-    }
-  }
 }
 
 // Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col]

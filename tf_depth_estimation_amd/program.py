@@ -243,8 +243,8 @@ class NetProgram:
         self._sizes = {}
         self.timer = None
 
-    def _span(self, family, flops=0.0):
-        return NO_SPAN if self.timer is None else self.timer.span(family, flops)
+    def _span(self, family, flops=0.0, nbytes=0.0):
+        return NO_SPAN if self.timer is None else self.timer.span(family, flops, nbytes)
 
     # ---------------------------------------------------------------- helpers
     def P(self, name):
@@ -296,7 +296,7 @@ class NetProgram:
                 z = run.z[i] if op.bn else None
                 if not op.bn:
                     raise NotImplementedError("BN-free conv/deconv layers")
-                with self._span("conv_fwd", conv_flops(op, N)):
+                with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
                     if op.deconv:
                         _lib.check(lib.tde_deconv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws),
                                                         wsb, st), op.layer)
@@ -334,11 +334,14 @@ class NetProgram:
         return [run.view_tensor(v) for v in spec.outputs]
 
     # ---------------------------------------------------------------- backward
-    def backward(self, run, grad_outputs, need_input_grad=False, on_grads=None):
+    def backward(self, run, grad_outputs, need_input_grad=False, on_grads=None, grad_accumulate=True):
         """grad_outputs: list (aligned with spec.outputs) of tensors or None.  Accumulates parameter
-        gradients into chunk.grad.  Returns d(input) if requested.  on_grads(names), if given, is
-        called after each op with the full variable names whose gradient that op just wrote (the
-        data-parallel exchange launches a bucket once all its parameters are final, ddp.py)."""
+        gradients into chunk.grad, or with grad_accumulate=False OVERWRITES them (every parameter is
+        written by one backward call, so a trainer's first call of the step needs no zeroed buffer
+        and the kernels skip the read-modify-write).  Returns d(input) if requested.  on_grads(names),
+        if given, is called after each op with the full variable names whose gradient that op just
+        wrote (the data-parallel exchange launches a bucket once all its parameters are final, ddp.py)."""
+        pacc = 1 if grad_accumulate else 0
         N = run.N
         lib = _lib.load()
         st = _lib.stream_ptr()
@@ -382,27 +385,27 @@ class NetProgram:
                     _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
                                               ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
                                               op.dst.buf.cs, op.dst.coff, ptr(dz),
-                                              ptr(self.G(f"{op.layer}/BatchNorm/beta")), 1, 1, ptr(ws), wsb, st),
+                                              ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws), wsb, st),
                                op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
                 if op.deconv:
-                    with self._span("conv_wgrad", fl):
-                        _lib.check(lib.tde_deconv2d_bwd_filter(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(gw), 1,
+                    with self._span("conv_wgrad", fl, conv_bytes(op, N)):
+                        _lib.check(lib.tde_deconv2d_bwd_filter(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(gw), pacc,
                                                                ptr(ws), wsb, st), op.layer + " wgrad")
                     if src_needs:
                         acc = mark(op.src)
-                        with self._span("conv_dgrad", fl):
+                        with self._span("conv_dgrad", fl, conv_bytes(op, N)):
                             _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w),
                                                                  run.vptr(op.src, True), acc, ptr(ws), wsb, st),
                                        op.layer + " dgrad")
                 else:
-                    with self._span("conv_wgrad", fl):
-                        _lib.check(lib.tde_conv2d_bwd_filter(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(gw), 1,
+                    with self._span("conv_wgrad", fl, conv_bytes(op, N)):
+                        _lib.check(lib.tde_conv2d_bwd_filter(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(gw), pacc,
                                                              ptr(ws), wsb, st), op.layer + " wgrad")
                     if src_needs:
                         acc = mark(op.src)
-                        with self._span("conv_dgrad", fl):
+                        with self._span("conv_dgrad", fl, conv_bytes(op, N)):
                             _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
                                                                acc, ptr(ws), wsb, st), op.layer + " dgrad")
                 if on_grads is not None:
@@ -415,7 +418,7 @@ class NetProgram:
                                                 run.vptr(op.dst), run.vptr(op.dst, True),
                                                 run.vptr(op.src, True) if src_needs else None, acc,
                                                 ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")),
-                                                1, op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
+                                                pacc, op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
                 if on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Resize):
@@ -447,8 +450,10 @@ class KernelTimer:
     def __init__(self):
         self.spans = []   # (family, start_event, end_event, flops, tag)
         self.tag = None   # set by the executor to the current layer name
+        self.nbytes = {}  # family -> algorithmic bytes
 
-    def span(self, family, flops=0.0):
+    def span(self, family, flops=0.0, nbytes=0.0):
+        self.nbytes[family] = self.nbytes.get(family, 0.0) + nbytes
         return _Span(self, family, flops)
 
     def totals(self):
@@ -489,6 +494,20 @@ class _NoSpan:
 
 
 NO_SPAN = _NoSpan()
+
+
+def conv_bytes(op, N):
+    """Algorithmic HBM bytes of one conv / deconv call in any of its three modes: each reads two of
+    {x, w, y} and writes the third, once (fp32)."""
+    if not isinstance(op, ConvBN):
+        return 0.0
+    if op.deconv:
+        x = N * op.dst.H * op.dst.W * op.K
+        y = N * op.src.H * op.src.W * op.src.creal
+    else:
+        x = N * op.src.H * op.src.W * op.src.creal
+        y = N * op.OH * op.OW * op.K
+    return 4.0 * (x + y + op.k * op.k * op.src.creal * op.K)
 
 
 def conv_flops(op, N):

@@ -47,7 +47,7 @@ class AllReduceGrads:
 
 
 class Trainer:
-    """Common capture/replay machinery.  A step is phase_compute (zero grads, fwd, loss, bwd),
+    """Common capture/replay machinery.  A step is phase_compute (fwd, loss, bwd -- the first backward call of a chunk overwrites its gradients),
     the optional gradient exchange, then phase_update (Adam).  Without an exchange the whole step is
     one hipGraph.  With a ddp.GradSync, backward reports finished parameters and each full bucket's
     RCCL all-reduce is launched on a side stream while backward continues; under capture, every
@@ -191,8 +191,6 @@ class DepthOnlyTrainer(Trainer):
 
     def phase_compute(self):
         lib, st = _lib.load(), _lib.stream_ptr()
-        c = self.chunk
-        _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
         _lib.check(lib.tde_zero_bytes(16, ptr(self.parts), st), "zero loss")
         for g in self.d_out:
             _lib.check(lib.tde_zero_bytes(g.numel() * 4, ptr(g), st), "zero dout")
@@ -210,7 +208,8 @@ class DepthOnlyTrainer(Trainer):
                                             1, 0, st), "smooth")
             _lib.check(lib.tde_loss_l1(N, h, w, ptr(pred), 1, 0, ptr(self.label_pyr[s]), 0, self.w["depth"] / 2 ** s,
                                        p_depth, ptr(g), 1, 0, st), "depth l1")
-        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
+        # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
 
     def total_loss(self):
         return float(self.parts.sum().item())
@@ -312,8 +311,6 @@ class DepthThenCamTrainer(Trainer):
         lib, st = _lib.load(), _lib.stream_ptr()
         B, H, W, w = self.N, self.H, self.W, self.w
         M = B * H * W
-        for c in self.chunks:
-            _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
         self._zero(self.acc, self.gP["lr"], self.gP["rl"], self.gT["lr"], self.gT["rl"],
                    *[g for v in self.d_out.values() for g in v])
         # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
@@ -358,8 +355,11 @@ class DepthThenCamTrainer(Trainer):
             gpp = self.d_out[run_key][4]
             _lib.check(lib.tde_spatial_mean_bwd(B, gpp.shape[1] * gpp.shape[2], 6, ptr(gpp), 6, 0,
                                                 ptr(self.g_pose[d]), st), "pose mean bwd")
-        for k, prog in (("pr", self.pair), ("pl", self.pair), ("sr", self.single), ("sl", self.single)):
-            prog.backward(self.runs[k], self.d_out[k], on_grads=self.hook(prog.chunk))
+        # each net runs twice (shared variables): the first backward call overwrites its gradients,
+        # the second accumulates -- no zeroed gradient buffer needed
+        for k, prog, first in (("pr", self.pair, True), ("pl", self.pair, False), ("sr", self.single, True),
+                               ("sl", self.single, False)):
+            prog.backward(self.runs[k], self.d_out[k], on_grads=self.hook(prog.chunk), grad_accumulate=not first)
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
@@ -421,8 +421,6 @@ class OptflowCombineTrainer(Trainer):
         lib, st = _lib.load(), _lib.stream_ptr()
         B, H, W, w = self.N, self.H, self.W, self.w
         M = B * H * W
-        c = self.prog.chunk
-        _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
         self._zero(self.acc, *self.d_out)
         _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["l"]), 3, 0, ptr(self.pair_in), 6, 0, 0, st), "concat")
         _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["r"]), 3, 0, ptr(self.pair_in), 6, 3, 0, st), "concat")
@@ -451,7 +449,8 @@ class OptflowCombineTrainer(Trainer):
                          photo_w=w["data"] * ws, g_flow=gf)                              # :191-198
             Ls.l1(flow, self.gflow[s][0], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=0)   # :205-207
             Ls.l1(flow, self.gflow[s][1], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=1)   # :209-210
-        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
+        # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
 
     def total_loss(self):
         return float(self.acc.sum().item())
@@ -504,8 +503,6 @@ class RefineTrainer(Trainer):
     def phase_compute(self):
         from . import losses as Ls
         lib, st = _lib.load(), _lib.stream_ptr()
-        c = self.prog.chunk
-        _lib.check(lib.tde_zero_bytes(c.numel * 4, ptr(c.grad), st), "zero grad")
         self._zero(self.acc, *self.d_out)
         out = self.prog.forward(self.run, self.x1)
         for s in range(1, 4):
@@ -520,7 +517,8 @@ class RefineTrainer(Trainer):
             Ls.warp_loss(self.acc, S["photo"], self.pyr2[s], self.pyr1[s], P=self.P[s], Kinv=self.Kinv[s],
                          disp=disp, photo_w=1.0, g_disp=g)                                  # :200-212
             Ls.l1(disp, self.gt_pyr[s], g, w["data"] / 2 ** s, self.acc, S["depth"])         # :210-213
-        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk))
+        # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
+        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
 
     def total_loss(self):
         return float(self.acc.sum().item())
