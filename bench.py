@@ -217,7 +217,7 @@ def main():
             tr.enable_ddp(world, bucket_mb=args.bucket_mb)
         else:
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
-    progs = [p for p in (getattr(tr, "prog", None), getattr(tr, "single", None), getattr(tr, "pair", None)) if p]
+    progs = tr.programs()
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
     tr.step_eager()

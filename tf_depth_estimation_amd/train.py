@@ -14,6 +14,11 @@ from .program import NetRun
 
 W_CONFIG2 = dict(smooth=1.0, depth=1.0)     # train_depth_only.py:33-37
 
+# Thread-local capture: RCCL's watchdog thread polls the events of earlier collectives while a step is
+# being recorded; under the default "global" mode that poll is an illegal call during capture and
+# aborts the process (hipErrorStreamCaptureUnsupported).
+CAPTURE_MODE = "thread_local"
+
 
 class Adam:
     """tf.train.AdamOptimizer(lr, beta1) over one ParamChunk (flat buffers)."""
@@ -63,7 +68,12 @@ class Trainer:
         from .ddp import GradSync
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
+        self.grad_sync.producers = self.programs()
         return self.grad_sync
+
+    def programs(self):
+        return [p for p in (getattr(self, "prog", None), getattr(self, "single", None), getattr(self, "pair", None))
+                if p is not None]
 
     def hook(self, chunk):
         """on_grads callback for NetProgram.backward (None without an overlapped exchange)."""
@@ -90,16 +100,16 @@ class Trainer:
         gs = self.grad_sync
         if gs is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 self.phase_compute()
                 self.phase_update()
             self.graphs = [g]
             return self.graphs
         if not hasattr(gs, "begin_step"):       # plain exchange after backward
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
+            with torch.cuda.graph(g1, capture_error_mode=CAPTURE_MODE):
                 self.phase_compute()
-            with torch.cuda.graph(g2):
+            with torch.cuda.graph(g2, capture_error_mode=CAPTURE_MODE):
                 self.phase_update()
             self.graphs = [g1, g2]
             return self.graphs
@@ -111,21 +121,23 @@ class Trainer:
         state = {"g": torch.cuda.CUDAGraph()}
 
         def cut(buckets):
+            for p in self.programs():       # join the WGRAD branch before closing the segment
+                p.join()
             state["g"].capture_end()
             segs.append((state["g"], list(buckets)))
             state["g"] = torch.cuda.CUDAGraph()
-            state["g"].capture_begin(pool=pool)
+            state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
 
         gs.begin_step()
         gs.capturing = cut
         try:
             with torch.cuda.stream(cs):
-                state["g"].capture_begin(pool=pool)
+                state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                 self.phase_compute()
                 state["g"].capture_end()
                 segs.append((state["g"], gs.leftovers()))
                 upd = torch.cuda.CUDAGraph()
-                upd.capture_begin(pool=pool)
+                upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                 self.phase_update()
                 upd.capture_end()
         finally:
