@@ -19,6 +19,10 @@
  *     the host and is safe to capture in a hipGraph.  Re-entrant across streams.
  *   - Return value: TDE_OK (0) or a negative tde_status.
  *   - `ws` / `ws_bytes`: caller-provided device workspace; size it with the *_workspace_size query.
+ *     Its first TDE_WS_HEADER_BYTES hold tile-arrival counters (the split-K and batch-norm
+ *     reductions finish inside the producing kernel: the last block of a tile to arrive reduces, in
+ *     a fixed order, so results stay deterministic).  Zero a workspace ONCE after allocating it
+ *     (tde_zero_bytes); every call leaves the counters zero again.  One workspace per stream.
  */
 #ifndef TDE_H_
 #define TDE_H_
@@ -30,7 +34,8 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 1
+#define TDE_ABI_VERSION 2
+#define TDE_WS_HEADER_BYTES 65536
 
 typedef enum {
   TDE_OK = 0,
@@ -74,6 +79,25 @@ int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw,
                           int accumulate, void* ws, size_t ws_bytes, void* stream);
 
+/* conv + training-mode batch norm + ReLU in one call: slim.conv2d / conv2d_transpose with
+ * normalizer_fn=batch_norm (arg_scope nets_optflow_depth.py:82-87; same semantics as
+ * tde_bn_fwd_train).  z = conv(x) is written densely (the backward needs it); the BN pass reads the
+ * conv's split-K partials directly (no separate reduce launch), computes the batch statistics (fp64,
+ * fixed order), updates moving_mean / moving_var (both NULL: no update) and writes
+ * y = relu?((z - mean) * invstd + beta) into the channel view (y, y_cstride, y_coff). */
+typedef struct {
+  const float* beta;
+  float eps, decay;
+  int bessel;
+  float* moving_mean; float* moving_var;
+  float* save_mean; float* save_invstd;
+  float* y; int y_cstride, y_coff;
+  int relu;
+} tde_bn_train_t;
+/* z dense [N*OH*OW][K] (y_cstride == K, y_coff == 0 in d).  Workspace: tde_conv2d_workspace_size(d, 3). */
+int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z,
+                      const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream);
+
 /* slim.conv2d_transpose (stride 2, SAME), nets_optflow_depth.py:103,109,114,119,126,133,140.
  * `d` is the virtual forward conv (see above); x = deconv input, y = deconv output.
  *   fwd       : y_big  = Conv2DBackpropInput(x_small)     (weights [KH][KW][Cout][Cin])
@@ -82,6 +106,9 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
 size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op);
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* deconv forward + BN + ReLU: z_big dense [N*H*W][C] (x_cstride == C, x_coff == 0); workspace op 3. */
+int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
+                        const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream);
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w,
                           float* dx_small, int accumulate, void* ws, size_t ws_bytes, void* stream);
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small,
@@ -150,6 +177,28 @@ int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int co
 int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, const float* label,
                 int nonfinite, float weight, double* loss, float* grad, int g_cstride, int g_coff,
                 void* stream);
+
+/* The per-scale smooth + depth-L1 terms of every scale in ONE launch (train_depth_only.py:160-187;
+ * the same terms inside train_depth_then_cam_lr.py:216-243, refine_depth.py:185-213):
+ *   loss_smooth += sum_s smooth_w[s] * compute_smooth_loss(pred_s or 1/pred_s)
+ *   loss_l1     += sum_s l1_w[s] * mean|nf(resize_area(label, 2^-s) - pred_s)|
+ * pred_s / grad_s are 1-channel views at (H >> s, W >> s); label is the full-resolution [N,H,W,1]
+ * (area-downsampled on the fly, H and W divisible by 2^s).  A zero weight disables a term.
+ * grad_accumulate = 0 WRITES every grad_s pixel (no zeroed buffer needed), 1 adds. */
+#define TDE_MAX_SCALES 4
+typedef struct {
+  int N, H, W, nscales;
+  const float* pred[TDE_MAX_SCALES]; int pred_cs[TDE_MAX_SCALES], pred_co[TDE_MAX_SCALES];
+  float* grad[TDE_MAX_SCALES]; int g_cs[TDE_MAX_SCALES], g_co[TDE_MAX_SCALES];
+  float smooth_w[TDE_MAX_SCALES];
+  int recip;
+  const float* label;
+  int nonfinite;
+  float l1_w[TDE_MAX_SCALES];
+  double* loss_smooth; double* loss_l1;
+  int grad_accumulate;
+} tde_depth_loss_t;
+int tde_loss_depth_pyramid(const tde_depth_loss_t* args, void* stream);
 
 /* ---------------------------------------------------------------- projective warp loss head
  * Fused forward + hand-derived backward of the per-scale self-supervised terms of

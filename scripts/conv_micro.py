@@ -42,7 +42,7 @@ def run(lib, name, N, H, W, C, K, k, s, reps, modes=("fwd", "dgrad", "wgrad"), a
     y = torch.randn(N, OH, OW, K, device="cuda")
     dx, dw = torch.zeros_like(x), torch.zeros_like(w)
     wsz = max(lib.tde_conv2d_workspace_size(ctypes.byref(d), o) for o in range(3))
-    ws = torch.empty(wsz // 4 + 16, device="cuda")
+    ws = torch.zeros(wsz // 4 + 16, device="cuda")
     st = _lib.stream_ptr()
     flops = 2.0 * N * OH * OW * K * k * k * C
     calls = {

@@ -68,8 +68,8 @@ def conv_desc(L, **kw):
 def ws_for(L, d, deconv=False):
     lib = L.load()
     q = lib.tde_deconv2d_workspace_size if deconv else lib.tde_conv2d_workspace_size
-    n = max(q(ctypes.byref(d), o) for o in range(3))
-    return torch.empty(max(n // 4 + 16, 16), device="cuda")
+    n = max(q(ctypes.byref(d), o) for o in range(4))
+    return torch.zeros(max(n // 4 + 16, 16), device="cuda")   # header counters start at zero
 
 
 CONV_CASES = [
@@ -178,6 +178,82 @@ def test_deconv2d_fwd_bwd(L, case, conv_tol):
     close(gdw, wr.grad, tol=tol, what="deconv wgrad")
 
 
+BN_FUSED_CASES = [
+    # deconv?, N, H, W, C(in view), K, k, s      (conv: input H x W;  deconv: input h x w, output 2h x 2w)
+    (False, 8, 96, 128, 4, 32, 7, 2),            # cnv1: 768 row tiles, no split
+    (False, 8, 2, 2, 512, 512, 3, 1),            # cnv7b-like: split-K 36, last-block reduce
+    (False, 4, 24, 32, 256, 128, 3, 1),          # split-K with several row tiles
+    (False, 3, 13, 17, 32, 64, 5, 2),            # ragged tiles
+    (True, 2, 6, 8, 32, 16, 3, 2),               # deconv: 4 parity classes
+    (True, 8, 1, 1, 512, 512, 3, 2),             # upcnv7-like (1x1 -> 2x2), split-K over classes
+    (True, 2, 3, 4, 64, 32, 7, 2),               # k7 deconv: classes with different tap counts
+    (True, 4, 24, 32, 64, 32, 3, 2),             # deconv, split-K, BN partials from the reduce kernel
+    (True, 8, 48, 64, 32, 16, 3, 2),             # deconv, no split, BN partials from the epilogue
+    (False, 8, 48, 64, 64, 64, 5, 1),            # cnv2b-like: split-K + reduce-kernel partials
+]
+
+
+@pytest.mark.parametrize("case", BN_FUSED_CASES)
+def test_conv_fused_bn_relu(L, case):
+    """tde_conv2d_fwd_bn / tde_deconv2d_fwd_bn (conv + training BN + ReLU, split-K partials consumed by
+    the BN pass): z equals the plain conv, batch statistics and moving averages equal the fp64
+    statistics of z (tde_bn_fwd_train semantics), y = relu(BN(z)) in an offset channel view, and a second
+    call is bit-identical (fixed reduction order)."""
+    deconv, N, H, W, C, K, k, s = case
+    lib = L.load()
+    st = L.stream_ptr()
+    if deconv:
+        cin, cout = C, K
+        OHb, OWb = 2 * H, 2 * W
+        _, pt, _ = T.same_pad(OHb, k, 2)
+        _, pl, _ = T.same_pad(OWb, k, 2)
+        d = conv_desc(L, N=N, H=OHb, W=OWb, C=cout, OH=H, OW=W, K=cin, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
+                      w_cin=cout, x_cstride=cout, x_coff=0, y_cstride=cin, y_coff=0)
+        x = rnd(N, H, W, cin, seed=21)
+        w = rnd(k, k, cout, cin, seed=22) * 0.2
+        zr = T.conv2d_transpose_same(x, w, 2)
+        fn = lib.tde_deconv2d_fwd_bn
+        q = lib.tde_deconv2d_workspace_size
+    else:
+        OH, pt, _ = T.same_pad(H, k, s)
+        OW, pl, _ = T.same_pad(W, k, s)
+        d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
+                      w_cin=C, x_cstride=C, x_coff=0, y_cstride=K, y_coff=0)
+        x = rnd(N, H, W, C, seed=21)
+        w = rnd(k, k, C, K, seed=22) * 0.2
+        zr = T.conv2d_same(x, w, s)
+        fn = lib.tde_conv2d_fwd_bn
+        q = lib.tde_conv2d_workspace_size
+    Kc = zr.shape[-1]
+    M = zr.numel() // Kc
+    ws = torch.zeros(q(ctypes.byref(d), 3) // 4 + 16, device="cuda")
+    gx, gw = dev(x), dev(w)
+    beta = dev(rnd(Kc, seed=23) * 0.2)
+    mm, mv = torch.zeros(Kc, device="cuda"), torch.ones(Kc, device="cuda")
+    sm = torch.empty(2, Kc, device="cuda")
+    z = torch.empty(zr.shape, device="cuda")
+    ycs, yco = Kc + 8, 4
+    y = torch.zeros(M, ycs, device="cuda")
+    bn = L.BnTrain(L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(y), ycs, yco, 1)
+    L.check(fn(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(z), ctypes.byref(bn), L.ptr(ws), ws.numel() * 4, st))
+    close(z, zr, what="z")
+    z64 = zr.double().reshape(M, Kc)
+    mean, var = z64.mean(0), z64.var(0, unbiased=False)
+    close(sm[0], mean, tol=1e-5, what="batch mean")
+    close(sm[1], 1.0 / torch.sqrt(var + 1e-3), tol=1e-5, what="batch invstd")
+    close(mm, 0.01 * mean, tol=1e-5, what="moving mean")
+    close(mv, 0.99 + 0.01 * var * M / (M - 1), tol=1e-5, what="moving var")
+    ref = torch.relu((z.reshape(M, Kc) - sm[0]) * sm[1] + beta)
+    close(y[:, yco:yco + Kc], ref, what="bn+relu")
+    assert float(y[:, :yco].abs().sum()) == 0.0 and float(y[:, yco + Kc:].abs().sum()) == 0.0
+    assert int(ws[:16384].count_nonzero()) == 0, "workspace header counters must stay zero"
+    # determinism: same inputs, same bits (no moving-average update this time)
+    z2, sm2, y2 = torch.empty_like(z), torch.empty_like(sm), torch.zeros_like(y)
+    bn2 = L.BnTrain(L.ptr(beta), 1e-3, 0.99, 1, None, None, L.ptr(sm2[0]), L.ptr(sm2[1]), L.ptr(y2), ycs, yco, 1)
+    L.check(fn(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(z2), ctypes.byref(bn2), L.ptr(ws), ws.numel() * 4, st))
+    assert torch.equal(z, z2) and torch.equal(sm, sm2) and torch.equal(y, y2)
+
+
 HEAD_CASES = [
     # N, H, W, C, K, k, act, scale, offset, x_cs, x_co
     (2, 12, 16, 16, 1, 3, 1, 4.0, 0.0, 16, 0),
@@ -214,7 +290,7 @@ def test_head_fwd_bwd(L, case):
     yr.backward(dy)
     gdx = torch.zeros(N, H, W, xcs, device="cuda")
     gdw, gdb = torch.empty_like(gw), torch.empty_like(gb)
-    ws = torch.empty(lib.tde_head_workspace_size(ctypes.byref(d)) // 4 + 16, device="cuda")
+    ws = torch.zeros(lib.tde_head_workspace_size(ctypes.byref(d)) // 4 + 16, device="cuda")
     L.check(lib.tde_head_bwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(gy), L.ptr(dev(dy)), L.ptr(gdx), 0,
                              L.ptr(gdw), L.ptr(gdb), 0, act, scale, offset, L.ptr(ws), ws.numel() * 4, st))
     close(gdx[..., xco:xco + C], xr.grad, tol=3e-5, what="head dgrad")
@@ -223,7 +299,7 @@ def test_head_fwd_bwd(L, case):
 
 
 @pytest.mark.parametrize("M,C,ycs,yco", [(8 * 96 * 128, 32, 68, 32), (32, 512, 1024, 512), (8 * 12 * 16, 256, 256, 0),
-                                         (2048, 20, 24, 4), (2049, 20, 20, 0), (8, 1024, 1024, 0)])
+                                         (2048, 20, 24, 4), (2049, 20, 20, 0), (8, 1024, 1024, 0), (8193, 64, 64, 0)])
 def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     lib = L.load()
     st = L.stream_ptr()
@@ -234,7 +310,7 @@ def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     mv = torch.ones(C, device="cuda")
     sm = torch.empty(2, C, device="cuda")
     y = torch.zeros(M, ycs, device="cuda")
-    ws = torch.empty(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
+    ws = torch.zeros(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
     L.check(lib.tde_bn_fwd_train(M, C, L.ptr(gz), L.ptr(gb), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
                                  L.ptr(sm[1]), L.ptr(y), ycs, yco, 1, L.ptr(ws), ws.numel() * 4, st))
     zr = z.clone().reshape(1, 1, M, C).requires_grad_(True)
@@ -353,3 +429,52 @@ def test_adam_matches_tf_form(L):
                                     1e-8, L.stream_ptr()))
         opt.step(pr, {"p": g})
     close(gp - dev(p0), pr["p"] - p0, tol=1e-4, what="adam delta")
+
+
+@pytest.mark.parametrize("recip,nonfinite,acc", [(0, 0, 0), (1, 1, 1), (0, 1, 0)])
+def test_loss_depth_pyramid_matches_separate_terms(L, recip, nonfinite, acc):
+    """tde_loss_depth_pyramid (all scales, one launch) == tde_resize_area_fwd + tde_loss_smooth2 +
+    tde_loss_l1 per scale, values and gradients, including the write (acc=0) and add modes."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, H, W = 2, 24, 32
+    preds = [dev(rnd(N, H >> s, W >> s, 3, seed=40 + s, lo=0.2, hi=2.0)) for s in range(4)]
+    label = rnd(N, H, W, 1, seed=50, lo=0.25, hi=4.0)
+    if nonfinite:
+        label[0, 3, 5, 0] = float("nan")
+        label[1, 10, 7, 0] = float("inf")
+    glab = dev(label)
+    base = [dev(rnd(N, H >> s, W >> s, 2, seed=60 + s)) for s in range(4)]
+    sw, lw = [1.0, 0.5, 0.25, 0.125], [0.7, 0.35, 0.0, 0.1]
+    # reference: separate kernels
+    ref_g = [b.clone() if acc else torch.zeros_like(b) for b in base]
+    ref_loss = torch.zeros(2, dtype=torch.float64, device="cuda")
+    for s in range(4):
+        h, w = H >> s, W >> s
+        lab_s = torch.empty(N, h, w, 1, device="cuda")
+        L.check(lib.tde_resize_area_fwd(N, H, W, 1, L.ptr(glab), h, w, L.ptr(lab_s), st))
+        p = preds[s]
+        L.check(lib.tde_loss_smooth2(N, h, w, L.ptr(p), 3, 1, recip, sw[s], ctypes.c_void_p(ref_loss.data_ptr()),
+                                     L.ptr(ref_g[s]), 2, 1, st))
+        if lw[s]:
+            L.check(lib.tde_loss_l1(N, h, w, L.ptr(p), 3, 1, L.ptr(lab_s), nonfinite, lw[s],
+                                    ctypes.c_void_p(ref_loss.data_ptr() + 8), L.ptr(ref_g[s]), 2, 1, st))
+    got_g = [b.clone() for b in base]
+    loss = torch.zeros(2, dtype=torch.float64, device="cuda")
+    a = L.DepthLoss()
+    a.N, a.H, a.W, a.nscales = N, H, W, 4
+    for s in range(4):
+        a.pred[s] = preds[s].data_ptr()
+        a.pred_cs[s], a.pred_co[s] = 3, 1
+        a.grad[s] = got_g[s].data_ptr()
+        a.g_cs[s], a.g_co[s] = 2, 1
+        a.smooth_w[s], a.l1_w[s] = sw[s], lw[s]
+    a.recip, a.nonfinite, a.grad_accumulate = recip, nonfinite, acc
+    a.label = glab.data_ptr()
+    a.loss_smooth, a.loss_l1 = loss.data_ptr(), loss.data_ptr() + 8
+    L.check(lib.tde_loss_depth_pyramid(ctypes.byref(a), st))
+    for s in range(4):
+        close(got_g[s][..., 1], ref_g[s][..., 1], what=f"grad scale {s}")
+        close(got_g[s][..., 0], base[s][..., 0], what=f"untouched channel scale {s}")
+    close(loss, ref_loss, tol=1e-6, what="loss values")
+

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int, c_float, c_size_t, c_void_p, c_double_p = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p,
                                                   ctypes.POINTER(ctypes.c_double))
@@ -27,6 +27,13 @@ class ConvDesc(ctypes.Structure):
 P = c_void_p
 
 
+class BnTrain(ctypes.Structure):
+    """Mirror of tde_bn_train_t (include/tde.h): batch norm + ReLU fused behind a conv."""
+    _fields_ = [("beta", P), ("eps", c_float), ("decay", c_float), ("bessel", c_int), ("moving_mean", P),
+                ("moving_var", P), ("save_mean", P), ("save_invstd", P), ("y", P), ("y_cstride", c_int),
+                ("y_coff", c_int), ("relu", c_int)]
+
+
 class WarpLossArgs(ctypes.Structure):
     """Mirror of tde_warp_loss_t (include/tde.h)."""
     _fields_ = [("B", c_int), ("H", c_int), ("W", c_int),
@@ -39,7 +46,17 @@ class WarpLossArgs(ctypes.Structure):
                 ("loss", P), ("g_disp", P), ("g_flow", P), ("g_logits", P), ("g_other", P), ("g_P", P)]
 
 
+class DepthLoss(ctypes.Structure):
+    """Mirror of tde_depth_loss_t (include/tde.h): the multi-scale smooth + depth-L1 loss head."""
+    _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("nscales", c_int),
+                ("pred", P * 4), ("pred_cs", c_int * 4), ("pred_co", c_int * 4),
+                ("grad", P * 4), ("g_cs", c_int * 4), ("g_co", c_int * 4),
+                ("smooth_w", c_float * 4), ("recip", c_int), ("label", P), ("nonfinite", c_int),
+                ("l1_w", c_float * 4), ("loss_smooth", P), ("loss_l1", P), ("grad_accumulate", c_int)]
+
+
 _SIGS = {
+    "tde_loss_depth_pyramid": (c_int, [P, P]),
     "tde_warp_loss": (c_int, [P, P]),
     "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),
     "tde_pose_prep": (c_int, [c_int, P, P, P, P, P, P, P]),
@@ -52,6 +69,8 @@ _SIGS = {
     "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_deconv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
+    "tde_conv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
+    "tde_deconv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
     "tde_conv2d_bwd_data": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_conv2d_bwd_filter": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_deconv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),

@@ -19,6 +19,7 @@
 // Split-K partials go to a caller workspace and are reduced by a second kernel (deterministic; no
 // float atomics).
 #include "tde_common.h"
+#include "bn_internal.h"
 
 #include <cstdlib>
 
@@ -54,6 +55,8 @@ struct ConvArgs {
   float* ws; int splits; int accumulate;
   int kt_per;  // k-tiles per split
   FDiv fC, fK, fKW, fOW, fOHW;
+  double* bnp;  // BN statistics partials [row tile][2][Nn] from the epilogue (FWD/DGRAD, splits == 1)
+  int bn_gx;    // row tiles per DGRAD class (grid x)
 };
 
 // Per-class geometry of the DGRAD sub-pixel decomposition.
@@ -419,6 +422,46 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
     }
   }
 
+  // ---- batch-norm statistics of the output tile (slim.batch_norm after this conv, bn.hip): per-channel
+  // sum and sum of squares over the tile's rows (rows past M hold exact zeros: their operand rows loaded
+  // as zero), lanes -> waves in a fixed order, one fp64 partial per row tile.  Workgroup-local: the
+  // cross-tile reduction is the next kernel's (a launch costs what an in-kernel hand-off costs).
+  if constexpr (MODE != MODE_WGRAD) {
+    if (p.bnp != nullptr) {
+      float cs[TN], cq[TN];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        cs[b] = 0.f; cq[b] = 0.f;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { const float v = acc[a][b][r]; cs[b] += v; cq[b] += v * v; }
+        cs[b] += __shfl_xor(cs[b], 16, 64); cq[b] += __shfl_xor(cq[b], 16, 64);
+        cs[b] += __shfl_xor(cs[b], 32, 64); cq[b] += __shfl_xor(cq[b], 32, 64);
+      }
+      float* red = reinterpret_cast<float*>(smem);   // [2][WM][BN]; the main loop ended with a barrier
+      if (lane < 16) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          red[wm * BN + wcol0 + b * 16 + lane] = cs[b];
+          red[(WM + wm) * BN + wcol0 + b * 16 + lane] = cq[b];
+        }
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < Nn) {
+        // dense row-tile index (class-major for DGRAD: classes own disjoint pixel sets)
+        int j = bx;
+        if constexpr (MODE == MODE_DGRAD)
+          for (int c = 0; c < (int)(bz % (p.S * p.S)); ++c) j += (dg_class(p, c).M + BM - 1) / BM;
+        double sv = 0.0, sq = 0.0;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) { sv += red[w * BN + tid]; sq += red[(WM + w) * BN + tid]; }
+        p.bnp[(size_t)j * 2 * Nn + n0 + tid] = sv;
+        p.bnp[(size_t)j * 2 * Nn + Nn + n0 + tid] = sq;
+      }
+    }
+  }
+
   // ---- epilogue (16x16 C/D map is dtype-independent on gfx950).  Row addresses first; when
   // accumulating into the destination, ALL old values are loaded before any store (a store may alias a
   // later load, so an interleaved read-modify-write would serialise one memory latency per element).
@@ -476,24 +519,42 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
       }
 }
 
-// Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col]
+// Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col].  A block is ZL z-lanes x (256/ZL)
+// output quads: lane l sums splits l, l+ZL, ... with 4 loads in flight, then the ZL lanes of a quad are
+// combined through LDS in lane order (fixed order: deterministic).  ZL > 1 only when the output is too
+// small to fill the chip otherwise (few outputs, hundreds of splits: the WGRAD of 192x256 layers).
 template <int MODE>
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols) {
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols, int zl) {
+  __shared__ f4 tmp[256];
   const long total4 = (long)rows * (cols / 4);
   const long stride = (long)rows * cols;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
-    const int row = (int)(i / (cols / 4));
-    const int col = 4 * (int)(i - (long)row * (cols / 4));
-    // 4 independent partial sums (fixed order -> deterministic) keep 4 slab loads in flight
-    const float* src = p.ws + (long)row * cols + col;
-    f4 s4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    int z = 0;
-    for (; z + 3 < p.splits; z += 4) {
+  const int zlane = threadIdx.x % zl, ql = threadIdx.x / zl, qpb = 256 / zl;
+  for (long i0 = (long)blockIdx.x * qpb; i0 < total4; i0 += (long)gridDim.x * qpb) {
+    const long i = i0 + ql;
+    f4 s = {0.f, 0.f, 0.f, 0.f};
+    int row = 0, col = 0;
+    if (i < total4) {
+      row = (int)(i / (cols / 4));
+      col = 4 * (int)(i - (long)row * (cols / 4));
+      const float* src = p.ws + (long)row * cols + col;
+      f4 s4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      int z = zlane;
+      for (; z + 3 * zl < p.splits; z += 4 * zl) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s4[u] += ld4(src + (z + u) * stride);
+        for (int u = 0; u < 4; ++u) s4[u] += ld4(src + (z + u * zl) * stride);
+      }
+      for (int u = 0; z < p.splits; z += zl, ++u) s4[u] += ld4(src + z * stride);
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
-    for (int u = 0; z < p.splits; ++z, ++u) s4[u] += ld4(src + z * stride);
-    f4 s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    if (zl > 1) {
+      tmp[threadIdx.x] = s;
+      __syncthreads();
+      if (zlane == 0) {
+        for (int k = 1; k < zl; ++k) s += tmp[threadIdx.x + k];
+      }
+      __syncthreads();
+    }
+    if (zlane != 0 || i >= total4) continue;
     float* dst;
     if constexpr (MODE == MODE_FWD) {
       dst = p.y + (long)row * p.ycs + p.yco + col;
@@ -509,11 +570,59 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
   }
 }
 
+// Split-K reduction for a conv followed by batch norm: z = sum_z ws[z] (same fixed order as
+// splitk_reduce_kernel) written densely, plus per-row-chunk fp64 statistics partials [chunk][2][cols].
+// Grid (row chunk, 64-channel group): a thread owns one channel quad of a row lane.
+__global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, int splits, int rows, int cols,
+                                                               float* z, int rows_per_chunk, double* part) {
+  __shared__ double sh[2][256 * 4];
+  const int q0 = blockIdx.y * 16;
+  const int nq = min(16, cols / 4 - q0);
+  const int ty_n = 256 / nq;
+  const int tx = threadIdx.x % nq, ty = threadIdx.x / nq;
+  const int c = 4 * (q0 + tx);
+  const long stride = (long)rows * cols;
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  const int r0 = blockIdx.x * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
+  if (ty < ty_n) {
+    float f0[4] = {0, 0, 0, 0}, f1[4] = {0, 0, 0, 0};
+    for (int r = r0 + ty; r < r1; r += ty_n) {
+      const float* src = ws + (long)r * cols + c;
+      f4 a[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      int zi = 0;
+      for (; zi + 3 < splits; zi += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] += ld4(src + (zi + u) * stride);
+      }
+      for (int u = 0; zi < splits; ++zi, ++u) a[u] += ld4(src + zi * stride);
+      const f4 v = (a[0] + a[1]) + (a[2] + a[3]);
+      *reinterpret_cast<f4*>(z + (long)r * cols + c) = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f0[j] += v[j]; f1[j] += v[j] * v[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { s0[j] = f0[j]; s1[j] = f1[j]; }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { sh[0][threadIdx.x * 4 + j] = s0[j]; sh[1][threadIdx.x * 4 + j] = s1[j]; }
+  __syncthreads();
+  if (ty == 0) {
+    for (int t = 1; t < ty_n; ++t) {
+      const int o = (t * nq + tx) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s0[j] += sh[0][o + j]; s1[j] += sh[1][o + j]; }
+    }
+    double* o = part + (long)blockIdx.x * 2 * cols;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[c + j] = s0[j]; o[cols + c + j] = s1[j]; }
+  }
+}
+
 // ------------------------------------------------------------------ host dispatch
 struct Plan {
   int bm, bn, splits, kt_per, gx, gy, gz;
   int rows, cols;  // reduce extent
-  size_t ws_bytes;
+  size_t slab_bytes, ws_bytes;
 };
 
 static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, long& Kd, int& ncls) {
@@ -589,8 +698,51 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
   if (mode == MODE_FWD) { pl.rows = (int)M; pl.cols = (int)Nn; }
   else if (mode == MODE_DGRAD) { pl.rows = d.N * d.H * d.W; pl.cols = d.C; }
   else { pl.rows = (int)M; pl.cols = (int)Nn; }
-  pl.ws_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.rows * pl.cols * sizeof(float) : 0;
+  pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.rows * pl.cols * sizeof(float) : 0;
+  pl.ws_bytes = TDE_WS_HDR + pl.slab_bytes;
   return pl;
+}
+
+// Fused conv + BN + ReLU (tde_conv2d_fwd_bn / tde_deconv2d_fwd_bn, workspace op 3).  Where the BN
+// statistics come from:
+//   BN_SMALL : <= 2048 output rows -- [split-K reduce], then one BN kernel (bn.hip) does it all;
+//   BN_EPI   : no split -- the conv epilogue writes one fp64 partial per row tile;
+//   BN_REDUCE: split-K -- the reduce kernel writes z and one partial per row chunk;
+// then bn.hip finalizes and applies (two launches).
+enum { BN_SMALL = 0, BN_EPI = 1, BN_REDUCE = 2 };
+struct BnPlan {
+  int path, nparts;
+  BnChunks ch;
+  size_t part_bytes;
+};
+
+static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl) {
+  BnPlan b{};
+  if (pl.rows <= BN_SMALL_M) {
+    b.path = BN_SMALL;
+  } else if (pl.splits == 1) {
+    b.path = BN_EPI;
+    if (mode == MODE_DGRAD)
+      for (int c = 0; c < d.stride * d.stride; ++c) {
+        const int py = c / d.stride, px = c - py * d.stride;
+        const long mc = (long)d.N * ((d.H - py + d.stride - 1) / d.stride) * ((d.W - px + d.stride - 1) / d.stride);
+        b.nparts += tde_cdiv(mc, pl.bm);
+      }
+    else
+      b.nparts = pl.gx;
+  } else {
+    b.path = BN_REDUCE;
+    b.ch = bn_chunk_plan(pl.rows, pl.cols, pl.splits);
+    b.nparts = b.ch.chunks;
+  }
+  b.part_bytes = (size_t)b.nparts * 2 * pl.cols * sizeof(double);
+  return b;
+}
+
+static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
+  const Plan pl = make_plan(d, mode);
+  if (!bn) return pl.ws_bytes;
+  return pl.ws_bytes + bn_plan(d, mode, pl).part_bytes;
 }
 
 template <int MODE, int BM, int BN>
@@ -646,22 +798,52 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
 }
 
 template <int MODE>
-static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
+               size_t ws_bytes, void* stream) {
   const Plan pl = make_plan(*d, MODE);
-  if (pl.ws_bytes > ws_bytes || (pl.ws_bytes && !tde_aligned16(ws))) return TDE_ERR_WORKSPACE;
-  a.ws = static_cast<float*>(ws);
+  BnPlan bp{};
+  if (bn) bp = bn_plan(*d, MODE, pl);
+  if (pl.ws_bytes + bp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  char* body = tde_ws_body(ws);
+  double* part = reinterpret_cast<double*>(body + pl.slab_bytes);
+  a.ws = reinterpret_cast<float*>(body);
   a.splits = pl.splits;
   a.kt_per = pl.kt_per;
   a.accumulate = accumulate;
+  a.bnp = (bn && bp.path == BN_EPI) ? part : nullptr;
+  a.bn_gx = pl.gx;
   hipStream_t st = static_cast<hipStream_t>(stream);
   launch_mode<MODE>(pl, a, st);
-  if (pl.splits > 1) {
+  float* z = MODE == MODE_FWD ? a.y : (MODE == MODE_DGRAD ? a.dx : a.dw);
+  if (pl.splits > 1 && !(bn && bp.path == BN_REDUCE)) {
     const long n4 = (long)pl.rows * (pl.cols / 4);
-    int blocks = (int)((n4 + 255) / 256);
+    // z-lanes per output quad: fill >= ~256 blocks, keep >= 4 splits per lane
+    int zl = 1;
+    while (zl < 64 && (n4 * zl * 2 + 255) / 256 <= 256 && pl.splits / (zl * 2) >= 4) zl *= 2;
+    long blocks = (n4 * zl + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3(blocks), dim3(256), 0, st, a, pl.rows, pl.cols);
+    hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3((int)blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
+  }
+  if (bn) {
+    // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
+    const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu};
+    if (bp.path == BN_SMALL) {
+      bn_fwd_small_launch(pl.rows, pl.cols, z, o, st);
+    } else {
+      if (bp.path == BN_REDUCE)
+        hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws,
+                           pl.splits, pl.rows, pl.cols, z, bp.ch.rows_per_chunk, part);
+      bn_fwd_from_partials_launch(pl.rows, pl.cols, z, bp.nparts, part, o, st);
+    }
   }
   return tde_launch_status();
+}
+
+static bool bn_ok(const tde_bn_train_t* bn, int C) {
+  return bn && bn->beta && bn->save_mean && bn->save_invstd && bn->y && C <= 1024 &&
+         ((bn->moving_mean == nullptr) == (bn->moving_var == nullptr)) && bn->y_cstride % 4 == 0 &&
+         bn->y_coff % 4 == 0 && bn->y_coff + C <= bn->y_cstride && tde_aligned16(bn->y) && tde_aligned16(bn->beta);
 }
 
 }  // namespace
@@ -677,14 +859,15 @@ int tde_set_conv_math(int mode) {
 int tde_get_conv_math(void) { return g_conv_math; }
 
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op) {
-  if (!desc_ok(d) || op < 0 || op > 2) return 0;
-  return make_plan(*d, op == 0 ? MODE_FWD : (op == 1 ? MODE_DGRAD : MODE_WGRAD)).ws_bytes;
+  // op 3 = forward + batch norm + ReLU (tde_conv2d_fwd_bn)
+  if (!desc_ok(d) || op < 0 || op > 3) return 0;
+  return plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_FWD : (op == 1 ? MODE_DGRAD : MODE_WGRAD), op == 3);
 }
 
 size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op) {
-  // deconv fwd = DGRAD, bwd_data = FWD, bwd_filter = WGRAD of the virtual conv
-  if (!desc_ok(d) || op < 0 || op > 2) return 0;
-  return make_plan(*d, op == 0 ? MODE_DGRAD : (op == 1 ? MODE_FWD : MODE_WGRAD)).ws_bytes;
+  // deconv fwd = DGRAD, bwd_data = FWD, bwd_filter = WGRAD of the virtual conv; op 3 = fwd + BN + ReLU
+  if (!desc_ok(d) || op < 0 || op > 3) return 0;
+  return plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_DGRAD : (op == 1 ? MODE_FWD : MODE_WGRAD), op == 3);
 }
 
 int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y, int accumulate,
@@ -692,7 +875,16 @@ int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, flo
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y;
-  return run<MODE_FWD>(d, a, accumulate, ws, ws_bytes, stream);
+  return run<MODE_FWD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
+}
+
+int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z, const tde_bn_train_t* bn,
+                      void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(z) && bn_ok(bn, d->K));
+  TDE_CHECK_ARG(d->y_cstride == d->K && d->y_coff == 0);   // z is the dense pre-BN output
+  ConvArgs a = make_args(*d);
+  a.x = x; a.w = w; a.y = z;
+  return run<MODE_FWD>(d, a, 0, bn, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
@@ -700,7 +892,7 @@ int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* 
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx));
   ConvArgs a = make_args(*d);
   a.dy = dy; a.w = w; a.dx = dx;
-  return run<MODE_DGRAD>(d, a, accumulate, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
@@ -708,12 +900,21 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(dw));
   ConvArgs a = make_args(*d);
   a.x = x; a.dy = dy; a.dw = dw;
-  return run<MODE_WGRAD>(d, a, accumulate, ws, ws_bytes, stream);
+  return run<MODE_WGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream) {
   return tde_conv2d_bwd_data(d, x_small, w, y_big, accumulate, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
+                        const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(z_big) && bn_ok(bn, d->C));
+  TDE_CHECK_ARG(d->x_cstride == d->C && d->x_coff == 0);   // z is the dense pre-BN output
+  ConvArgs a = make_args(*d);
+  a.dy = x_small; a.w = w; a.dx = z_big;
+  return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,

@@ -326,7 +326,7 @@ size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
   const WgPlan w = wg_plan(d);
   const size_t part = (size_t)w.chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
-  return dz_bytes(d) + part;
+  return TDE_WS_HDR + dz_bytes(d) + part;
 }
 
 int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, float* y,
@@ -351,7 +351,8 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   TDE_CHECK_ARG(head_desc_ok(d) && d->stride == 1 && x && w && y && dy && tde_aligned16(x));
   TDE_CHECK_ARG(d->x_cstride % 4 == 0 && d->x_coff % 4 == 0);
   TDE_CHECK_ARG(d->K == 1 || d->K == 2 || d->K == 6);
-  if (ws_bytes < tde_head_workspace_size(d) || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  if (ws_bytes < tde_head_workspace_size(d) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  ws = tde_ws_body(ws);
   HeadArgs a = make_head_args(d);
   a.x = x; a.w = w; a.yin = y; a.dy = dy; a.dx = dx; a.acc_dx = accumulate_dx;
   a.act = act; a.scale = scale; a.offset = offset;

@@ -93,6 +93,85 @@ int ew_grid(long n) {
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
 }
 
+// ------------------------------------------------------------------ fused multi-scale depth loss head
+// One launch for every scale of train_depth_only.py:160-187 (and the per-scale smooth / depth-L1 terms
+// of the other trainers): for scale s, compute_smooth_loss of pred_s (or 1/pred_s) and
+// mean|nf(resize_area(label, s) - pred_s)|, values into two fp64 accumulators, gradients written (or
+// added) into grad_s.  The area-downsampled label (train_depth_only.py:170) is formed on the fly from
+// the full-resolution label (integer factor 2^s, same summation order as tde_resize_area_fwd).
+struct PyrArgs {
+  tde_depth_loss_t a;
+  long start[TDE_MAX_SCALES + 1];   // first flat pixel index of each scale
+};
+
+__global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
+  __shared__ double sh[4];
+  const tde_depth_loss_t& a = P.a;
+  double ls = 0.0, ll = 0.0;
+  const long total = P.start[a.nscales];
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    int s = 0;
+    while (idx >= P.start[s + 1]) ++s;
+    const long loc = idx - P.start[s];
+    const int H = a.H >> s, W = a.W >> s;
+    const int j = (int)(loc % W);
+    const long t = loc / W;
+    const int i = (int)(t % H), n = (int)(t / H);
+    const Map f{a.pred[s], H, W, a.pred_cs[s], a.pred_co[s], a.recip};
+    float gf = 0.f;
+    if (a.smooth_w[s] != 0.f && H >= 3 && W >= 3) {
+      const double n1 = (double)a.N * H * (W - 2), n23 = (double)a.N * (H - 1) * (W - 1), n4 = (double)a.N * (H - 2) * W;
+      const float w1 = (float)(a.smooth_w[s] / n1), w23 = (float)(a.smooth_w[s] / n23), w4 = (float)(a.smooth_w[s] / n4);
+      float lv = 0.f;
+      if (j < W - 2) lv += fabsf(t_dx2(f, n, i, j)) * w1;
+      if (i < H - 1 && j < W - 1) lv += (fabsf(t_dxdy(f, n, i, j)) + fabsf(t_dydx(f, n, i, j))) * w23;
+      if (i < H - 2) lv += fabsf(t_dy2(f, n, i, j)) * w4;
+      ls += lv;
+      if (j < W - 2) gf += tde_sign(t_dx2(f, n, i, j)) * w1;
+      if (j >= 1 && j - 1 < W - 2) gf -= 2.f * tde_sign(t_dx2(f, n, i, j - 1)) * w1;
+      if (j >= 2) gf += tde_sign(t_dx2(f, n, i, j - 2)) * w1;
+      if (i < H - 2) gf += tde_sign(t_dy2(f, n, i, j)) * w4;
+      if (i >= 1 && i - 1 < H - 2) gf -= 2.f * tde_sign(t_dy2(f, n, i - 1, j)) * w4;
+      if (i >= 2) gf += tde_sign(t_dy2(f, n, i - 2, j)) * w4;
+      if (i < H - 1 && j < W - 1) gf += (tde_sign(t_dxdy(f, n, i, j)) + tde_sign(t_dydx(f, n, i, j))) * w23;
+      if (i < H - 1 && j >= 1) gf -= (tde_sign(t_dxdy(f, n, i, j - 1)) + tde_sign(t_dydx(f, n, i, j - 1))) * w23;
+      if (i >= 1 && j < W - 1) gf -= (tde_sign(t_dxdy(f, n, i - 1, j)) + tde_sign(t_dydx(f, n, i - 1, j))) * w23;
+      if (i >= 1 && j >= 1) gf += (tde_sign(t_dxdy(f, n, i - 1, j - 1)) + tde_sign(t_dydx(f, n, i - 1, j - 1))) * w23;
+      if (a.recip) {
+        const float p = a.pred[s][((long)(n * H + i) * W + j) * a.pred_cs[s] + a.pred_co[s]];
+        gf *= -1.f / (p * p);
+      }
+    }
+    const float pv = a.pred[s][((long)(n * H + i) * W + j) * a.pred_cs[s] + a.pred_co[s]];
+    if (a.l1_w[s] != 0.f) {
+      const int fct = 1 << s;
+      float lab;
+      if (s == 0) {
+        lab = a.label[((long)n * a.H + i) * a.W + j];
+      } else {
+        float sum = 0.f;
+        for (int u = 0; u < fct; ++u)
+          for (int v = 0; v < fct; ++v) sum += a.label[((long)n * a.H + i * fct + u) * a.W + j * fct + v];
+        lab = sum * (1.f / (float)(fct * fct));
+      }
+      float d = lab - pv;
+      if (a.nonfinite && !isfinite(d)) d = 0.f;   // replace_nonfinite: value and gradient masked
+      const double tot = (double)a.N * H * W;
+      ll += fabsf(d) * ((double)a.l1_w[s] / tot);
+      gf += -tde_sign(d) * (float)(a.l1_w[s] / tot);
+    }
+    float* gp = a.grad[s] + ((long)(n * H + i) * W + j) * a.g_cs[s] + a.g_co[s];
+    *gp = a.grad_accumulate ? *gp + gf : gf;
+  }
+  const double bs = tde_block_sum_d(ls, sh);
+  __syncthreads();
+  const double bl = tde_block_sum_d(ll, sh);
+  if (threadIdx.x == 0) {
+    if (a.loss_smooth) atomicAdd(a.loss_smooth, bs);
+    if (a.loss_l1) atomicAdd(a.loss_l1, bl);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -112,6 +191,21 @@ int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, c
   const long total = (long)N * H * W;
   hipLaunchKernelGGL(l1_kernel, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, pred,
                      cstride, coff, label, nonfinite, weight, loss, grad, g_cstride, g_coff);
+  return tde_launch_status();
+}
+
+int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
+  TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
+  PyrArgs P;
+  P.a = *a;
+  P.start[0] = 0;
+  for (int s = 0; s < a->nscales; ++s) {
+    TDE_CHECK_ARG(a->pred[s] && a->grad[s] && (a->H >> s) > 0 && (a->W >> s) > 0);
+    TDE_CHECK_ARG(a->l1_w[s] == 0.f || (a->label && a->H % (1 << s) == 0 && a->W % (1 << s) == 0));
+    P.start[s + 1] = P.start[s] + (long)a->N * (a->H >> s) * (a->W >> s);
+  }
+  hipLaunchKernelGGL(depth_pyramid_kernel, dim3(ew_grid(P.start[a->nscales])), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), P);
   return tde_launch_status();
 }
 

@@ -21,6 +21,17 @@ static inline bool tde_aligned16(const void* p) { return (reinterpret_cast<uintp
 
 static inline int tde_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Every workspace starts with TDE_WS_HEADER_BYTES of uint32 arrival counters (include/tde.h): the
+// deterministic "last block reduces" steps of the conv and BN kernels count tile arrivals there and
+// reset their counter to zero before exiting, so a workspace zeroed once stays valid for every call.
+constexpr size_t TDE_WS_HDR = TDE_WS_HEADER_BYTES;
+constexpr int TDE_CNT_SPLIT = 0;        // [0, 8192): split-K tiles of one conv launch
+constexpr int TDE_CNT_SPLIT_MAX = 8192;
+constexpr int TDE_CNT_BN = 8192;        // [8192, 16384): BN statistics groups and column tiles
+constexpr int TDE_CNT_BN_MAX = 8192;
+static inline unsigned* tde_ws_counters(void* ws) { return static_cast<unsigned*>(ws); }
+static inline char* tde_ws_body(void* ws) { return static_cast<char*>(ws) + TDE_WS_HDR; }
+
 __device__ __forceinline__ float tde_sign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
 // Block-wide sum of a double (blockDim.x == 256), result valid in thread 0.

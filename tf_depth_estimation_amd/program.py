@@ -202,8 +202,9 @@ class Workspace:
 
     def get(self, ws_bytes, device):
         if self.ws is None or self.ws.numel() * 4 < ws_bytes:
-            self.ws = torch.empty(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
-            self.ws_side = torch.empty(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
+            # zeroed once: the leading TDE_WS_HEADER_BYTES are tile counters every call leaves at zero
+            self.ws = torch.zeros(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
+            self.ws_side = torch.zeros(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
         return self.ws, self.ws_side
 
     def dz_for(self, i, numel, device):
@@ -275,7 +276,7 @@ class NetProgram:
                 if isinstance(op, ConvBN):
                     d = op.desc(N)
                     q = lib.tde_deconv2d_workspace_size if op.deconv else lib.tde_conv2d_workspace_size
-                    for o in range(3):
+                    for o in range(4):
                         ws = max(ws, q(ctypes_ref(d), o))
                     M = N * op.dst.H * op.dst.W
                     ws = max(ws, lib.tde_bn_workspace_size(M, op.K))
@@ -318,23 +319,33 @@ class NetProgram:
                 z = run.z[i] if op.bn else None
                 if not op.bn:
                     raise NotImplementedError("BN-free conv/deconv layers")
-                with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
-                    if op.deconv:
-                        _lib.check(lib.tde_deconv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws),
-                                                        wsb, st), op.layer)
-                    else:
-                        _lib.check(lib.tde_conv2d_fwd(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws),
-                                                      wsb, st), op.layer)
                 M = N * op.dst.H * op.dst.W
                 beta = self.P(f"{op.layer}/BatchNorm/beta")
                 sm = run.stats[i]
                 mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
-                with self._span("bn_fwd"):
-                    if is_training:
+                if is_training and self.timer is None:
+                    # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
+                    # consumes the conv's split-K partials directly
+                    bn = _lib.BnTrain(ptr(beta), 1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
+                                      ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1)
+                    fn = lib.tde_deconv2d_fwd_bn if op.deconv else lib.tde_conv2d_fwd_bn
+                    _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb, st),
+                               op.layer)
+                elif is_training:
+                    # instrumented step (bench.py roofline): the same layer as separate conv and BN calls, so
+                    # the conv kernel's time is measured on its own
+                    fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
+                    with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
+                        _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
+                    with self._span("bn_fwd"):
                         _lib.check(lib.tde_bn_fwd_train(M, op.K, ptr(z), ptr(beta), 1e-3, op.decay, int(self.bessel),
                                                         ptr(mm), ptr(mv), ptr(sm[0]), ptr(sm[1]), run.vptr(op.dst),
                                                         op.dst.buf.cs, op.dst.coff, 1, ptr(ws), wsb, st), op.layer)
-                    else:
+                else:
+                    fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
+                    with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
+                        _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
+                    with self._span("bn_fwd"):
                         _lib.check(lib.tde_bn_fwd_infer(M, op.K, ptr(z), ptr(beta), 1e-3, ptr(mm), ptr(mv),
                                                         run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st), op.layer)
             elif isinstance(op, Head):

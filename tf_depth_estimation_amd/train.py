@@ -188,11 +188,24 @@ class DepthOnlyTrainer(Trainer):
         dev = "cuda"
         self.images = torch.zeros(batch, H, W, 3, device=dev, dtype=torch.float32)
         self.label = torch.ones(batch, H, W, 1, device=dev, dtype=torch.float32)
-        self.label_pyr = [self.label] + [torch.empty(batch, H >> s, W >> s, 1, device=dev, dtype=torch.float32) for s in (1, 2, 3)]
         outs = self.prog.spec.outputs
         self.d_out = [torch.empty(batch, v.H, v.W, v.C, device=dev, dtype=torch.float32) for v in outs]
         self.loss = torch.zeros(1, dtype=torch.float64, device=dev)
         self.parts = torch.zeros(2, dtype=torch.float64, device=dev)   # [depth, smooth]
+        a = _lib.DepthLoss()
+        a.N, a.H, a.W, a.nscales = batch, H, W, 4
+        for s, v in enumerate(outs):
+            a.pred[s] = self.run.vptr(v).value + 4 * v.coff   # 1-channel view of the net output
+            a.pred_cs[s], a.pred_co[s] = v.buf.cs, 0
+            a.grad[s] = self.d_out[s].data_ptr()
+            a.g_cs[s], a.g_co[s] = 1, 0
+            a.smooth_w[s] = self.w["smooth"] / 2 ** s        # train_depth_only.py:167-168
+            a.l1_w[s] = self.w["depth"] / 2 ** s             # :183-184
+        a.recip, a.nonfinite, a.grad_accumulate = 0, 0, 0
+        a.label = self.label.data_ptr()
+        a.loss_smooth = self.parts.data_ptr() + 8
+        a.loss_l1 = self.parts.data_ptr()
+        self.loss_args = a
 
     def set_batch(self, images, label):
         self.images.copy_(images)
@@ -204,22 +217,10 @@ class DepthOnlyTrainer(Trainer):
     def phase_compute(self):
         lib, st = _lib.load(), _lib.stream_ptr()
         _lib.check(lib.tde_zero_bytes(16, ptr(self.parts), st), "zero loss")
-        for g in self.d_out:
-            _lib.check(lib.tde_zero_bytes(g.numel() * 4, ptr(g), st), "zero dout")
         outs = self.prog.forward(self.run, self.images, True)
-        N, H, W = self.N, self.H, self.W
-        for s in (1, 2, 3):
-            _lib.check(lib.tde_resize_area_fwd(N, H, W, 1, ptr(self.label), H >> s, W >> s, ptr(self.label_pyr[s]),
-                                               st), "label pyramid")
-        p_depth = ctypes_double_ptr(self.parts, 0)
-        p_smooth = ctypes_double_ptr(self.parts, 1)
-        for s in range(4):
-            pred, g = outs[s], self.d_out[s]
-            h, w = pred.shape[1], pred.shape[2]
-            _lib.check(lib.tde_loss_smooth2(N, h, w, ptr(pred), 1, 0, 0, self.w["smooth"] / 2 ** s, p_smooth, ptr(g),
-                                            1, 0, st), "smooth")
-            _lib.check(lib.tde_loss_l1(N, h, w, ptr(pred), 1, 0, ptr(self.label_pyr[s]), 0, self.w["depth"] / 2 ** s,
-                                       p_depth, ptr(g), 1, 0, st), "depth l1")
+        # the whole loss head (4 scales x (smooth + L1 to the area-downsampled label)) in one launch that
+        # WRITES the output gradients (no zeroed gradient buffers)
+        _lib.check(lib.tde_loss_depth_pyramid(ctypes_ref(self.loss_args), st), "depth loss head")
         # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
         self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
 
@@ -228,6 +229,11 @@ class DepthOnlyTrainer(Trainer):
 
     def outputs(self):
         return [self.run.view_tensor(v) for v in self.prog.spec.outputs]
+
+
+def ctypes_ref(x):
+    import ctypes
+    return ctypes.byref(x)
 
 
 def ctypes_double_ptr(t, idx):
