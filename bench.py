@@ -228,7 +228,7 @@ def main():
     for p in progs:
         p.timer = None
     fam = timer.totals()
-    conv = [fam[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad") if k in fam]
+    conv = [fam[k] for k in ("conv_fwd", "conv_bwd", "conv_dgrad", "conv_wgrad") if k in fam]
     conv_ms = sum(c[0] for c in conv)
     conv_flops = sum(c[1] for c in conv)
     conv_launches = sum(c[2] for c in conv)

@@ -19,10 +19,7 @@
  *     the host and is safe to capture in a hipGraph.  Re-entrant across streams.
  *   - Return value: TDE_OK (0) or a negative tde_status.
  *   - `ws` / `ws_bytes`: caller-provided device workspace; size it with the *_workspace_size query.
- *     Its first TDE_WS_HEADER_BYTES hold tile-arrival counters (the split-K and batch-norm
- *     reductions finish inside the producing kernel: the last block of a tile to arrive reduces, in
- *     a fixed order, so results stay deterministic).  Zero a workspace ONCE after allocating it
- *     (tde_zero_bytes); every call leaves the counters zero again.  One workspace per stream.
+ *     One workspace per stream (calls on one stream reuse it in order).
  */
 #ifndef TDE_H_
 #define TDE_H_
@@ -35,7 +32,6 @@ extern "C" {
 #endif
 
 #define TDE_ABI_VERSION 2
-#define TDE_WS_HEADER_BYTES 65536
 
 typedef enum {
   TDE_OK = 0,
@@ -98,6 +94,15 @@ typedef struct {
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z,
                       const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream);
 
+/* Both backward GEMMs of one conv layer (TF's Conv2DBackpropInput + Conv2DBackpropFilter of one
+ * slim.conv2d): dx (+)= dL/dx and dw (+)= dL/dw from dy, horizontally fused into one launch (the two are
+ * independent; at the deep levels neither fills the chip alone), then the split-K reductions.
+ * Workspace: tde_conv2d_bwd_workspace_size(d). */
+size_t tde_conv2d_bwd_workspace_size(const tde_conv_desc_t* d);
+int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, const float* w, float* dx,
+                   int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes,
+                   void* stream);
+
 /* slim.conv2d_transpose (stride 2, SAME), nets_optflow_depth.py:103,109,114,119,126,133,140.
  * `d` is the virtual forward conv (see above); x = deconv input, y = deconv output.
  *   fwd       : y_big  = Conv2DBackpropInput(x_small)     (weights [KH][KW][Cout][Cin])
@@ -106,6 +111,12 @@ int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, 
 size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op);
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* deconv backward: dx_small (+)= Conv2D(dy_big), dw (+)= Conv2DBackpropFilter(dy_big, x_small), one
+ * fused launch (see tde_conv2d_bwd).  Workspace: tde_deconv2d_bwd_workspace_size(d). */
+size_t tde_deconv2d_bwd_workspace_size(const tde_conv_desc_t* d);
+int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, const float* w,
+                     float* dx_small, int accumulate_dx, float* dw, int accumulate_dw, void* ws,
+                     size_t ws_bytes, void* stream);
 /* deconv forward + BN + ReLU: z_big dense [N*H*W][C] (x_cstride == C, x_coff == 0); workspace op 3. */
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
                         const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream);

@@ -9,5 +9,5 @@ for spec in "$@"; do
   env $vars timeout -k 10 200 python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline ${AB_BENCH_ARGS:-} \
     > "gpurun_out/abe_$name.json" 2> "gpurun_out/abe_$name.err"
   rc=$?; [ $rc -ne 0 ] && { echo "$name rc=$rc"; tail -3 "gpurun_out/abe_$name.err"; exit $rc; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernel_breakdown_ms']; print(sys.argv[2], d['ms_per_step'], 'ms/step conv', d['roofline']['conv_ms_per_step'], 'fwd', k.get('conv_fwd'), 'dgrad', k.get('conv_dgrad'), 'wgrad', k.get('conv_wgrad'))" "gpurun_out/abe_$name.json" "$name"
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); k=d['kernel_breakdown_ms']; print(sys.argv[2], d['ms_per_step'], 'ms/step conv', d['roofline']['conv_ms_per_step'], 'fwd', k.get('conv_fwd'), 'bwd', k.get('conv_bwd'), 'wgrad', k.get('conv_wgrad'))" "gpurun_out/abe_$name.json" "$name"
 done

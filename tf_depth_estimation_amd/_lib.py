@@ -71,6 +71,10 @@ _SIGS = {
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_conv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
     "tde_deconv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
+    "tde_conv2d_bwd_workspace_size": (c_size_t, [P]),
+    "tde_deconv2d_bwd_workspace_size": (c_size_t, [P]),
+    "tde_conv2d_bwd": (c_int, [P, P, P, P, P, c_int, P, c_int, P, c_size_t, P]),
+    "tde_deconv2d_bwd": (c_int, [P, P, P, P, P, c_int, P, c_int, P, c_size_t, P]),
     "tde_conv2d_bwd_data": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_conv2d_bwd_filter": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_deconv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),

@@ -395,7 +395,7 @@ extern "C" {
 
 size_t tde_bn_workspace_size(int M, int C) {
   if (M <= 0 || C <= 0 || C % 4) return 0;
-  return TDE_WS_HDR + (size_t)bn_chunk_plan(M, C, 1).chunks * 2 * C * sizeof(double) + 2 * (size_t)C * sizeof(float) +
+  return (size_t)bn_chunk_plan(M, C, 1).chunks * 2 * C * sizeof(double) + 2 * (size_t)C * sizeof(float) +
          64;
 }
 

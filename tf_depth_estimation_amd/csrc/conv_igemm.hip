@@ -83,17 +83,6 @@ __device__ __forceinline__ DgClass dg_class(const ConvArgs& p, int cls) {
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
-// Raw buffer resource over n floats (byte range clamped below 2^31 so OOB is always out of range;
-// 0x00020000 = DATA_FORMAT 32 for gfx9-family raw buffers).
-constexpr int OOB = (int)0x80000000;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, long n) {
-  const long bytes = 4 * n;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0,
-                                           (int)(bytes < 0x7fffffffl ? bytes : 0x7fffffffl), 0x00020000);
-}
-__device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
 
 // ------------------------------------------------------------------ bf16x3 split-precision variant
 // Same three gather modes, but each fp32 operand element x is split at staging time into
@@ -165,8 +154,18 @@ template <int ROWS>
 struct ImgSel<1, ROWS> { using type = Img3<ROWS>; using T = u16; };
 
 // MATH 0: exact fp32 (2 x 4 v_mfma_f32_16x16x4_f32 per 32-deep k-tile); MATH 1: bf16x3.
-template <int MATH, int MODE, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
+template <int MATH, int BM, int BN>
+struct SmemSize {
+  using IA = typename ImgSel<MATH, BM>::type;
+  using IB = typename ImgSel<MATH, BN>::type;
+  using ET = typename ImgSel<MATH, BM>::T;
+  static constexpr int N = 2 * (IA::SIZE + IB::SIZE);
+};
+
+// One output tile (bx, by) of split / class bz.  The kernels below map blocks onto tiles.
+template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
+__device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const int by, const int bz,
+                                          typename ImgSel<MATH, BM>::T* smem) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
   constexpr bool A_T = (MODE == MODE_WGRAD);   // A global vectors along rows -> register transpose
@@ -174,17 +173,11 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
   using IA = typename ImgSel<MATH, BM>::type;
   using IB = typename ImgSel<MATH, BN>::type;
   using ET = typename ImgSel<MATH, BM>::T;
-  __shared__ __attribute__((aligned(16))) ET smem[2 * (IA::SIZE + IB::SIZE)];
   ET* const As0 = smem;
   ET* const Bs0 = smem + 2 * IA::SIZE;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
-
-  // Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
-  // share a pixel slab -- was measured 5-20% SLOWER on config 2's layers: the round-robin order
-  // already lets neighbouring tiles, dispatched together, share the slab through the Infinity Cache.)
-  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
 
   int M, Nn, Kd;
   DgClass g{};
@@ -254,9 +247,11 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
     }
   }
 
-  f4 ra[A_PER][A_V], rb[B_PER][B_V];
+  // register staging sets: set 0, and set 1 for the second tile in flight when PF == 2
+  f4 ra0[A_PER][A_V], rb0[B_PER][B_V];
+  f4 ra1[PF == 2 ? A_PER : 1][A_V], rb1[PF == 2 ? B_PER : 1][B_V];
 
-  auto load_tiles = [&](int kt) {
+  auto load_tiles = [&](int kt, auto& ra, auto& rb) {
     const int kbase = kt * BK3;
     // k decode shared by every A slot (and the DGRAD B slots): s & 7 == tid & 7 for all slots
     const int kq = kbase + 4 * (tid & 7);
@@ -323,7 +318,7 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
     }
   };
 
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, auto& ra, auto& rb) {
     ET* A = As0 + buf * IA::SIZE;
     ET* Bm = Bs0 + buf * IB::SIZE;
 #pragma unroll
@@ -363,62 +358,91 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
   const int r16 = lane & 15, q = lane >> 4;
   const int wrow0 = wm * TM * 16, wcol0 = wn * TN * 16;
 
-  if (kt0 < kt1) {
-    load_tiles(kt0);
-    store_tiles(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = (kt + 1 < kt1);
-      const ET* A = As0 + cur * IA::SIZE;
-      const ET* Bm = Bs0 + cur * IB::SIZE;
-      // fragment reads first, then the next tile's global loads (their address arithmetic overlaps
-      // the LDS latency), then the MFMAs
-      if constexpr (MATH == 1) {
-        bf8 ah[TM], al[TM], bh[TN], bl[TN];
+  // one k-tile from LDS buffer `cur`: fragment reads first, then `issue` (the global loads of a later
+  // tile: their address arithmetic overlaps the LDS latency), then the MFMAs
+  auto compute = [&](int cur, auto&& issue) {
+    const ET* A = As0 + cur * IA::SIZE;
+    const ET* Bm = Bs0 + cur * IB::SIZE;
+    if constexpr (MATH == 1) {
+      bf8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-          ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
-          al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
-        }
+      for (int a = 0; a < TM; ++a) {
+        ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+        al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+        bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
+      }
+      issue();
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-          bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
-          bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
-        if (more) load_tiles(kt + 1);
+    } else {
+      // lane (r16, q) holds k = 16*kc + 4*q + j of MFMA (kc, j): same permutation for A and B
+      f4 fa[2][TM], fb[2][TN];
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+      for (int kc = 0; kc < 2; ++kc) {
 #pragma unroll
-          for (int b = 0; b < TN; ++b) {
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-          }
-      } else {
-        // lane (r16, q) holds k = 16*kc + 4*q + j of MFMA (kc, j): same permutation for A and B
-        f4 fa[2][TM], fb[2][TN];
+        for (int a = 0; a < TM; ++a) fa[kc][a] = IA::frag(A, wrow0 + a * 16 + r16, 16 * kc + 4 * q);
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) {
-#pragma unroll
-          for (int a = 0; a < TM; ++a) fa[kc][a] = IA::frag(A, wrow0 + a * 16 + r16, 16 * kc + 4 * q);
-#pragma unroll
-          for (int b = 0; b < TN; ++b) fb[kc][b] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 * kc + 4 * q);
-        }
-        if (more) load_tiles(kt + 1);
-#pragma unroll
-        for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-              for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kc][a][j], fb[kc][b][j], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TN; ++b) fb[kc][b] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 * kc + 4 * q);
       }
-      if (more) store_tiles(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
+      issue();
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kc][a][j], fb[kc][b][j], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  if (kt0 < kt1) {
+    load_tiles(kt0, ra0, rb0);
+    store_tiles(0, ra0, rb0);
+    __syncthreads();
+    int cur = 0;
+    if constexpr (PF == 1) {
+      // one tile in flight: the load of tile kt+1 overlaps the MFMAs of tile kt
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = (kt + 1 < kt1);
+        compute(cur, [&] { if (more) load_tiles(kt + 1, ra0, rb0); });
+        if (more) store_tiles(cur ^ 1, ra0, rb0);
+        __syncthreads();
+        cur ^= 1;
+      }
+    } else {
+      // two tiles in flight (register sets 0/1 alternate; the loop is unrolled by two so every register
+      // index is static): tile kt is consumed from LDS while kt+1 and kt+2 are loading.  For the small
+      // tiles of the deep, weight-streaming layers one tile's MFMAs are shorter than a memory latency.
+      // Loads and stores are issued unconditionally (past the last tile they re-load tile kt1-1 into
+      // the idle buffer): a conditional issue makes hipcc wait vmcnt(0) at the merge point, which
+      // would drain the second tile in flight.
+      const int klast = kt1 - 1;
+      load_tiles(min(kt0 + 1, klast), ra1, rb1);
+      int kt = kt0;
+      while (true) {
+        compute(cur, [&] { load_tiles(min(kt + 2, klast), ra0, rb0); });
+        store_tiles(cur ^ 1, ra1, rb1);
+        __syncthreads();
+        cur ^= 1;
+        if (++kt >= kt1) break;
+        compute(cur, [&] { load_tiles(min(kt + 2, klast), ra1, rb1); });
+        store_tiles(cur ^ 1, ra0, rb0);
+        __syncthreads();
+        cur ^= 1;
+        if (++kt >= kt1) break;
+      }
     }
   }
 
@@ -517,6 +541,168 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
         const int n = n0 + wcol0 + b * 16 + r16;
         if (rowaddr[a][r] >= 0 && n < Nn) base[rowaddr[a][r] + n] = acc[a][b][r];
       }
+}
+
+// Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
+// share a pixel slab -- was measured 5-20% SLOWER on config 2's layers: the round-robin order
+// already lets neighbouring tiles, dispatched together, share the slab through the Infinity Cache.)
+template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
+__global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
+  __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
+  conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// The two backward GEMMs of one layer in ONE launch (horizontal fusion): blocks [0, nd) compute the
+// data gradient (MODE1: DGRAD of a conv, FWD of a deconv's virtual conv), blocks [nd, nd + nw) the
+// filter gradient (WGRAD).  Both
+// only read dz, so they are independent; at the deep levels neither fills the chip alone.
+template <int MODE1, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT) igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
+                                                        int gxw, int gyw, int nd) {
+  constexpr int MATH = 0;
+  __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
+  int id = blockIdx.x;
+  if (id < nd) {
+    const int bx = id % gxd;
+    id /= gxd;
+    conv_tile<MATH, MODE1, BM, BN, WM, WN, 1>(pd, bx, id % gyd, id / gyd, smem);
+  } else {
+    id -= nd;
+    const int bx = id % gxw;
+    id /= gxw;
+    conv_tile<MATH, MODE_WGRAD, BM, BN, WM, WN, 1>(pw, bx, id % gyw, id / gyw, smem);
+  }
+}
+
+// ------------------------------------------------------------------ skinny-M path (deep levels)
+// At the 3x4 / 2x2 levels (M = N*OH*OW <= 96 output rows) FWD and stride-1 DGRAD are weight streams:
+// the operand W is read exactly once and the activations are a few hundred KB.  A tiled GEMM stages W
+// through LDS one 32-deep k-tile per barrier and cannot keep enough bytes in flight.  Here each wave
+// owns a k-slice of KG x 16 and issues ALL its loads (activations and weights, straight to registers)
+// before the first MFMA; the block's 4 waves are 4 consecutive k-slices of the same 64 output
+// columns, combined through LDS in wave order.  Grid = (64-column tiles, k splits); the per-split
+// partials go to the usual slab and splitk_reduce_kernel (fixed order: deterministic).
+//   MFMA operand mapping (v_mfma_f32_16x16x4_f32, MFMA m of a 16-deep group uses k = k0 + 4q + m):
+//     A  lane (i, q) = X[row 16a + i][k0 + 4q + m]      (one f4 per row fragment and group)
+//     B  FWD  : lane (i, q) f4 = W[k0 + 4q + m][n0 + 4i .. 4i+3]  -> column fragment j = output
+//               columns n0 + 4i + j (weights are [k][n], n contiguous)
+//        DGRAD: lane (i, q) f4 = W[tap][c = n0 + 16f + i][kx .. kx+3] -> column fragment f
+//               (the [k][c] operand is contiguous along k)
+template <int MODE, int TM, int KG>
+__global__ void __launch_bounds__(NT) skinny_kernel(const ConvArgs p) {
+  constexpr int KW = 16 * KG, KB = 4 * KW;   // k per wave, k per block (one split)
+  __shared__ float red[4 * TM * 16 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 64, zsplit = blockIdx.y;
+  int M, Nn, Kd;
+  if constexpr (MODE == MODE_FWD) {
+    M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
+  } else {
+    M = p.N * p.H * p.W; Nn = p.C; Kd = p.KH * p.KW * p.K;
+  }
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, (long)p.N * p.OH * p.OW * p.ycs);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, (long)p.KH * p.KW * p.wcin * p.K);
+  // row geometry of this lane's TM rows
+  int rb[TM], r1[TM], r2[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const int m = 16 * a + i;
+    rb[a] = 0; r1[a] = -(1 << 28); r2[a] = -(1 << 28);
+    if (m < M) {
+      if constexpr (MODE == MODE_FWD) {
+        const int ohw = p.OH * p.OW;
+        const int n = m / ohw, r = m - n * ohw, oh = r / p.OW, ow = r - oh * p.OW;
+        r1[a] = oh * p.S - p.PT; r2[a] = ow * p.S - p.PL;
+        rb[a] = ((n * p.H + r1[a]) * p.W + r2[a]) * p.xcs + p.xco;
+      } else {
+        const int hw = p.H * p.W;
+        const int n = m / hw, r = m - n * hw, ih = r / p.W, iw = r - ih * p.W;
+        r1[a] = ih + p.PT; r2[a] = iw + p.PL;
+        rb[a] = ((n * p.OH + r1[a]) * p.OW + r2[a]) * p.ycs + p.yco;
+      }
+    }
+  }
+  // issue every load of this wave's k-slice
+  f4 xa[KG][TM], wb[KG][4];
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const int kq = zsplit * KB + wv * KW + 16 * g + 4 * q;
+    const bool kok = kq < Kd;
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = fdiv(kq, p.fC), c = kq - tap * p.C;
+      const int th = fdiv(tap, p.fKW), tw = tap - th * p.KW;
+      const int koff = (th * p.W + tw) * p.xcs + c;
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const bool ok = kok && (unsigned)(r1[a] + th) < (unsigned)p.H && (unsigned)(r2[a] + tw) < (unsigned)p.W;
+        xa[g][a] = bload(rx, ok ? 4 * (rb[a] + koff) : OOB);
+      }
+      const int n = n0 + 4 * i;
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm)
+        wb[g][mm] = bload(rw, kok && c + mm < p.wcin && n < Nn ? 4 * ((tap * p.wcin + c + mm) * p.K + n) : OOB);
+    } else {
+      const int tap = fdiv(kq, p.fK), kx = kq - tap * p.K;
+      const int th = fdiv(tap, p.fKW), tw = tap - th * p.KW;
+      const int koff = -(th * p.OW + tw) * p.ycs + kx;
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const bool ok = kok && (unsigned)(r1[a] - th) < (unsigned)p.OH && (unsigned)(r2[a] - tw) < (unsigned)p.OW;
+        xa[g][a] = bload(rdy, ok ? 4 * (rb[a] + koff) : OOB);
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int c = n0 + 16 * f + i;
+        wb[g][f] = bload(rw, kok && c < p.wcin ? 4 * ((tap * p.wcin + c) * p.K + kx) : OOB);
+      }
+    }
+  }
+  f4 acc[TM][4];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[a][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const float bv = MODE == MODE_FWD ? wb[g][mm][j] : wb[g][j][mm];
+          acc[a][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[g][a][mm], bv, acc[a][j], 0, 0, 0);
+        }
+  // combine the 4 waves (k-slices) in wave order; thread t then owns output columns n0 + (t & 63)
+  float* mine = red + wv * (TM * 16 * 64);
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mine[((a * 4 + j) * 4 + r) * 64 + lane] = acc[a][j][r];
+  __syncthreads();
+  const int cc = tid & 63;                     // column within the tile
+  const int col = n0 + cc;
+  // this column's (fragment, lane i) in the accumulator layout
+  const int jf = MODE == MODE_FWD ? (cc & 3) : (cc >> 4);
+  const int il = MODE == MODE_FWD ? (cc >> 2) : (cc & 15);
+  const bool direct = p.splits == 1;
+  float* base;
+  if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
+  else base = direct ? p.dx : p.ws;
+  for (int rr = tid >> 6; rr < 16 * TM; rr += 4) {   // rows of the tile
+    const int a = rr >> 4, qq = (rr & 15) >> 2, r = rr & 3;
+    const int e = ((a * 4 + jf) * 4 + r) * 64 + qq * 16 + il;
+    const float v = ((red[e] + red[TM * 1024 + e]) + red[2 * TM * 1024 + e]) + red[3 * TM * 1024 + e];
+    if (rr >= M || col >= Nn) continue;
+    long off;
+    if (direct) off = (long)rr * (MODE == MODE_FWD ? p.ycs : p.xcs) + (MODE == MODE_FWD ? p.yco : p.xco) + col;
+    else off = ((long)zsplit * M + rr) * Nn + col;
+    base[off] = (direct && p.accumulate) ? base[off] + v : v;
+  }
 }
 
 // Split-K reduction: dst(row, col) (+)= sum_z ws[z][row][col].  A block is ZL z-lanes x (256/ZL)
@@ -621,6 +807,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, 
 // ------------------------------------------------------------------ host dispatch
 struct Plan {
   int bm, bn, splits, kt_per, gx, gy, gz;
+  int skinny_tm, skinny_kg;   // > 0: skinny_kernel<MODE, TM, KG> (weight-streaming deep layers)
   int rows, cols;  // reduce extent
   size_t slab_bytes, ws_bytes;
 };
@@ -651,12 +838,40 @@ static long env_long(const char* name, long dflt) {
 static const long g_split_target = env_long("TDE_SPLIT_TARGET", 512);   // blocks to aim for
 static const long g_split_minkt = env_long("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
 static const long g_split_slab = env_long("TDE_SPLIT_SLAB_MB", 128) << 20;
+// tile / split overrides for kernel exploration (scripts/conv_micro.py); 0 = planner's choice
+static const long g_force_bn = env_long("TDE_FORCE_BN", 0);
+static const long g_force_bm = env_long("TDE_FORCE_BM", 0);
+static const long g_force_splits = env_long("TDE_FORCE_SPLITS", 0);
 
-static Plan make_plan(const tde_conv_desc_t& d, int mode) {
+static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to which FWD / DGRAD go skinny
+
+// fix_bm / fix_bn > 0: plan with that tile (the fused backward launch needs one tile for both GEMMs)
+static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fix_bn = 0) {
   const int BK = BK3;
   long M, Nn, Kd; int ncls;
   gemm_dims(d, mode, M, Nn, Kd, ncls);
   Plan pl{};
+  if ((mode == MODE_FWD || (mode == MODE_DGRAD && d.stride == 1)) && M <= g_skinny_m && M <= 96 && !fix_bm &&
+      g_conv_math == 0) {
+    // skinny path: 64-column tiles, 4 waves x KG x 16 of k per block; the largest KG (fewest splits)
+    // that still gives >= 256 blocks, TM x KG <= 8 register fragments
+    pl.skinny_tm = (int)((M + 15) / 16);
+    pl.gx = tde_cdiv(Nn, 64);
+    pl.skinny_kg = 1;
+    for (int kg = 4; kg >= 1; kg /= 2) {
+      if (pl.skinny_tm * kg > 8) continue;
+      if ((long)pl.gx * tde_cdiv(Kd, 64 * kg) >= 256 || kg == 1) { pl.skinny_kg = kg; break; }
+    }
+    pl.splits = tde_cdiv(Kd, 64 * pl.skinny_kg);
+    pl.kt_per = 0;
+    pl.gy = pl.splits;
+    pl.gz = 1;
+    pl.bm = 0; pl.bn = 64;
+    pl.rows = (int)M; pl.cols = (int)Nn;
+    pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.rows * pl.cols * sizeof(float) : 0;
+    pl.ws_bytes = pl.slab_bytes;
+    return pl;
+  }
   // N tile: minimise computed columns + a per-tile overhead (~24 columns' worth), so odd widths such
   // as the decoder concats in DGRAD (68, 132, 260 channels) do not run half-empty 128-wide tiles
   {
@@ -668,12 +883,18 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
       if (best < 0 || cost < best || (cost == best && bn > pl.bn)) { best = cost; pl.bn = bn; }
     }
   }
+  if (g_force_bn) pl.bn = (int)g_force_bn;
+  if (fix_bn) pl.bn = fix_bn;
   pl.bm = 128;
   long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   // WGRAD reduces over every pixel (Kd ~ 1e5): parallelism comes from split-K, so keep the
   // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.
-  if (mode != MODE_WGRAD && tiles < 256 && M <= 4096) {
+  if ((mode != MODE_WGRAD && tiles < 256 && M <= 4096) || g_force_bm == 64 || fix_bm == 64) {
     pl.bm = 64;
+    tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
+  }
+  if (fix_bm == 128 && pl.bm != 128) {
+    pl.bm = 128;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
   const int nkt = tde_cdiv(Kd, BK);
@@ -690,6 +911,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
     long cols = mode == MODE_DGRAD ? d.C : Nn;
     while (splits > 1 && (long)splits * rows * cols * 4 > g_split_slab) splits /= 2;
   }
+  if (g_force_splits) splits = (int)(g_force_splits < nkt ? g_force_splits : nkt);
   pl.kt_per = tde_cdiv(nkt, splits);
   pl.splits = tde_cdiv(nkt, pl.kt_per);
   pl.gx = tde_cdiv(M, pl.bm);
@@ -699,7 +921,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode) {
   else if (mode == MODE_DGRAD) { pl.rows = d.N * d.H * d.W; pl.cols = d.C; }
   else { pl.rows = (int)M; pl.cols = (int)Nn; }
   pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.rows * pl.cols * sizeof(float) : 0;
-  pl.ws_bytes = TDE_WS_HDR + pl.slab_bytes;
+  pl.ws_bytes = pl.slab_bytes;
   return pl;
 }
 
@@ -745,16 +967,51 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   return pl.ws_bytes + bn_plan(d, mode, pl).part_bytes;
 }
 
+// prefetch depth (tiles in flight) of the fp32 kernels: 1 for 128-row tiles, 2 for the 64-row tiles of
+// the deep layers (TDE_CONV_PF: 1 / 2 forces one depth for all, tuning experiments)
+static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
+
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   constexpr int WN = BN % 32 == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
-  if (g_conv_math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN>), grid, dim3(NT), 0, st, a);
+  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? 2 : 1);
+  if (g_conv_math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  else if (pf == 2) hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+}
+
+template <int MODE, int TM>
+static void launch_skinny_tm(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  const dim3 grid(pl.gx, pl.gy);
+  switch (pl.skinny_kg) {
+    case 4: if constexpr (TM <= 2) hipLaunchKernelGGL((skinny_kernel<MODE, TM, 4>), grid, dim3(NT), 0, st, a); break;
+    case 2: if constexpr (TM <= 4) hipLaunchKernelGGL((skinny_kernel<MODE, TM, 2>), grid, dim3(NT), 0, st, a); break;
+    default: hipLaunchKernelGGL((skinny_kernel<MODE, TM, 1>), grid, dim3(NT), 0, st, a); break;
+  }
+}
+
+template <int MODE>
+static void launch_skinny(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  if constexpr (MODE == MODE_WGRAD) return;
+  else {
+    switch (pl.skinny_tm) {
+      case 1: launch_skinny_tm<MODE, 1>(pl, a, st); break;
+      case 2: launch_skinny_tm<MODE, 2>(pl, a, st); break;
+      case 3: launch_skinny_tm<MODE, 3>(pl, a, st); break;
+      case 4: launch_skinny_tm<MODE, 4>(pl, a, st); break;
+      case 5: launch_skinny_tm<MODE, 5>(pl, a, st); break;
+      default: launch_skinny_tm<MODE, 6>(pl, a, st); break;
+    }
+  }
 }
 
 template <int MODE>
 static void launch_mode(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  if (pl.skinny_tm > 0) {
+    launch_skinny<MODE>(pl, a, st);
+    return;
+  }
   dim3 grid(pl.gx, pl.gy, pl.gz);
   if (pl.bm == 128) {
     switch (pl.bn) {
@@ -797,9 +1054,33 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
   return a;
 }
 
+// Timing experiments only (results are garbage): skip every conv launch of layers whose forward
+// output has <= / > this many pixels, to measure what those layers cost inside the captured step.
+static const long g_skip_le = env_long("TDE_SKIP_CONV_LE", -1);
+static const long g_skip_gt = env_long("TDE_SKIP_CONV_GT", -1);
+static const long g_skip_what = env_long("TDE_SKIP_WHAT", 3);   // bit 0: GEMM kernels, bit 1: reduces
+static bool skip_conv(const tde_conv_desc_t* d) {
+  const long m = (long)d->N * d->OH * d->OW;
+  return (g_skip_le >= 0 && m <= g_skip_le) || (g_skip_gt >= 0 && m > g_skip_gt);
+}
+
+template <int MODE>
+static void launch_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  if (pl.splits <= 1) return;
+  const long n4 = (long)pl.rows * (pl.cols / 4);
+  // z-lanes per output quad: fill >= ~256 blocks, keep >= 4 splits per lane
+  int zl = 1;
+  while (zl < 64 && (n4 * zl * 2 + 255) / 256 <= 256 && pl.splits / (zl * 2) >= 4) zl *= 2;
+  long blocks = (n4 * zl + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3((int)blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
+}
+
 template <int MODE>
 static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
                size_t ws_bytes, void* stream) {
+  const bool skipm = skip_conv(d);
+  const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   const Plan pl = make_plan(*d, MODE);
   BnPlan bp{};
   if (bn) bp = bn_plan(*d, MODE, pl);
@@ -813,17 +1094,9 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   a.bnp = (bn && bp.path == BN_EPI) ? part : nullptr;
   a.bn_gx = pl.gx;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  launch_mode<MODE>(pl, a, st);
+  if (!skip) launch_mode<MODE>(pl, a, st);
   float* z = MODE == MODE_FWD ? a.y : (MODE == MODE_DGRAD ? a.dx : a.dw);
-  if (pl.splits > 1 && !(bn && bp.path == BN_REDUCE)) {
-    const long n4 = (long)pl.rows * (pl.cols / 4);
-    // z-lanes per output quad: fill >= ~256 blocks, keep >= 4 splits per lane
-    int zl = 1;
-    while (zl < 64 && (n4 * zl * 2 + 255) / 256 <= 256 && pl.splits / (zl * 2) >= 4) zl *= 2;
-    long blocks = (n4 * zl + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3((int)blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
-  }
+  if (!skipr && !(bn && bp.path == BN_REDUCE)) launch_reduce<MODE>(pl, a, st);
   if (bn) {
     // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
     const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
@@ -831,13 +1104,76 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     if (bp.path == BN_SMALL) {
       bn_fwd_small_launch(pl.rows, pl.cols, z, o, st);
     } else {
-      if (bp.path == BN_REDUCE)
+      if (bp.path == BN_REDUCE && !skipr)
         hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws,
                            pl.splits, pl.rows, pl.cols, z, bp.ch.rows_per_chunk, part);
       bn_fwd_from_partials_launch(pl.rows, pl.cols, z, bp.nparts, part, o, st);
     }
   }
   return tde_launch_status();
+}
+
+template <int MODE1, int BM, int BN>
+static void launch_bwd2_cfg(const Plan& p1, const ConvArgs& a1, const Plan& p2, const ConvArgs& a2, hipStream_t st) {
+  constexpr int WN = BN % 32 == 0 ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  const int nd = p1.gx * p1.gy * p1.gz, nw = p2.gx * p2.gy * p2.gz;
+  hipLaunchKernelGGL((igemm_bwd2_kernel<MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx, p1.gy,
+                     p2.gx, p2.gy, nd);
+}
+
+template <int MODE1>
+static void launch_bwd2(const Plan& p1, const ConvArgs& a1, const Plan& p2, const ConvArgs& a2, hipStream_t st) {
+  switch (p1.bm * 1000 + p1.bn) {
+#define BWD2_CASE(BM_, BN_) case BM_ * 1000 + BN_: launch_bwd2_cfg<MODE1, BM_, BN_>(p1, a1, p2, a2, st); break;
+    BWD2_CASE(128, 16) BWD2_CASE(128, 32) BWD2_CASE(128, 48) BWD2_CASE(128, 64) BWD2_CASE(128, 96)
+    BWD2_CASE(128, 128) BWD2_CASE(64, 16) BWD2_CASE(64, 32) BWD2_CASE(64, 48) BWD2_CASE(64, 64)
+    BWD2_CASE(64, 96) BWD2_CASE(64, 128)
+#undef BWD2_CASE
+    default: break;
+  }
+}
+
+static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches (A/B experiments)
+
+
+// Data + filter gradient of one layer.  MODE1 = the data-gradient GEMM of the virtual conv (DGRAD for a
+// conv, FWD for a deconv); the filter gradient is always its WGRAD.  One fused launch when the data
+// gradient's tile fits the filter gradient (re-planned on that tile), then the split-K reduces.
+template <int MODE1>
+static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2, int acc2, void* ws, size_t ws_bytes,
+                   void* stream) {
+  const bool skipm = skip_conv(d);
+  const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  const Plan p1 = make_plan(*d, MODE1);
+  const bool fuse = g_bwd_fuse != 0 && g_conv_math == 0 && p1.skinny_tm == 0;
+  const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : make_plan(*d, MODE_WGRAD);
+  if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  char* body = tde_ws_body(ws);
+  a1.ws = reinterpret_cast<float*>(body);
+  a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
+  a2.ws = reinterpret_cast<float*>(body + p1.slab_bytes);
+  a2.splits = p2.splits; a2.kt_per = p2.kt_per; a2.accumulate = acc2; a2.bnp = nullptr;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (skip) {
+  } else if (fuse) {
+    launch_bwd2<MODE1>(p1, a1, p2, a2, st);
+  } else {
+    launch_mode<MODE1>(p1, a1, st);
+    launch_mode<MODE_WGRAD>(p2, a2, st);
+  }
+  if (!skipr) {
+    launch_reduce<MODE1>(p1, a1, st);
+    launch_reduce<MODE_WGRAD>(p2, a2, st);
+  }
+  return tde_launch_status();
+}
+
+static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
+  const Plan p1 = make_plan(d, mode1);
+  const size_t fused = p1.skinny_tm ? 0 : p1.slab_bytes + make_plan(d, MODE_WGRAD, p1.bm, p1.bn).slab_bytes;
+  const size_t split = p1.slab_bytes + make_plan(d, MODE_WGRAD).slab_bytes;
+  return (fused > split ? fused : split) + 64;
 }
 
 static bool bn_ok(const tde_bn_train_t* bn, int C) {
@@ -915,6 +1251,35 @@ int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const fl
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = z_big;
   return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream);
+}
+
+size_t tde_conv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
+  return desc_ok(d) ? bwd_ws_bytes(*d, MODE_DGRAD) : 0;
+}
+
+size_t tde_deconv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
+  return desc_ok(d) ? bwd_ws_bytes(*d, MODE_FWD) : 0;
+}
+
+int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, const float* w, float* dx,
+                   int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx) &&
+                tde_aligned16(dw));
+  ConvArgs a1 = make_args(*d), a2 = make_args(*d);
+  a1.dy = dy; a1.w = w; a1.dx = dx;
+  a2.x = x; a2.dy = dy; a2.dw = dw;
+  return run_bwd<MODE_DGRAD>(d, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, const float* w,
+                     float* dx_small, int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes,
+                     void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(x_small) && tde_aligned16(w) &&
+                tde_aligned16(dx_small) && tde_aligned16(dw));
+  ConvArgs a1 = make_args(*d), a2 = make_args(*d);
+  a1.x = dy_big; a1.w = w; a1.y = dx_small;          // data gradient = Conv2D(dy_big) (virtual FWD)
+  a2.x = dy_big; a2.dy = x_small; a2.dw = dw;        // filter gradient (virtual WGRAD)
+  return run_bwd<MODE_FWD>(d, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,

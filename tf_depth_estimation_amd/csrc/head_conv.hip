@@ -21,6 +21,7 @@ struct HeadArgs {
   float* y; const float* yin; const float* dy; int ycs, yco;
   float* dx; int acc_dx;
   const float* dz;   // [M][K] dense (backward)
+  float* dzw;        // same buffer, written by the wgrad pass
   int act; float scale, offset;
 };
 
@@ -77,6 +78,115 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const HeadArgs p) {
 #pragma unroll
       for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[k] + p.b[k], p.act, p.scale, p.offset);
     }
+  }
+}
+
+// Weights of a head staged in LDS once per block: [tap][wcin][KC] (<= HEAD_WMAX floats; every head of
+// the reference nets fits: 3x3x128x2, 7x7x16x2, 1x1x256x6).
+constexpr int HEAD_WMAX = 4608;
+
+__device__ __forceinline__ void stage_weights(const float* w, int n, float* sw) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) sw[i] = w[i];
+  __syncthreads();
+}
+
+// Forward, taps unrolled (KS x KS, stride 1): L lanes per output pixel, each lane QPL channel quads;
+// all of a lane's activation loads (KS*KS*QPL branch-free buffer loads) are issued before the FMAs,
+// weights from LDS, xor-shuffle combine, bias + activation fused.
+template <int KC, int KS, int L, int QPL>
+__global__ void __launch_bounds__(256) head_fwd2_kernel(const HeadArgs p) {
+  __shared__ __attribute__((aligned(16))) float sw[HEAD_WMAX];
+  stage_weights(p.w, KS * KS * p.wcin * KC, sw);
+  constexpr int PPB = 256 / L;
+  const int lane = threadIdx.x & (L - 1);
+  const long M = (long)p.N * p.OH * p.OW;
+  const long m = (long)blockIdx.x * PPB + threadIdx.x / L;
+  const int CQ = (p.wcin + 3) / 4;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  float acc[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) acc[k] = 0.f;
+  const long mm = m < M ? m : 0;
+  const int ohw = p.OH * p.OW;
+  const int n = (int)(mm / ohw), r = (int)(mm - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
+  const int base = ((n * p.H + oh - p.PT) * p.W + ow - p.PL) * p.xcs + p.xco;
+  f4 xv[KS * KS][QPL];
+#pragma unroll
+  for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) {
+      const bool ok = m < M && (unsigned)(oh - p.PT + kh) < (unsigned)p.H && (unsigned)(ow - p.PL + kw) < (unsigned)p.W;
+#pragma unroll
+      for (int u = 0; u < QPL; ++u) {
+        const int cq = lane + u * L;
+        xv[kh * KS + kw][u] = bload(rx, ok && cq < CQ ? 4 * (base + (kh * p.W + kw) * p.xcs + 4 * cq) : OOB);
+      }
+    }
+#pragma unroll
+  for (int t = 0; t < KS * KS; ++t) {
+    const float* wp = sw + t * p.wcin * KC;
+#pragma unroll
+    for (int u = 0; u < QPL; ++u) {
+      const int c0 = 4 * (lane + u * L);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        if (c < p.wcin) {
+#pragma unroll
+          for (int k = 0; k < KC; ++k) acc[k] = fmaf(xv[t][u][j], wp[c * KC + k], acc[k]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < KC; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+  if (m < M && lane == 0) {
+    float* yp = p.y + m * p.ycs + p.yco;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[k] + p.b[k], p.act, p.scale, p.offset);
+  }
+}
+
+// Data gradient, taps unrolled, weights from LDS: thread = (input pixel, channel quad), stride 1.
+template <int KC, int KS>
+__global__ void __launch_bounds__(256) head_dgrad2_kernel(const HeadArgs p) {
+  __shared__ __attribute__((aligned(16))) float sw[HEAD_WMAX];
+  stage_weights(p.w, KS * KS * p.wcin * KC, sw);
+  const int CQ = p.C / 4;
+  const long total = (long)p.N * p.H * p.W * CQ;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / CQ;
+    const int c = 4 * (int)(i - pix * CQ);
+    const int hw = p.H * p.W;
+    const int n = (int)(pix / hw), r = (int)(pix - (long)n * hw), ih = r / p.W, iw = r - ih * p.W;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < p.wcin) {
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        const int oh = ih + p.PT - kh;
+        if ((unsigned)oh >= (unsigned)p.OH) continue;
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const int ow = iw + p.PL - kw;
+          if ((unsigned)ow >= (unsigned)p.OW) continue;
+          const float* dzp = p.dz + ((long)(n * p.OH + oh) * p.OW + ow) * KC;
+          const float* wp = sw + ((kh * KS + kw) * p.wcin + c) * KC;
+#pragma unroll
+          for (int k = 0; k < KC; ++k) {
+            const float dz = dzp[k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (c + j < p.wcin) acc[j] = fmaf(dz, wp[j * KC + k], acc[j]);
+          }
+        }
+      }
+    }
+    float* dst = p.dx + pix * p.xcs + p.xco + c;
+    f4 out = acc;
+    if (p.acc_dx) out += *reinterpret_cast<const f4*>(dst);
+    *reinterpret_cast<f4*>(dst) = out;
   }
 }
 
@@ -170,9 +280,18 @@ __global__ void __launch_bounds__(256) head_wgrad_partial_kernel(const HeadArgs 
   for (int k = 0; k < KC; ++k) bacc[k] = 0.f;
   if (pl < P) {
     for (long pix = cbeg + pl; pix < cend; pix += P) {
+      // dL/dz from y and dL/dy (sigmoid head) computed here; tap group 0's first channel-quad lane
+      // stores it for the data-gradient pass
       float dz[KC];
 #pragma unroll
-      for (int k = 0; k < KC; ++k) dz[k] = p.dz[pix * KC + k];
+      for (int k = 0; k < KC; ++k) {
+        const long o = pix * p.ycs + p.yco + k;
+        dz[k] = head_dz(p.yin[o], p.dy[o], p.act, p.scale, p.offset);
+      }
+      if (blockIdx.y == 0 && q == 0) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) p.dzw[pix * KC + k] = dz[k];
+      }
 #pragma unroll
       for (int k = 0; k < KC; ++k) bacc[k] += dz[k];
       const int n = (int)(pix / ohw), r = (int)(pix - (long)n * ohw), oh = r / p.OW, ow = r - oh * p.OW;
@@ -298,15 +417,73 @@ size_t dz_bytes(const tde_conv_desc_t* d) {
   return (n + 255) / 256 * 256;
 }
 
+template <int KC, int KS, int QPL>
+void launch_fwd_l(const HeadArgs& a, long M, int L, hipStream_t st) {
+  const dim3 g((unsigned)((M * L + 255) / 256));
+  switch (L) {
+    case 1: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 1, QPL>), g, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 2, QPL>), g, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 4, QPL>), g, dim3(256), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 8, QPL>), g, dim3(256), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 16, QPL>), g, dim3(256), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 32, QPL>), g, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((head_fwd2_kernel<KC, KS, 64, QPL>), g, dim3(256), 0, st, a); break;
+  }
+}
+
+template <int KC, int KS>
+void launch_fwd_ks(const HeadArgs& a, long M, hipStream_t st) {
+  // lanes per pixel: enough threads (~64K) in flight, then quads per lane (QPL) from the channel count;
+  // at most 36 activation vectors in flight per lane
+  const int cq = (a.wcin + 3) / 4;
+  constexpr int QMAX = KS * KS >= 25 ? 1 : (KS == 3 ? 4 : 8);
+  int L = 1;
+  while (L < 64 && (M * L < 65536 || (cq + L - 1) / L > QMAX)) L *= 2;
+  const int qpl = (cq + L - 1) / L;
+  if (qpl <= 1) launch_fwd_l<KC, KS, 1>(a, M, L, st);
+  else if (qpl <= 2) launch_fwd_l<KC, KS, (QMAX >= 2 ? 2 : 1)>(a, M, L, st);
+  else if (qpl <= 4) launch_fwd_l<KC, KS, (QMAX >= 4 ? 4 : 1)>(a, M, L, st);
+  else launch_fwd_l<KC, KS, (QMAX >= 8 ? 8 : 1)>(a, M, L, st);
+}
+
 template <int KC>
 int launch_fwd(const HeadArgs& a, long M, hipStream_t st) {
-  const int cq = (a.wcin + 3) / 4;
-  const int L = cq <= 4 ? 4 : (cq <= 8 ? 8 : 16);
-  const long blocks = (M * L + 255) / 256;
-  const dim3 g((unsigned)(blocks > 16384 ? 16384 : blocks));
-  if (L == 4) hipLaunchKernelGGL((head_fwd_kernel<KC, 4>), g, dim3(256), 0, st, a);
-  else if (L == 8) hipLaunchKernelGGL((head_fwd_kernel<KC, 8>), g, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((head_fwd_kernel<KC, 16>), g, dim3(256), 0, st, a);
+  if (a.KH != a.KW || a.S != 1 || a.KH * a.KW * a.wcin * KC > HEAD_WMAX) {
+    // generic fallback (unused by the reference nets): lanes split channels, weights from global
+    const int cq = (a.wcin + 3) / 4;
+    const int L = cq <= 4 ? 4 : (cq <= 8 ? 8 : 16);
+    const long blocks = (M * L + 255) / 256;
+    const dim3 g((unsigned)(blocks > 16384 ? 16384 : blocks));
+    if (L == 4) hipLaunchKernelGGL((head_fwd_kernel<KC, 4>), g, dim3(256), 0, st, a);
+    else if (L == 8) hipLaunchKernelGGL((head_fwd_kernel<KC, 8>), g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((head_fwd_kernel<KC, 16>), g, dim3(256), 0, st, a);
+    return TDE_OK;
+  }
+  switch (a.KH) {
+    case 1: launch_fwd_ks<KC, 1>(a, M, st); break;
+    case 3: launch_fwd_ks<KC, 3>(a, M, st); break;
+    case 5: launch_fwd_ks<KC, 5>(a, M, st); break;
+    case 7: launch_fwd_ks<KC, 7>(a, M, st); break;
+    default: return TDE_ERR_UNSUPPORTED;
+  }
+  return TDE_OK;
+}
+
+template <int KC>
+int launch_dgrad(const HeadArgs& a, hipStream_t st) {
+  const long n = (long)a.N * a.H * a.W * (a.C / 4);
+  const dim3 g(grid_for(n));
+  if (a.KH != a.KW || a.KH * a.KW * a.wcin * KC > HEAD_WMAX) {
+    hipLaunchKernelGGL(head_dgrad_kernel<KC>, g, dim3(256), 0, st, a);
+    return TDE_OK;
+  }
+  switch (a.KH) {
+    case 1: hipLaunchKernelGGL((head_dgrad2_kernel<KC, 1>), g, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((head_dgrad2_kernel<KC, 3>), g, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((head_dgrad2_kernel<KC, 5>), g, dim3(256), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((head_dgrad2_kernel<KC, 7>), g, dim3(256), 0, st, a); break;
+    default: return TDE_ERR_UNSUPPORTED;
+  }
   return TDE_OK;
 }
 
@@ -326,7 +503,7 @@ size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
   const WgPlan w = wg_plan(d);
   const size_t part = (size_t)w.chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
-  return TDE_WS_HDR + dz_bytes(d) + part;
+  return dz_bytes(d) + part;
 }
 
 int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, float* y,
@@ -360,22 +537,37 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   const long M = (long)d->N * d->OH * d->OW;
   float* dz = static_cast<float*>(ws);
   a.dz = dz;
-  hipLaunchKernelGGL(head_dz_kernel, dim3(grid_for(M * d->K)), dim3(256), 0, st, M, d->K, y, dy, d->y_cstride,
-                     d->y_coff, act, scale, offset, dz);
-  if (dx) {
-    TDE_CHECK_ARG(tde_aligned16(dx));
-    const long n = (long)d->N * d->H * d->W * (d->C / 4);
-    HEAD_DISPATCH(d->K, head_dgrad_kernel, dim3(grid_for(n)), a);
-  }
+  a.dzw = dz;
+  TDE_CHECK_ARG(!dx || tde_aligned16(dx));
+  TDE_CHECK_ARG(!dw || dbias != nullptr);
+  // the wgrad pass computes dz on the fly and stores it; without a weight gradient a dz pass does that
   if (dw) {
-    TDE_CHECK_ARG(dbias != nullptr);
     float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
     const WgPlan wp = wg_plan(d);
     HEAD_DISPATCH(d->K, head_wgrad_partial_kernel, dim3(wp.chunks, wp.tgroups), a, part, wp.ppc);
+    if (dx) {
+      int rc = TDE_OK;
+      switch (d->K) {
+        case 1: rc = launch_dgrad<1>(a, st); break;
+        case 2: rc = launch_dgrad<2>(a, st); break;
+        default: rc = launch_dgrad<6>(a, st); break;
+      }
+      if (rc != TDE_OK) return rc;
+    }
     const int E = d->KH * d->KW * d->w_cin;
     const int total = E * d->K + d->K;
     hipLaunchKernelGGL(head_wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, st, part, wp.chunks, total,
                        E * d->K, dw, dbias, accumulate_dw);
+  } else if (dx) {
+    hipLaunchKernelGGL(head_dz_kernel, dim3(grid_for(M * d->K)), dim3(256), 0, st, M, d->K, y, dy, d->y_cstride,
+                       d->y_coff, act, scale, offset, dz);
+    int rc = TDE_OK;
+    switch (d->K) {
+      case 1: rc = launch_dgrad<1>(a, st); break;
+      case 2: rc = launch_dgrad<2>(a, st); break;
+      default: rc = launch_dgrad<6>(a, st); break;
+    }
+    if (rc != TDE_OK) return rc;
   }
   return tde_launch_status();
 }

@@ -101,19 +101,22 @@ int ew_grid(long n) {
 // the full-resolution label (integer factor 2^s, same summation order as tde_resize_area_fwd).
 struct PyrArgs {
   tde_depth_loss_t a;
-  long start[TDE_MAX_SCALES + 1];   // first flat pixel index of each scale
+  int bstart[TDE_MAX_SCALES + 1];   // first block of each scale (a block works on ONE scale, so the
+                                    // per-scale parameters are indexed uniformly: scalar loads)
 };
 
 __global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
   __shared__ double sh[4];
   const tde_depth_loss_t& a = P.a;
   double ls = 0.0, ll = 0.0;
-  const long total = P.start[a.nscales];
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    int s = 0;
-    while (idx >= P.start[s + 1]) ++s;
-    const long loc = idx - P.start[s];
-    const int H = a.H >> s, W = a.W >> s;
+  int s = 0;
+  while ((int)blockIdx.x >= P.bstart[s + 1]) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  const int H = a.H >> s, W = a.W >> s;
+  const long total = (long)a.N * H * W;
+  const int nb = P.bstart[s + 1] - P.bstart[s];
+  for (long loc = (blockIdx.x - P.bstart[s]) * (long)blockDim.x + threadIdx.x; loc < total;
+       loc += (long)nb * blockDim.x) {
     const int j = (int)(loc % W);
     const long t = loc / W;
     const int i = (int)(t % H), n = (int)(t / H);
@@ -198,13 +201,14 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
   PyrArgs P;
   P.a = *a;
-  P.start[0] = 0;
+  P.bstart[0] = 0;
   for (int s = 0; s < a->nscales; ++s) {
     TDE_CHECK_ARG(a->pred[s] && a->grad[s] && (a->H >> s) > 0 && (a->W >> s) > 0);
     TDE_CHECK_ARG(a->l1_w[s] == 0.f || (a->label && a->H % (1 << s) == 0 && a->W % (1 << s) == 0));
-    P.start[s + 1] = P.start[s] + (long)a->N * (a->H >> s) * (a->W >> s);
+    P.bstart[s + 1] = P.bstart[s] + ew_grid((long)a->N * (a->H >> s) * (a->W >> s));
   }
-  hipLaunchKernelGGL(depth_pyramid_kernel, dim3(ew_grid(P.start[a->nscales])), dim3(256), 0,
+  for (int s = a->nscales; s < TDE_MAX_SCALES; ++s) P.bstart[s + 1] = P.bstart[s];
+  hipLaunchKernelGGL(depth_pyramid_kernel, dim3(P.bstart[a->nscales]), dim3(256), 0,
                      static_cast<hipStream_t>(stream), P);
   return tde_launch_status();
 }

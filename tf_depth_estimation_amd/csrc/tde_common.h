@@ -21,16 +21,20 @@ static inline bool tde_aligned16(const void* p) { return (reinterpret_cast<uintp
 
 static inline int tde_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
-// Every workspace starts with TDE_WS_HEADER_BYTES of uint32 arrival counters (include/tde.h): the
-// deterministic "last block reduces" steps of the conv and BN kernels count tile arrivals there and
-// reset their counter to zero before exiting, so a workspace zeroed once stays valid for every call.
-constexpr size_t TDE_WS_HDR = TDE_WS_HEADER_BYTES;
-constexpr int TDE_CNT_SPLIT = 0;        // [0, 8192): split-K tiles of one conv launch
-constexpr int TDE_CNT_SPLIT_MAX = 8192;
-constexpr int TDE_CNT_BN = 8192;        // [8192, 16384): BN statistics groups and column tiles
-constexpr int TDE_CNT_BN_MAX = 8192;
-static inline unsigned* tde_ws_counters(void* ws) { return static_cast<unsigned*>(ws); }
-static inline char* tde_ws_body(void* ws) { return static_cast<char*>(ws) + TDE_WS_HDR; }
+static inline char* tde_ws_body(void* ws) { return static_cast<char*>(ws); }
+
+// Raw buffer resource over n floats (byte range clamped below 2^31 so OOB is always out of range;
+// 0x00020000 = DATA_FORMAT 32 for gfx9-family raw buffers).  An access at byte offset OOB reads zero:
+// branch-free predicated loads.
+constexpr int OOB = (int)0x80000000;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, long n) {
+  const long bytes = 4 * n;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0,
+                                           (int)(bytes < 0x7fffffffl ? bytes : 0x7fffffffl), 0x00020000);
+}
+__device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 __device__ __forceinline__ float tde_sign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 

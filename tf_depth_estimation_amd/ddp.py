@@ -86,7 +86,6 @@ class GradSync:
         self.gpu = self.device.type == "cuda"
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
         self.capturing = None       # set by Trainer.capture: callable(buckets) closing a graph segment
-        self.producers = []         # NetPrograms whose side (WGRAD) stream also writes gradients
         self.log = []               # launch order (names), for tests
         self.begin_step()
 
@@ -139,9 +138,6 @@ class GradSync:
         ev = torch.cuda.Event()
         ev.record()
         self.comm.wait_event(ev)
-        for p in self.producers:          # filter gradients are written on the programs' side streams
-            if p._side is not None:
-                self.comm.wait_stream(p._side)
         lib = _lib.load()
         with torch.cuda.stream(self.comm):
             st = _lib.stream_ptr()

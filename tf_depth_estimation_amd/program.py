@@ -15,8 +15,6 @@ accumulate into the ParamChunk's flat gradient buffer, which the trainer zeroes 
 network called twice with shared variables (train_depth_then_cam_lr.py:130-136) sums both calls like
 TF does.
 """
-import os
-
 import numpy as np
 import torch
 
@@ -191,28 +189,19 @@ class NetSpec:
 
 
 class Workspace:
-    """Per-(program, batch) scratch: the split-K / reduction workspace of the main stream, a second one
-    for the filter-gradient stream, and one dense dz buffer per BN layer (a layer's dz is read by its
-    WGRAD on the side stream while the main stream already runs the next layer's BN backward)."""
+    """Per-(program, batch) scratch shared by all calls on one stream: the split-K / reduction workspace
+    and the dense dz buffer of the BN backward."""
 
     def __init__(self):
         self.ws = None
-        self.ws_side = None
-        self.dz = {}
+        self.dz = None
 
-    def get(self, ws_bytes, device):
+    def get(self, ws_bytes, dz_numel, device):
         if self.ws is None or self.ws.numel() * 4 < ws_bytes:
-            # zeroed once: the leading TDE_WS_HEADER_BYTES are tile counters every call leaves at zero
-            self.ws = torch.zeros(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
-            self.ws_side = torch.zeros(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
-        return self.ws, self.ws_side
-
-    def dz_for(self, i, numel, device):
-        t = self.dz.get(i)
-        if t is None or t.numel() < numel:
-            t = torch.empty(max(numel, 4), dtype=torch.float32, device=device)
-            self.dz[i] = t
-        return t
+            self.ws = torch.empty(max(ws_bytes // 4 + 64, 64), dtype=torch.float32, device=device)
+        if self.dz is None or self.dz.numel() < dz_numel:
+            self.dz = torch.empty(max(dz_numel, 4), dtype=torch.float32, device=device)
+        return self.ws, self.dz
 
 
 class NetRun:
@@ -252,11 +241,7 @@ class NetProgram:
         self.prefix = chunk.prefix
         self._ws = {}
         self._sizes = {}
-        self._side = None
         self.timer = None
-        # WGRAD of layers with at most this many output pixels runs on a side stream, concurrent with the
-        # DGRAD/BN chain (large layers fill the chip alone; overlapping them only adds contention)
-        self.overlap_max_pixels = int(os.environ.get("TDE_OVERLAP_MAXM", "0"))
 
     def _span(self, family, flops=0.0, nbytes=0.0):
         return NO_SPAN if self.timer is None else self.timer.span(family, flops, nbytes)
@@ -271,30 +256,24 @@ class NetProgram:
     def _scratch(self, N):
         if N not in self._sizes:
             lib = _lib.load()
-            ws = 0
+            ws, dz = 0, 0
             for op in self.spec.ops:
                 if isinstance(op, ConvBN):
                     d = op.desc(N)
                     q = lib.tde_deconv2d_workspace_size if op.deconv else lib.tde_conv2d_workspace_size
                     for o in range(4):
                         ws = max(ws, q(ctypes_ref(d), o))
+                    qb = lib.tde_deconv2d_bwd_workspace_size if op.deconv else lib.tde_conv2d_bwd_workspace_size
+                    ws = max(ws, qb(ctypes_ref(d)))
                     M = N * op.dst.H * op.dst.W
                     ws = max(ws, lib.tde_bn_workspace_size(M, op.K))
+                    dz = max(dz, M * op.K)
                 elif isinstance(op, Head):
                     ws = max(ws, lib.tde_head_workspace_size(ctypes_ref(op.desc(N))))
-            self._sizes[N] = ws
+            self._sizes[N] = (ws, dz)
+        ws, dz = self._sizes[N]
         w = self._ws.setdefault(N, Workspace())
-        return w.get(self._sizes[N], "cuda")
-
-    def _dz(self, N, i, numel):
-        return self._ws.setdefault(N, Workspace()).dz_for(i, numel, "cuda")
-
-    def side_stream(self):
-        """Stream of the filter-gradient (WGRAD) launches; forked from / joined into the caller's stream
-        inside every backward call, so it is captured into the same hipGraph as a parallel branch."""
-        if self._side is None:
-            self._side = torch.cuda.Stream()
-        return self._side
+        return w.get(ws, dz, "cuda")
 
     # ---------------------------------------------------------------- forward
     def forward(self, run, x, is_training=True):
@@ -402,15 +381,9 @@ class NetProgram:
             g = g.contiguous()
             _lib.check(lib.tde_copy_view(N * v.H * v.W, v.C, ptr(g), v.C, 0, run.vptr(v, True), v.buf.cs, v.coff,
                                          acc, st), "grad_out")
-        ws, ws_side = self._scratch(N)
+        ws, dz = self._scratch(N)
         wsb = ws.numel() * 4
         iv = spec.input_view
-        # Filter gradients run on a side stream: the WGRAD of layer i only needs dz_i and x_i, and nothing
-        # later in the backward chain (BN backward -> DGRAD -> ...) needs dW, so the two chains overlap.
-        # Serialized when instrumented (per-kernel event times must not include a concurrent kernel).
-        side = self.side_stream() if (self.overlap_max_pixels > 0 and self.timer is None) else None
-        main = torch.cuda.current_stream()
-        forked = False
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             if self.timer is not None:
@@ -420,8 +393,6 @@ class NetProgram:
                 d = op.desc(N)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
-                lside = side is not None and M <= self.overlap_max_pixels
-                dz = self._dz(N, i, M * op.K) if lside else self._dz(N, -1, self._max_dz(N))
                 with self._span("bn_bwd"):
                     _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
                                               ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
@@ -430,25 +401,26 @@ class NetProgram:
                                op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
-                wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
-                a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
-                if lside:
-                    side.wait_stream(main)
-                    forked = True
-                    with torch.cuda.stream(side):
-                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws_side), ws_side.numel() * 4,
-                                      _lib.stream_ptr()), op.layer + " wgrad")
+                if src_needs:
+                    # data + filter gradient: one fused launch (tde_conv2d_bwd / tde_deconv2d_bwd)
+                    acc = mark(op.src)
+                    with self._span("conv_bwd", 2 * fl, 2 * conv_bytes(op, N)):
+                        if op.deconv:
+                            _lib.check(lib.tde_deconv2d_bwd(ctypes_ref(d), ptr(dz), run.vptr(op.src), ptr(w),
+                                                            run.vptr(op.src, True), acc, ptr(gw), pacc, ptr(ws), wsb,
+                                                            st), op.layer + " bwd")
+                        else:
+                            _lib.check(lib.tde_conv2d_bwd(ctypes_ref(d), run.vptr(op.src), ptr(dz), ptr(w),
+                                                          run.vptr(op.src, True), acc, ptr(gw), pacc, ptr(ws), wsb,
+                                                          st), op.layer + " bwd")
                 else:
+                    # first layer: no input gradient
+                    wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
+                    a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
                     with self._span("conv_wgrad", fl, conv_bytes(op, N)):
                         _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
                 if on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
-                if src_needs:
-                    acc = mark(op.src)
-                    dg = lib.tde_deconv2d_bwd_data if op.deconv else lib.tde_conv2d_bwd_data
-                    with self._span("conv_dgrad", fl, conv_bytes(op, N)):
-                        _lib.check(dg(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True), acc, ptr(ws), wsb, st),
-                                   op.layer + " dgrad")
             elif isinstance(op, Head):
                 d = op.desc(N)
                 acc = mark(op.src) if src_needs else 0
@@ -472,20 +444,9 @@ class NetProgram:
                 acc = mark(s)
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
-        if forked:
-            main.wait_stream(side)
         if need_input_grad:
             return run.view_tensor(iv, grad=True)[..., :spec.cin]
         return None
-
-    def join(self):
-        """Order the current stream after this program's side stream (closing a graph segment with the
-        WGRAD branch still forked would leave the capture unjoined)."""
-        if self._side is not None:
-            torch.cuda.current_stream().wait_stream(self._side)
-
-    def _max_dz(self, N):
-        return max([N * op.dst.H * op.dst.W * op.K for op in self.spec.ops if isinstance(op, ConvBN)] + [4])
 
 
 def ctypes_ref(d):

@@ -68,7 +68,6 @@ class Trainer:
         from .ddp import GradSync
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
-        self.grad_sync.producers = self.programs()
         return self.grad_sync
 
     def programs(self):
@@ -121,8 +120,6 @@ class Trainer:
         state = {"g": torch.cuda.CUDAGraph()}
 
         def cut(buckets):
-            for p in self.programs():       # join the WGRAD branch before closing the segment
-                p.join()
             state["g"].capture_end()
             segs.append((state["g"], list(buckets)))
             state["g"] = torch.cuda.CUDAGraph()
