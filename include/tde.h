@@ -255,6 +255,28 @@ int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_di
  * T may be NULL.  K is [B][9]. */
 int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const float* K, float* T,
                   float* P, float* Kinv, void* stream);
+/* ---- reference-named geometry ops with their backward (the un-fused utils_lr.py path; the host layer
+ * tf_depth_estimation_amd/utils_lr.py wraps them as autograd functions).
+ * pose_vec2mat(vec, format) (utils_lr.py:106-149): vec [B][6] (tx,ty,tz,rx,ry,rz) -> T [B][16];
+ * format 0 'angleaxis' (Rodrigues, :77-103, NaN at r = 0), 1 'eular' (euler2mat, :26-75, angles clipped
+ * to [-pi,pi]), 2 'test' (identity, zero translation). */
+int tde_pose_vec2mat(int B, const float* vec, int format, float* T, void* stream);
+/* dvec (+)= d<dT, T(vec)>/dvec ('eular': zero outside the clip range, as tf.clip_by_value). */
+int tde_pose_vec2mat_bwd(int B, const float* vec, int format, const float* dT, float* dvec, int accumulate,
+                         void* stream);
+/* bilinear_sampler backward (utils_lr.py:276-366) of tde_warp_fwd's given-coords mode:
+ * d_img += scatter of w*d_out (float atomics; zero it first), d_coords [B,H,W,2] = d_out . dout/dcoords
+ * + d_wmask . dwmask/dcoords (d_out / d_wmask may be NULL). */
+int tde_sampler_bwd(int B, int H, int W, int C, const float* coords, const float* img, int Hs, int Ws,
+                    const float* d_out, const float* d_wmask, float* d_img, float* d_coords, void* stream);
+/* backward of (coords, z) = cam2pixel(P, pixel2cam(depth, meshgrid, Kinv)) (utils_lr.py:151-194,
+ * :240-251): d_depth (+)= ..., gP [B][12] += dL/dP (fp64).  Intrinsics are data (no gradient, as at every
+ * reference call site). */
+int tde_cam_coords_bwd(int B, int H, int W, const float* depth, const float* P, const float* Kinv,
+                       const float* d_coords, const float* d_z, float* d_depth, int accumulate, double* gP,
+                       void* stream);
+/* dT [B][16] = d/dT of P = (K4 @ T)[0:3] given gP [B][12] (row 3 of dT = 0). */
+int tde_pose_dp_to_dt(int B, const float* K, const double* gP, float* dT, void* stream);
 /* d loss / d pose_vec from gP [nscales][B][12] (each scale's K_s at K + b*k_stride_b + 9*s) plus an
  * optional direct dL/dT [B][16]; Rodrigues backward. */
 int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, long k_stride_b,

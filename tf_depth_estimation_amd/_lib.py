@@ -62,6 +62,11 @@ _SIGS = {
     "tde_pose_prep": (c_int, [c_int, P, P, P, P, P, P, P]),
     "tde_pose_grad": (c_int, [c_int, c_int, P, P, ctypes.c_long, P, P, P, c_int, P]),
     "tde_cam_loss": (c_int, [c_int, P, P, P, c_float, P, P, P, P]),
+    "tde_pose_vec2mat": (c_int, [c_int, P, c_int, P, P]),
+    "tde_pose_vec2mat_bwd": (c_int, [c_int, P, c_int, P, P, c_int, P]),
+    "tde_sampler_bwd": (c_int, [c_int, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, P, P]),
+    "tde_cam_coords_bwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P]),
+    "tde_pose_dp_to_dt": (c_int, [c_int, P, P, P, P]),
     "tde_abi_version": (c_int, []),
     "tde_status_string": (ctypes.c_char_p, [c_int]),
     "tde_set_conv_math": (c_int, [c_int]),

@@ -387,9 +387,248 @@ __global__ void __launch_bounds__(256) warp_fwd_kernel(int B, int H, int W, int 
   if (zout) zout[pix] = z;
 }
 
+// ------------------------------------------------------------------ reference-named geometry ops
+// (the un-fused utils_lr.py functions, for callers that build their own loss: pose_vec2mat,
+// projective_inverse_warp, bilinear_sampler, optflow_warp, consistent_depth_loss) and their backward.
+
+// euler2mat (utils_lr.py:26-75): R = Rx(x) @ Ry(y) @ Rz(z), angles clipped to [-pi, pi].
+__device__ void euler_R(float z, float y, float x, float R[9]) {
+  const float pi = 3.14159265358979f;
+  z = fminf(fmaxf(z, -pi), pi); y = fminf(fmaxf(y, -pi), pi); x = fminf(fmaxf(x, -pi), pi);
+  const float cz = cosf(z), sz = sinf(z), cy = cosf(y), sy = sinf(y), cx = cosf(x), sx = sinf(x);
+  const float Rz[9] = {cz, -sz, 0.f, sz, cz, 0.f, 0.f, 0.f, 1.f};
+  const float Ry[9] = {cy, 0.f, sy, 0.f, 1.f, 0.f, -sy, 0.f, cy};
+  const float Rx[9] = {1.f, 0.f, 0.f, 0.f, cx, -sx, 0.f, sx, cx};
+  float XY[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) XY[3 * i + j] = Rx[3 * i] * Ry[j] + Rx[3 * i + 1] * Ry[3 + j] + Rx[3 * i + 2] * Ry[6 + j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = XY[3 * i] * Rz[j] + XY[3 * i + 1] * Rz[3 + j] + XY[3 * i + 2] * Rz[6 + j];
+}
+
+// pose_vec2mat (utils_lr.py:106-149): format 0 'angleaxis', 1 'eular', 2 'test' (identity, no translation).
+__global__ void pose_vec2mat_kernel(int B, const float* vec, int format, float* T) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* v = vec + 6 * b;
+  float R[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+  if (format == 0) rodrigues(v + 3, R);
+  else if (format == 1) euler_R(v[5], v[4], v[3], R);
+  float* Tb = T + 16 * b;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) Tb[4 * i + j] = R[3 * i + j];
+    Tb[4 * i + 3] = format == 2 ? 0.f : v[i];
+  }
+  Tb[12] = 0.f; Tb[13] = 0.f; Tb[14] = 0.f; Tb[15] = 1.f;
+}
+
+// Backward of the 'eular' branch: dL/d(rx,ry,rz) = <G, dR/dangle>, zero outside the clip range
+// (tf.clip_by_value passes the gradient on [min, max]); translation gradient = G[:,3].
+__global__ void pose_vec2mat_euler_bwd_kernel(int B, const float* vec, const float* dT, float* dvec, int accumulate) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float pi = 3.14159265358979f;
+  const float* v = vec + 6 * b;
+  const float* G = dT + 16 * b;
+  const float ang[3] = {v[5], v[4], v[3]};   // z, y, x
+  float out[6];
+  for (int i = 0; i < 3; ++i) out[i] = G[4 * i + 3];
+  float cl[3], c[3], s[3];
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = fminf(fmaxf(ang[i], -pi), pi);
+    c[i] = cosf(cl[i]); s[i] = sinf(cl[i]);
+  }
+  // matrices and their derivatives
+  const float Rz[9] = {c[0], -s[0], 0.f, s[0], c[0], 0.f, 0.f, 0.f, 1.f};
+  const float dRz[9] = {-s[0], -c[0], 0.f, c[0], -s[0], 0.f, 0.f, 0.f, 0.f};
+  const float Ry[9] = {c[1], 0.f, s[1], 0.f, 1.f, 0.f, -s[1], 0.f, c[1]};
+  const float dRy[9] = {-s[1], 0.f, c[1], 0.f, 0.f, 0.f, -c[1], 0.f, -s[1]};
+  const float Rx[9] = {1.f, 0.f, 0.f, 0.f, c[2], -s[2], 0.f, s[2], c[2]};
+  const float dRx[9] = {0.f, 0.f, 0.f, 0.f, -s[2], -c[2], 0.f, c[2], -s[2]};
+  const float* A[3][3] = {{Rx, Ry, dRz}, {Rx, dRy, Rz}, {dRx, Ry, Rz}};
+  float g[3];
+  for (int k = 0; k < 3; ++k) {
+    float M1[9], M[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        M1[3 * i + j] = A[k][0][3 * i] * A[k][1][j] + A[k][0][3 * i + 1] * A[k][1][3 + j] + A[k][0][3 * i + 2] * A[k][1][6 + j];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        M[3 * i + j] = M1[3 * i] * A[k][2][j] + M1[3 * i + 1] * A[k][2][3 + j] + M1[3 * i + 2] * A[k][2][6 + j];
+    float acc = 0.f;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) acc += G[4 * i + j] * M[3 * i + j];
+    g[k] = (ang[k] >= -pi && ang[k] <= pi) ? acc : 0.f;
+  }
+  out[3] = g[2]; out[4] = g[1]; out[5] = g[0];   // (rx, ry, rz)
+  for (int i = 0; i < 6; ++i) dvec[6 * b + i] = accumulate ? dvec[6 * b + i] + out[i] : out[i];
+}
+
+// bilinear_sampler backward (utils_lr.py:276-366): out[c] = sum_taps w * img[tap][c], wmask = sum w.
+// d_img[tap] += w * d_out (atomic scatter), d_coords = d_out . d out/d(u,v) + d_wmask * d wmask/d(u,v).
+__global__ void __launch_bounds__(256) sampler_bwd_kernel(int B, int H, int W, int C, const float* coords,
+                                                          const float* img, int Hs, int Ws, const float* d_out,
+                                                          const float* d_wmask, float* d_img, float* d_coords) {
+  const int b = blockIdx.y;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= H * W) return;
+  const long pix = (long)b * H * W + idx;
+  const float u = coords[2 * pix], v = coords[2 * pix + 1];
+  const Tap4 t = taps(u, v, Ws, Hs);
+  const float w00 = t.wx0 * t.wy0, w01 = t.wx0 * t.wy1, w10 = t.wx1 * t.wy0, w11 = t.wx1 * t.wy1;
+  const long base = (long)b * Hs * Ws;
+  const long i00 = (base + (long)t.y0 * Ws + t.x0) * C, i01 = (base + (long)t.y1 * Ws + t.x0) * C;
+  const long i10 = (base + (long)t.y0 * Ws + t.x1) * C, i11 = (base + (long)t.y1 * Ws + t.x1) * C;
+  float gu = 0.f, gv = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float g = d_out ? d_out[pix * C + c] : 0.f;
+    if (g == 0.f) continue;
+    if (d_coords) {
+      const float s00 = img[i00 + c], s01 = img[i01 + c], s10 = img[i10 + c], s11 = img[i11 + c];
+      gu += g * (-t.mx0 * (t.wy0 * s00 + t.wy1 * s01) + t.mx1 * (t.wy0 * s10 + t.wy1 * s11));
+      gv += g * (-t.my0 * (t.wx0 * s00 + t.wx1 * s10) + t.my1 * (t.wx0 * s01 + t.wx1 * s11));
+    }
+    if (d_img) {
+      if (w00 != 0.f) atomicAdd(d_img + i00 + c, w00 * g);
+      if (w01 != 0.f) atomicAdd(d_img + i01 + c, w01 * g);
+      if (w10 != 0.f) atomicAdd(d_img + i10 + c, w10 * g);
+      if (w11 != 0.f) atomicAdd(d_img + i11 + c, w11 * g);
+    }
+  }
+  if (d_coords) {
+    if (d_wmask) {
+      const float gw = d_wmask[pix];
+      gu += gw * (t.mx1 - t.mx0) * (t.wy0 + t.wy1);
+      gv += gw * (t.my1 - t.my0) * (t.wx0 + t.wx1);
+    }
+    d_coords[2 * pix] = gu;
+    d_coords[2 * pix + 1] = gv;
+  }
+}
+
+// Backward of (coords, z) = cam2pixel(P, pixel2cam(depth, meshgrid, Kinv)) (utils_lr.py:151-194):
+// d_depth (+)= ..., gP[b][12] += dL/dP (fp64, block-reduced).  Intrinsics are data (no gradient).
+__global__ void __launch_bounds__(256) cam_coords_bwd_kernel(int B, int H, int W, const float* depth, const float* P,
+                                                             const float* Kinv, const float* d_coords,
+                                                             const float* d_z, float* d_depth, int accumulate,
+                                                             double* gP) {
+  __shared__ double sh[12][4];
+  const int b = blockIdx.y;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  double gp[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) gp[i] = 0.0;
+  if (idx < H * W) {
+    const long pix = (long)b * H * W + idx;
+    const int y = idx / W, x = idx - y * W;
+    const float dep = depth[pix];
+    const float* Ki = Kinv + 9 * b;
+    const float* Pb = P + 12 * b;
+    float cam[3];
+    for (int i = 0; i < 3; ++i) cam[i] = (Ki[3 * i] * x + Ki[3 * i + 1] * y + Ki[3 * i + 2]) * dep;
+    const float p0 = Pb[0] * cam[0] + Pb[1] * cam[1] + Pb[2] * cam[2] + Pb[3];
+    const float p1 = Pb[4] * cam[0] + Pb[5] * cam[1] + Pb[6] * cam[2] + Pb[7];
+    const float den = Pb[8] * cam[0] + Pb[9] * cam[1] + Pb[10] * cam[2] + Pb[11] + 1e-10f;
+    const float gu = d_coords ? d_coords[2 * pix] : 0.f, gv = d_coords ? d_coords[2 * pix + 1] : 0.f;
+    const float gp0 = gu / den, gp1 = gv / den;
+    const float gp2 = -(gu * p0 + gv * p1) / (den * den) + (d_z ? d_z[pix] : 0.f);
+    const float gcam0 = Pb[0] * gp0 + Pb[4] * gp1 + Pb[8] * gp2;
+    const float gcam1 = Pb[1] * gp0 + Pb[5] * gp1 + Pb[9] * gp2;
+    const float gcam2 = Pb[2] * gp0 + Pb[6] * gp1 + Pb[10] * gp2;
+    const float gps[3] = {gp0, gp1, gp2};
+    for (int i = 0; i < 3; ++i) {
+      gp[4 * i + 0] = gps[i] * cam[0];
+      gp[4 * i + 1] = gps[i] * cam[1];
+      gp[4 * i + 2] = gps[i] * cam[2];
+      gp[4 * i + 3] = gps[i];
+    }
+    if (d_depth) {
+      // cam = dep * (Kinv [x y 1]) -> d dep = gcam . (Kinv [x y 1])
+      float gd = 0.f;
+      const float gc[3] = {gcam0, gcam1, gcam2};
+      for (int i = 0; i < 3; ++i) gd += gc[i] * (Ki[3 * i] * x + Ki[3 * i + 1] * y + Ki[3 * i + 2]);
+      d_depth[pix] = accumulate ? d_depth[pix] + gd : gd;
+    }
+  }
+  if (!gP) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int i = 0; i < 12; ++i) {
+    double vv = gp[i];
+    for (int off = 32; off > 0; off >>= 1) vv += __shfl_down(vv, off, 64);
+    if (lane == 0) sh[i][wid] = vv;
+  }
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    const int i = threadIdx.x;
+    atomicAdd(gP + 12 * b + i, sh[i][0] + sh[i][1] + sh[i][2] + sh[i][3]);
+  }
+}
+
+// dL/dT rows 0..2 from dL/dP with P = K @ T[0:3] (dT = K^T dP), row 3 zero; then to dvec via
+// the pose backward of the chosen format (or left as dT for format 'matrix' == 3).
+__global__ void dP_to_dT_kernel(int B, const float* K, const double* gP, float* dT) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* Kb = K + 9 * b;
+  const double* g = gP + 12 * b;
+  for (int k = 0; k < 3; ++k)
+    for (int j = 0; j < 4; ++j)
+      dT[16 * b + 4 * k + j] = (float)(Kb[k] * g[j] + Kb[3 + k] * g[4 + j] + Kb[6 + k] * g[8 + j]);
+  for (int j = 0; j < 4; ++j) dT[16 * b + 12 + j] = 0.f;
+}
+
 }  // namespace
 
 extern "C" {
+
+int tde_pose_vec2mat(int B, const float* vec, int format, float* T, void* stream) {
+  TDE_CHECK_ARG(B > 0 && vec && T && format >= 0 && format <= 2);
+  hipLaunchKernelGGL(pose_vec2mat_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B, vec,
+                     format, T);
+  return tde_launch_status();
+}
+
+int tde_pose_vec2mat_bwd(int B, const float* vec, int format, const float* dT, float* dvec, int accumulate,
+                         void* stream) {
+  TDE_CHECK_ARG(B > 0 && vec && dT && dvec && format >= 0 && format <= 2);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (format == 0)
+    hipLaunchKernelGGL(pose_grad_kernel, dim3((B + 63) / 64), dim3(64), 0, st, B, 0, vec, (const float*)nullptr, 0L,
+                       (const double*)nullptr, dT, dvec, accumulate);
+  else if (format == 1)
+    hipLaunchKernelGGL(pose_vec2mat_euler_bwd_kernel, dim3((B + 63) / 64), dim3(64), 0, st, B, vec, dT, dvec,
+                       accumulate);
+  else if (!accumulate)
+    return tde_zero_bytes(sizeof(float) * 6 * (size_t)B, dvec, stream);   // 'test': constant
+  return tde_launch_status();
+}
+
+int tde_sampler_bwd(int B, int H, int W, int C, const float* coords, const float* img, int Hs, int Ws,
+                    const float* d_out, const float* d_wmask, float* d_img, float* d_coords, void* stream) {
+  TDE_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0 && Hs > 0 && Ws > 0 && coords && img);
+  TDE_CHECK_ARG(!d_img || d_out);
+  dim3 grid((H * W + 255) / 256, B);
+  hipLaunchKernelGGL(sampler_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream), B, H, W, C, coords,
+                     img, Hs, Ws, d_out, d_wmask, d_img, d_coords);
+  return tde_launch_status();
+}
+
+int tde_cam_coords_bwd(int B, int H, int W, const float* depth, const float* P, const float* Kinv,
+                       const float* d_coords, const float* d_z, float* d_depth, int accumulate, double* gP,
+                       void* stream) {
+  TDE_CHECK_ARG(B > 0 && H > 0 && W > 0 && depth && P && Kinv && (d_coords || d_z));
+  dim3 grid((H * W + 255) / 256, B);
+  hipLaunchKernelGGL(cam_coords_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream), B, H, W, depth, P,
+                     Kinv, d_coords, d_z, d_depth, accumulate, gP);
+  return tde_launch_status();
+}
+
+int tde_pose_dp_to_dt(int B, const float* K, const double* gP, float* dT, void* stream) {
+  TDE_CHECK_ARG(B > 0 && K && gP && dT);
+  hipLaunchKernelGGL(dP_to_dT_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B, K, gP,
+                     dT);
+  return tde_launch_status();
+}
 
 int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_disp, const float* P, const float* Kinv,
                  const float* coords_in, const float* img, int Hs, int Ws, float* out, float* coords, float* flow_x,

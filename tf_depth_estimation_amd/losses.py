@@ -84,3 +84,34 @@ def pose_prep(K, T=None, P=None, Kinv=None, vec=None, mat=None):
 
 def new(shape, dtype=torch.float32):
     return torch.empty(shape, device="cuda", dtype=dtype)
+
+
+class _SmoothLoss(torch.autograd.Function):
+    """compute_smooth_loss as a differentiable op: one tde_loss_smooth2 pass per channel yields the value
+    and the gradient together; backward scales the stored gradient by the upstream scalar."""
+
+    @staticmethod
+    def forward(ctx, pred):
+        if pred.dtype != torch.float32 or not pred.is_cuda:
+            raise TypeError("compute_smooth_loss takes a float32 CUDA tensor")
+        pred = pred.contiguous()
+        N, H, W, C = pred.shape
+        acc = torch.zeros(1, device=pred.device, dtype=torch.float64)
+        g = torch.zeros_like(pred)
+        for c in range(C):      # mean over all channels = (1/C) sum of per-channel means
+            smooth(pred, g, 1.0 / C, acc, 0, coff=c)
+        ctx.save_for_backward(g)
+        return acc[0].float()
+
+    @staticmethod
+    def backward(ctx, dl):
+        (g,) = ctx.saved_tensors
+        return g * dl
+
+
+def compute_smooth_loss(pred):
+    """train_depth_then_cam_lr.py:59-68 (== train_depth_only.py:45-54, my_losses.py:27-36): second-order
+    differences mean|dx2| + mean|dxdy| + mean|dydx| + mean|dy2| of an NHWC map (not edge-aware)."""
+    if pred.dim() != 4 or pred.shape[1] < 3 or pred.shape[2] < 3:
+        raise ValueError(f"compute_smooth_loss needs [N,H>=3,W>=3,C], got {tuple(pred.shape)}")
+    return _SmoothLoss.apply(pred)
