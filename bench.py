@@ -188,8 +188,9 @@ def main():
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--math", default="fp32", choices=["fp32", "bf16x3"],
-                    help="conv arithmetic: exact fp32 MFMA, or bf16x3 split precision (include/tde.h)")
+    ap.add_argument("--math", default="fp32", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r"],
+                    help="conv arithmetic (include/tde.h tde_set_conv_math): exact fp32 MFMA, bf16x3 split "
+                         "precision, or the fp32-accurate 3-way bf16 split (LDS-staged / register-split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
     ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
@@ -209,7 +210,7 @@ def main():
     H, W, Nd, gflop_unit, desc = WORKLOADS[args.workload]
     N = args.batch or Nd
     from tf_depth_estimation_amd import _lib
-    _lib.check(_lib.load().tde_set_conv_math(1 if args.math == "bf16x3" else 0), "conv math")
+    _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[args.math]), "conv math")
     tr = make_trainer(args.workload, N)
     tr.set_batch(*[t.cuda() for t in make_batch(args.workload, N, seed=1000 + rank)])
     if world > 1:
@@ -258,9 +259,11 @@ def main():
     loss = tr.total_loss()
 
     if rank == 0:
-        if args.math == "bf16x3":
-            # 3 bf16 MFMAs per fp32 product: priced against the dense bf16 MFMA peak, FLOPs counted once
-            kernel_name, peak = "igemmx_kernel<1,...> (conv fwd+dgrad+wgrad, bf16x3 on MFMA 16x16x32 bf16)", BF16_MFMA_PEAK
+        if args.math != "fp32":
+            # 3 or 6 bf16 MFMAs per fp32 product: priced against the dense bf16 MFMA peak, FLOPs counted once
+            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> (conv fwd+dgrad+wgrad, {args.math} on "
+                           "MFMA 16x16x32 bf16)")
+            peak = BF16_MFMA_PEAK
         else:
             kernel_name, peak = "igemmx_kernel<0,...> (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
         value = world * N * args.steps / el

@@ -79,10 +79,11 @@ def main():
     ap.add_argument("--accumulate", type=int, default=0)
     a = ap.parse_args()
     lib = _lib.load()
-    modes = {"fp32": [0], "bf16x3": [1], "both": [0, 1]}[a.math]
+    modes = [_lib.CONV_MATH[m] for m in _lib.CONV_MATH] if a.math in ("both", "all") else \
+        [_lib.CONV_MATH[m] for m in a.math.split(",")]
     for m in modes:
         _lib.check(lib.tde_set_conv_math(m))
-        print(f"== math {'fp32' if m == 0 else 'bf16x3'}")
+        print(f"== math {[k for k, v in _lib.CONV_MATH.items() if v == m][0]}")
         for sh in SHAPES:
             if a.shapes and sh[0] not in a.shapes.split(","):
                 continue

@@ -22,7 +22,10 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--loss-vs", type=float, default=0.0,
                     help="also rank conv entries by ms lost against this TFLOP/s reference")
+    ap.add_argument("--math", default="fp32")
     a = ap.parse_args()
+    from tf_depth_estimation_amd import _lib
+    _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[a.math]), "conv math")
     N = a.batch or bench.WORKLOADS[a.workload][2]
     tr = bench.make_trainer(a.workload, N)
     tr.set_batch(*[t.cuda() for t in bench.make_batch(a.workload, N, 0)])

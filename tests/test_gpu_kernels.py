@@ -90,13 +90,14 @@ CONV_CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1], ids=["fp32", "bf16x3"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["fp32", "bf16x3", "bf16x6", "bf16x6r"])
 def conv_tol(request, L):
-    """Conv arithmetic mode (include/tde.h tde_set_conv_math) -> tolerance: exact fp32 MFMA 1e-5;
-    bf16x3 (~2^-16 per product, fp32 accumulation) 1e-4 relative-to-max."""
+    """Conv arithmetic mode (include/tde.h tde_set_conv_math) -> tolerance: exact fp32 MFMA and the
+    exact-split bf16x6 modes (dropped terms < 2^-21 per product) 1e-5; bf16x3 (~2^-16 per product,
+    fp32 accumulation) 1e-4 relative-to-max."""
     lib = L.load()
     L.check(lib.tde_set_conv_math(request.param))
-    yield TOL if request.param == 0 else 1e-4
+    yield 1e-4 if request.param == 1 else TOL
     L.check(lib.tde_set_conv_math(0))
 
 

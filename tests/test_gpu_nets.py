@@ -29,7 +29,9 @@ GRAD_TOL = 1e-3
 # which compounds to a few 1e-4 over 20+ conv layers: it does NOT meet the 1e-4 north-star bar and is
 # held to 1e-3 on outputs and 16x (not 4x) the cpu-fp32 gradient noise.  fp32 (default) meets 1e-4.
 OUT_TOL_BF16X3 = 1e-3
-GRAD_FACTOR = {0: 4, 1: 16}
+# bf16x6 (modes 2/3: exact three-way bf16 split, six MFMAs per product, < 2^-21 per product) is held to
+# the fp32 bars.
+GRAD_FACTOR = {0: 4, 1: 16, 2: 4, 3: 4}
 
 
 def rel_err(gpu, ref):
@@ -86,7 +88,7 @@ def fresh_store():
     yield
 
 
-@pytest.fixture(params=[0, 1], ids=["fp32", "bf16x3"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["fp32", "bf16x3", "bf16x6", "bf16x6r"])
 def conv_math(request):
     from tf_depth_estimation_amd import _lib
     lib = _lib.load()
@@ -108,7 +110,7 @@ def test_disp_net_forward_parity(N, H, W, conv_math):
     for st in P.bn.values():
         st.moving_mean.zero_(); st.moving_variance.fill_(1.0)
     ref = ON.disp_net(P, x.double(), True, scope="model/depth_net")
-    tol = OUT_TOL if conv_math == 0 else OUT_TOL_BF16X3
+    tol = OUT_TOL_BF16X3 if conv_math == 1 else OUT_TOL
     for i, (o, r) in enumerate(zip(outs, ref)):
         e = rel_err(o, r)
         assert e <= tol, f"disp{i + 1}: rel err {e:.2e}"
@@ -237,7 +239,7 @@ def test_config2_train_step_parity(conv_math):
         lr.backward()
         grads[dt] = {k: v.grad for k, v in P.vars.items()}
         if dt == torch.float64:
-            assert abs(tr.total_loss() - lr.item()) <= (1e-5 if conv_math == 0 else 1e-4) * abs(lr.item())
+            assert abs(tr.total_loss() - lr.item()) <= (1e-4 if conv_math == 1 else 1e-5) * abs(lr.item())
     check_grads_global({k: tr.chunk.grad_view(k) for k in p0}, grads[torch.float64], grads[torch.float32],
                        GRAD_FACTOR[conv_math])
     # Adam: TF's first step is ~lr*sign(g), sign-sensitive where g ~ 0, so the update is checked

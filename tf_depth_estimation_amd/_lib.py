@@ -13,6 +13,9 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
 ABI_VERSION = 2
+# tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
+# fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
+CONV_MATH = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "bf16x6r": 3}
 
 c_int, c_float, c_size_t, c_void_p, c_double_p = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p,
                                                   ctypes.POINTER(ctypes.c_double))

@@ -146,12 +146,70 @@ struct Img1 {
   }
 };
 
+// ------------------------------------------------------------------ bf16x6: fp32-accurate split MFMA
+// x = hi + mid + lo EXACTLY for normal fp32 x: hi = x with the low 16 mantissa bits cleared (8
+// significant bits), r = x - hi (exact, <= 16 significant bits), mid = r truncated the same way,
+// lo = r - mid (exact, <= 8 significant bits, so representable in bf16).  The product keeps the six
+// terms of order <= 2^-14 (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid) on v_mfma_f32_16x16x32_bf16
+// with fp32 accumulation; the dropped mid*lo + lo*mid + lo*lo are < 2^-21 of |x*y| (worst case; fp32
+// rounding itself is 2^-24 per operation), at 16/6 = 2.7x the fp32-MFMA rate.
+//   MATH 2: split once per element at LDS staging, three bf16 planes in LDS;
+//   MATH 3: fp32 LDS image (as MATH 0), split per fragment in registers after the LDS read.
+__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
+  const unsigned u = __float_as_uint(x);
+  h = u & 0xFFFF0000u;
+  const float r = x - __uint_as_float(h);
+  m = __float_as_uint(r) & 0xFFFF0000u;
+  l = __float_as_uint(r - __uint_as_float(m));
+}
+__device__ __forceinline__ unsigned pack_hi16(unsigned a, unsigned b) { return (a >> 16) | (b & 0xFFFF0000u); }
+
+__device__ __forceinline__ void split4x3(f4 v, uint2& hi, uint2& mi, uint2& lo) {
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split3(v[j], h[j], m[j], l[j]);
+  hi = make_uint2(pack_hi16(h[0], h[1]), pack_hi16(h[2], h[3]));
+  mi = make_uint2(pack_hi16(m[0], m[1]), pack_hi16(m[2], m[3]));
+  lo = make_uint2(pack_hi16(l[0], l[1]), pack_hi16(l[2], l[3]));
+}
+
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// 8 consecutive-k fp32 values (two f4) -> hi / mid / lo bf16x8 fragments
+__device__ __forceinline__ void split8x3(f4 a, f4 b, bf8& hi, bf8& mi, bf8& lo) {
+  uint2 h0, m0, l0, h1, m1, l1;
+  split4x3(a, h0, m0, l0);
+  split4x3(b, h1, m1, l1);
+  hi = __builtin_bit_cast(bf8, u4v{h0.x, h0.y, h1.x, h1.y});
+  mi = __builtin_bit_cast(bf8, u4v{m0.x, m0.y, m1.x, m1.y});
+  lo = __builtin_bit_cast(bf8, u4v{l0.x, l0.y, l1.x, l1.y});
+}
+
+template <int ROWS>
+struct Img6 {
+  static constexpr int PLANE = ROWS * LDR;
+  static constexpr int SIZE = 3 * PLANE;       // hi + mid + lo
+  __device__ static __forceinline__ void put(u16* s, int row, int k, f4 v) {
+    uint2 hi, mi, lo;
+    split4x3(v, hi, mi, lo);
+    *reinterpret_cast<uint2*>(s + row * LDR + k) = hi;
+    *reinterpret_cast<uint2*>(s + PLANE + row * LDR + k) = mi;
+    *reinterpret_cast<uint2*>(s + 2 * PLANE + row * LDR + k) = lo;
+  }
+  __device__ static __forceinline__ bf8 plane(const u16* s, int pl, int row, int q) {
+    return *reinterpret_cast<const bf8*>(s + pl * PLANE + row * LDR + 8 * q);
+  }
+};
+
 template <int MATH, int ROWS>
 struct ImgSel;
 template <int ROWS>
 struct ImgSel<0, ROWS> { using type = Img1<ROWS>; using T = float; };
 template <int ROWS>
 struct ImgSel<1, ROWS> { using type = Img3<ROWS>; using T = u16; };
+template <int ROWS>
+struct ImgSel<2, ROWS> { using type = Img6<ROWS>; using T = u16; };
+template <int ROWS>
+struct ImgSel<3, ROWS> { using type = Img1<ROWS>; using T = float; };
 
 // MATH 0: exact fp32 (2 x 4 v_mfma_f32_16x16x4_f32 per 32-deep k-tile); MATH 1: bf16x3.
 template <int MATH, int BM, int BN>
@@ -384,6 +442,52 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
+    } else if constexpr (MATH == 2 || MATH == 3) {
+      bf8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+      if constexpr (MATH == 2) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          ah[a] = IA::plane(A, 0, wrow0 + a * 16 + r16, q);
+          am[a] = IA::plane(A, 1, wrow0 + a * 16 + r16, q);
+          al[a] = IA::plane(A, 2, wrow0 + a * 16 + r16, q);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          bh[b] = IB::plane(Bm, 0, wcol0 + b * 16 + r16, q);
+          bm[b] = IB::plane(Bm, 1, wcol0 + b * 16 + r16, q);
+          bl[b] = IB::plane(Bm, 2, wcol0 + b * 16 + r16, q);
+        }
+        issue();
+      } else {
+        f4 fa[TM][2], fb[TN][2];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          fa[a][0] = IA::frag(A, wrow0 + a * 16 + r16, 8 * q);
+          fa[a][1] = IA::frag(A, wrow0 + a * 16 + r16, 8 * q + 4);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          fb[b][0] = IB::frag(Bm, wcol0 + b * 16 + r16, 8 * q);
+          fb[b][1] = IB::frag(Bm, wcol0 + b * 16 + r16, 8 * q + 4);
+        }
+        issue();
+#pragma unroll
+        for (int a = 0; a < TM; ++a) split8x3(fa[a][0], fa[a][1], ah[a], am[a], al[a]);
+#pragma unroll
+        for (int b = 0; b < TN; ++b) split8x3(fb[b][0], fb[b][1], bh[b], bm[b], bl[b]);
+      }
+      // smallest terms first
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
     } else {
       // lane (r16, q) holds k = 16*kc + 4*q + j of MFMA (kc, j): same permutation for A and B
       f4 fa[2][TM], fb[2][TN];
@@ -556,10 +660,9 @@ __global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
 // data gradient (MODE1: DGRAD of a conv, FWD of a deconv's virtual conv), blocks [nd, nd + nw) the
 // filter gradient (WGRAD).  Both
 // only read dz, so they are independent; at the deep levels neither fills the chip alone.
-template <int MODE1, int BM, int BN, int WM, int WN>
+template <int MATH, int MODE1, int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(NT) igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
                                                         int gxw, int gyw, int nd) {
-  constexpr int MATH = 0;
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
   int id = blockIdx.x;
   if (id < nd) {
@@ -828,7 +931,7 @@ static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, lon
   }
 }
 
-static int g_conv_math = 0;   // 0: exact fp32 MFMA, 1: bf16x3 (process-wide, see tde_set_conv_math)
+static int g_conv_math = 0;   // 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6 (process-wide, see tde_set_conv_math)
 
 // Split-K policy (environment overrides are for tuning experiments; read once at load time).
 static long env_long(const char* name, long dflt) {
@@ -852,9 +955,10 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
   gemm_dims(d, mode, M, Nn, Kd, ncls);
   Plan pl{};
   if ((mode == MODE_FWD || (mode == MODE_DGRAD && d.stride == 1)) && M <= g_skinny_m && M <= 96 && !fix_bm &&
-      g_conv_math == 0) {
-    // skinny path: 64-column tiles, 4 waves x KG x 16 of k per block; the largest KG (fewest splits)
-    // that still gives >= 256 blocks, TM x KG <= 8 register fragments
+      g_conv_math != 1) {
+    // skinny path (fp32 MFMA in every exact math mode: a weight stream, not MFMA-bound): 64-column
+    // tiles, 4 waves x KG x 16 of k per block; the largest KG (fewest splits) that still gives >= 256
+    // blocks, TM x KG <= 8 register fragments
     pl.skinny_tm = (int)((M + 15) / 16);
     pl.gx = tde_cdiv(Nn, 64);
     pl.skinny_kg = 1;
@@ -970,13 +1074,27 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
 // prefetch depth (tiles in flight) of the fp32 kernels: 1 for 128-row tiles, 2 for the 64-row tiles of
 // the deep layers (TDE_CONV_PF: 1 / 2 forces one depth for all, tuning experiments)
 static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
+// wave layout of a tile: 2 x 2 waves when BN is a multiple of TDE_WN_DIV, else 4 x 1 (all rows split)
+#ifndef TDE_WN_DIV
+#define TDE_WN_DIV 32
+#endif
+
+// bf16x6 register split (math 3) costs ~44 VALU instructions per 8-element fragment per wave: it pays
+// only where a wave's fragments feed enough MFMAs (measured: 128x128 1.45x faster than fp32, 128x32
+// 10% slower), so narrower tiles run exact fp32 MFMA in that mode.
+static const long g_math3_min_bn = env_long("TDE_MATH3_MIN_BN", 64);
+static int tile_math(int bn) { return (g_conv_math == 3 && bn < g_math3_min_bn) ? 0 : g_conv_math; }
 
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
-  constexpr int WN = BN % 32 == 0 ? 2 : 1;
+  constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? 2 : 1);
-  if (g_conv_math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  const int math = tile_math(BN);
+  if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  else if (math == 3 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
+  else if (math == 3) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (pf == 2) hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
 }
@@ -1115,11 +1233,19 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
 
 template <int MODE1, int BM, int BN>
 static void launch_bwd2_cfg(const Plan& p1, const ConvArgs& a1, const Plan& p2, const ConvArgs& a2, hipStream_t st) {
-  constexpr int WN = BN % 32 == 0 ? 2 : 1;
+  constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int nd = p1.gx * p1.gy * p1.gz, nw = p2.gx * p2.gy * p2.gz;
-  hipLaunchKernelGGL((igemm_bwd2_kernel<MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx, p1.gy,
-                     p2.gx, p2.gy, nd);
+  const int math = tile_math(BN);
+  if (math == 2)
+    hipLaunchKernelGGL((igemm_bwd2_kernel<2, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
+                       p1.gy, p2.gx, p2.gy, nd);
+  else if (math == 3)
+    hipLaunchKernelGGL((igemm_bwd2_kernel<3, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
+                       p1.gy, p2.gx, p2.gy, nd);
+  else
+    hipLaunchKernelGGL((igemm_bwd2_kernel<0, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
+                       p1.gy, p2.gx, p2.gy, nd);
 }
 
 template <int MODE1>
@@ -1146,7 +1272,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   const Plan p1 = make_plan(*d, MODE1);
-  const bool fuse = g_bwd_fuse != 0 && g_conv_math == 0 && p1.skinny_tm == 0;
+  const bool fuse = g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0;
   const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : make_plan(*d, MODE_WGRAD);
   if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
@@ -1187,7 +1313,7 @@ static bool bn_ok(const tde_bn_train_t* bn, int C) {
 extern "C" {
 
 int tde_set_conv_math(int mode) {
-  if (mode != 0 && mode != 1) return TDE_ERR_ARG;
+  if (mode < 0 || mode > 3) return TDE_ERR_ARG;
   g_conv_math = mode;
   return TDE_OK;
 }
