@@ -130,6 +130,59 @@ def make_batch(name, N, seed):
     return (x1, x2, gt, intrinsics(N, H, W), T)
 
 
+# ---------------------------------------------------------------- depth L1 vs the reference (CPU leg)
+def depth_l1_vs_ref(name, N, seed=7):
+    """The metric's second half ("depth L1 vs ref"): the workload's network forward on the
+    GPU (public API, fresh Glorot variables, training-mode BN, the benched conv math) against the float64
+    oracle restatement of the same graph on identical inputs and weights.  Per output: mean |gpu - ref|
+    and max|gpu - ref| / max|ref| (north-star bar 1e-4).  Runs in the CPU-baseline leg (rank 0, N = 1)."""
+    from oracle import nets as ON
+    from tf_depth_estimation_amd import _api, variables
+    from tf_depth_estimation_amd import nets_depth, nets_optflow_depth, nets_optflow_depth_pairtest
+    H, W = WORKLOADS[name][:2]
+    rng = np.random.default_rng(seed)
+
+    def oracle_params(chunk):
+        P = ON.Params(dtype=torch.float64)
+        for v in chunk.names():
+            P.vars[v] = chunk.view(v).detach().double().cpu().clone()
+        return P
+
+    def img(C):
+        return torch.tensor(rng.uniform(-0.5, 0.5, (N, H, W, C)), dtype=torch.float32)
+
+    pairs = []   # (label, gpu outputs, oracle outputs)
+    with torch.no_grad(), variables.variable_scope("bench_ref_check"):
+        if name == "config3":
+            x = img(6)
+            outs, ep = nets_depth.disp_net(x.cuda(), is_training=True)
+            ref = ON.disp_net_depthflow(oracle_params(ep["program"].chunk), x.double(), True,
+                                        scope="bench_ref_check/depth_net")
+            pairs += [(f"{'disp' if i < 4 else 'flow'}{i % 4 + 1}", o, r) for i, (o, r) in enumerate(zip(outs, ref))]
+        else:
+            x = img(3)
+            outs, ep = nets_optflow_depth.disp_net(x.cuda(), is_training=True)
+            ref = ON.disp_net(oracle_params(ep["program"].chunk), x.double(), True, scope="bench_ref_check/depth_net")
+            pairs += [(f"disp{i + 1}", o, r) for i, (o, r) in enumerate(zip(outs, ref))]
+            if name == "config4":
+                x6 = img(6)
+                d, pose, m, ep = nets_optflow_depth_pairtest.depth_net(x6.cuda(), is_training=True)
+                rd, rp, rm = ON.depth_net(oracle_params(ep["program"].chunk), x6.double(), True,
+                                          scope="bench_ref_check/depth_cam_net", levels=4)
+                pairs += [(f"pair_disp{i + 1}", o, r) for i, (o, r) in enumerate(zip(d, rd))]
+                pairs += [("pose", pose, rp)]
+    _api.clear_programs()
+    res = {}
+    for lab, o, r in pairs:
+        g = o.detach().double().cpu()
+        r = r.detach().double()
+        res[lab] = {"mean_abs": float((g - r).abs().mean()), "max_rel": float((g - r).abs().max() / r.abs().max())}
+    worst = max(v["max_rel"] for v in res.values())
+    return {"outputs": res, "worst_max_rel": worst, "tol": 1e-4, "pass": worst <= 1e-4,
+            "sample": f"{N} x {W}x{H} synthetic input(s), fresh Glorot weights, training-mode BN, "
+                      "float64 oracle restatement (oracle/nets.py)"}
+
+
 # ---------------------------------------------------------------- CPU baseline (oracle restatement)
 def cpu_baseline(name, N, budget_s=12.0):
     from oracle import losses as OL
@@ -188,7 +241,7 @@ def main():
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--math", default="fp32", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r"],
+    ap.add_argument("--math", default="bf16x6r", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r"],
                     help="conv arithmetic (include/tde.h tde_set_conv_math): exact fp32 MFMA, bf16x3 split "
                          "precision, or the fp32-accurate 3-way bf16 split (LDS-staged / register-split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -260,12 +313,17 @@ def main():
 
     if rank == 0:
         if args.math != "fp32":
-            # 3 or 6 bf16 MFMAs per fp32 product: priced against the dense bf16 MFMA peak, FLOPs counted once
-            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> (conv fwd+dgrad+wgrad, {args.math} on "
-                           "MFMA 16x16x32 bf16)")
-            peak = BF16_MFMA_PEAK
+            # 3 or 6 bf16 MFMAs per fp32 product: the algorithmic fp32 FLOPs are counted once and priced
+            # against the dense bf16 MFMA peak divided by the MFMAs per product (the rate at which this
+            # arithmetic can retire fp32 products), so frac = fraction of the bf16 MFMA pipe doing useful work
+            per = 3 if args.math == "bf16x3" else 6
+            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> (conv fwd+dgrad+wgrad, {args.math}: "
+                           f"{per} x v_mfma_f32_16x16x32_bf16 per fp32 product)")
+            peak = round(BF16_MFMA_PEAK / per, 1)
+            peak_note = f"dense bf16 MFMA peak {BF16_MFMA_PEAK} TFLOP/s / {per} MFMAs per fp32 product"
         else:
             kernel_name, peak = "igemmx_kernel<0,...> (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
+            peak_note = "dense fp32 MFMA peak"
         value = world * N * args.steps / el
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         out = {
@@ -287,7 +345,7 @@ def main():
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "frac": round(achieved / peak, 4), "peak_note": peak_note, "traffic": None,
                          "flops_per_step": conv_flops, "conv_ms_per_step": round(conv_ms, 4),
                          "launches_per_step": conv_launches,
                          "survey_flops_per_step": gflop_unit * 1e9 * N},
@@ -306,6 +364,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] timing CPU baseline ...")
             out["cpu_baseline"] = cpu_baseline(args.workload, N)
+            log("[bench] depth L1 vs the float64 reference restatement ...")
+            out["depth_l1_vs_ref"] = depth_l1_vs_ref(args.workload, N)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

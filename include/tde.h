@@ -62,9 +62,15 @@ const char* tde_status_string(int status);
  * -> TF Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter.
  * Requires C, K, cstrides and coffs to be multiples of 4 (16-byte vectors). */
 /* Process-wide conv arithmetic (set before graph capture; not per-stream):
- *   0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32; bit-for-bit an fp32 fma chain), default;
+ *   0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32; bit-for-bit an fp32 fma chain);
  *   1 = bf16x3: each fp32 operand split into bf16 hi + lo, products hi*hi + hi*lo + lo*hi on
- *       v_mfma_f32_16x16x32_bf16 with fp32 accumulation (~2^-16 relative per product, 5.3x rate). */
+ *       v_mfma_f32_16x16x32_bf16 with fp32 accumulation (~2^-16 relative per product, 5.3x rate);
+ *       does NOT meet the 1e-4 output bar (opt-in only);
+ *   2 = bf16x6: exact three-way bf16 split x = hi + mid + lo of both operands, the six product terms
+ *       of order <= 2^-14 on v_mfma_f32_16x16x32_bf16, fp32 accumulation (dropped terms < 2^-21 of
+ *       |x*y|), split once at LDS staging;
+ *   3 = bf16x6 split per fragment in registers (fp32 LDS image); tiles narrower than 64 columns run
+ *       mode 0.  DEFAULT: held to the same parity bars as mode 0 and the fastest. */
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);

@@ -2,6 +2,7 @@
 # HBM traffic of one bench workload from two rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE), eager
 # mode (the same kernels as the captured graph, one dispatch each), then the per-family summary.
 #   bash scripts/pmc.sh TAG [WORKLOAD] [fp32|bf16x3] [BATCH] [extra bench args]
+# MATH: fp32|bf16x3|bf16x6|bf16x6r (bench.py --math)
 # -> gpurun_out/pmc_<WORKLOAD>_<MATH>_b<BATCH>.json (copy to profiles/ for bench.py's roofline.traffic)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -9,7 +10,7 @@ mkdir -p gpurun_out profiles
 export TMPDIR=/tmp
 TAG=${1:-r01}
 WL=${2:-config2}
-MATH=${3:-fp32}
+MATH=${3:-bf16x6r}
 B=${4:-$(python3 -c "import sys; sys.path.insert(0, '.'); import bench; print(bench.WORKLOADS['$WL'][2])")}
 shift $(( $# < 4 ? $# : 4 ))
 STEPS=6; WARM=2

@@ -96,9 +96,10 @@ def conv_tol(request, L):
     exact-split bf16x6 modes (dropped terms < 2^-21 per product) 1e-5; bf16x3 (~2^-16 per product,
     fp32 accumulation) 1e-4 relative-to-max."""
     lib = L.load()
+    prev = lib.tde_get_conv_math()
     L.check(lib.tde_set_conv_math(request.param))
     yield 1e-4 if request.param == 1 else TOL
-    L.check(lib.tde_set_conv_math(0))
+    L.check(lib.tde_set_conv_math(prev))
 
 
 @pytest.mark.parametrize("case", CONV_CASES)

@@ -9,7 +9,7 @@ from oracle import geometry as OG
 from oracle import losses as OL
 from oracle import nets as ON
 
-from test_gpu_nets import check_grads, check_grads_global, oracle_params_from
+from test_gpu_nets import GRAD_FACTOR, check_grads, check_grads_global, oracle_params_from
 
 pytestmark = pytest.mark.gpu
 
@@ -63,8 +63,18 @@ C4_TERMS = {
 }
 
 
+@pytest.fixture(params=[0, 3], ids=["fp32", "bf16x6r"])
+def step_math(request):
+    from tf_depth_estimation_amd import _lib
+    lib = _lib.load()
+    prev = lib.tde_get_conv_math()
+    _lib.check(lib.tde_set_conv_math(request.param))
+    yield request.param
+    _lib.check(lib.tde_set_conv_math(prev))
+
+
 @pytest.mark.parametrize("term", list(C4_TERMS))
-def test_config4_depth_then_cam_step(term):
+def test_config4_depth_then_cam_step(term, step_math):
     from tf_depth_estimation_amd import train
     B, H, W = 2, 64, 96
     w = C4_TERMS[term] or dict(OL.W_CONFIG4)
@@ -109,7 +119,7 @@ def test_config4_depth_then_cam_step(term):
     # 1/disp smoothness of near-flat random-init disparities is sign-noise in fp32 (see module doc of
     # test_gpu_nets); the per-kernel gradient checks are in test_warp_loss_kernel_gradients, here the
     # whole gradient vector is compared.
-    check_grads_global(gpu, grads[torch.float64], grads[torch.float32])
+    check_grads_global(gpu, grads[torch.float64], grads[torch.float32], GRAD_FACTOR[step_math])
 
 
 def test_config3_optflow_combine_step():

@@ -153,6 +153,10 @@ struct Img1 {
 // terms of order <= 2^-14 (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid) on v_mfma_f32_16x16x32_bf16
 // with fp32 accumulation; the dropped mid*lo + lo*mid + lo*lo are < 2^-21 of |x*y| (worst case; fp32
 // rounding itself is 2^-24 per operation), at 16/6 = 2.7x the fp32-MFMA rate.
+// Measured per conv against float64 (tests/diag_conv_err.py): rms error 2.9e-7 of rms(ref) (fp32 MFMA:
+// 3.5e-7) with a small negative bias (-4e-8 of rms; fp32 MFMA: ~1e-10).  The bias is the bf16 MFMA's
+// accumulation, not the split: a round-to-nearest split (+1 VALU op per level) left it unchanged and cost
+// 2% of the step, so the split truncates.
 //   MATH 2: split once per element at LDS staging, three bf16 planes in LDS;
 //   MATH 3: fp32 LDS image (as MATH 0), split per fragment in registers after the LDS read.
 __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
@@ -931,13 +935,14 @@ static void gemm_dims(const tde_conv_desc_t& d, int mode, long& M, long& Nn, lon
   }
 }
 
-static int g_conv_math = 0;   // 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6 (process-wide, see tde_set_conv_math)
-
 // Split-K policy (environment overrides are for tuning experiments; read once at load time).
 static long env_long(const char* name, long dflt) {
   const char* v = getenv(name);
   return v ? atol(v) : dflt;
 }
+// 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6 (process-wide, see tde_set_conv_math; TDE_CONV_MATH sets the initial
+// mode for A/B runs).  Default 3: the exact three-way split, the fastest mode within the parity bars.
+static int g_conv_math = (int)env_long("TDE_CONV_MATH", 3);
 static const long g_split_target = env_long("TDE_SPLIT_TARGET", 512);   // blocks to aim for
 static const long g_split_minkt = env_long("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
 static const long g_split_slab = env_long("TDE_SPLIT_SLAB_MB", 128) << 20;
@@ -1083,7 +1088,8 @@ static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
 // only where a wave's fragments feed enough MFMAs (measured: 128x128 1.45x faster than fp32, 128x32
 // 10% slower), so narrower tiles run exact fp32 MFMA in that mode.
 static const long g_math3_min_bn = env_long("TDE_MATH3_MIN_BN", 64);
-static int tile_math(int bn) { return (g_conv_math == 3 && bn < g_math3_min_bn) ? 0 : g_conv_math; }
+static const long g_narrow_math = env_long("TDE_NARROW_MATH", 0);   // math of those narrow tiles (0 or 2)
+static int tile_math(int bn) { return (g_conv_math == 3 && bn < g_math3_min_bn) ? (int)g_narrow_math : g_conv_math; }
 
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
