@@ -25,6 +25,8 @@ SHAPES = [
     ("icnv6", 8, 6, 8, 1024, 512, 3, 1),
     ("cnv4b", 8, 12, 16, 256, 256, 3, 1),
     ("icnv1", 8, 192, 256, 20, 16, 3, 1),
+    ("icnv2", 8, 96, 128, 68, 32, 3, 1),
+    ("icnv3", 8, 48, 64, 132, 64, 3, 1),
     ("cnv7", 8, 3, 4, 512, 512, 3, 2),
     ("cnv7b", 8, 2, 2, 512, 512, 3, 1),
     ("icnv7", 8, 2, 2, 1024, 512, 3, 1),

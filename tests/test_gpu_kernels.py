@@ -87,6 +87,12 @@ CONV_CASES = [
     (8, 3, 4, 512, 512, 512, 3, 1, 512, 0),         # skinny path: M = 96 rows (TM = 6)
     (8, 2, 2, 1020, 1024, 512, 3, 1, 1028, 4),      # skinny path, icnv7-like, w_cin < C, offset view
     (8, 6, 8, 256, 256, 512, 3, 2, 256, 0),         # skinny FWD at stride 2 (M = 8*3*4), tiled DGRAD
+    # halo path (halo_conv.hip; bf16x6 modes, stride 1, >= 16384 output pixels): FWD and DGRAD
+    (2, 96, 128, 32, 32, 32, 7, 1, 32, 0),          # cnv1b: 7x7, one 32-channel chunk, 8-wave tiles
+    (1, 130, 150, 17, 20, 16, 3, 1, 20, 0),         # icnv1-like: ragged tiles, 24-wide chunk, w_cin < C
+    (2, 90, 100, 65, 68, 32, 3, 1, 132, 64),        # icnv2-like: 2 chunks, offset view; DGRAD 2 column tiles
+    (1, 128, 136, 64, 64, 64, 5, 1, 64, 0),         # cnv2b-like: 5x5, 2 chunks, 64 columns
+    (1, 120, 140, 129, 132, 64, 3, 1, 132, 0),      # icnv3-like: 3 chunks; DGRAD 3 column tiles
 ]
 
 
@@ -194,7 +200,8 @@ BN_FUSED_CASES = [
     (True, 2, 3, 4, 64, 32, 7, 2),               # k7 deconv: classes with different tap counts
     (True, 4, 24, 32, 64, 32, 3, 2),             # deconv, split-K, BN partials from the reduce kernel
     (True, 8, 48, 64, 32, 16, 3, 2),             # deconv, no split, BN partials from the epilogue
-    (False, 8, 48, 64, 64, 64, 5, 1),            # cnv2b-like: split-K + reduce-kernel partials
+    (False, 8, 48, 64, 64, 64, 5, 1),            # cnv2b-like (halo path in the bf16x6 modes: tile partials)
+    (False, 2, 96, 128, 32, 32, 7, 1),           # cnv1b-like: halo path, BN partials per pixel tile
 ]
 
 

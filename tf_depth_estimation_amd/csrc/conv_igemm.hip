@@ -20,6 +20,8 @@
 // float atomics).
 #include "tde_common.h"
 #include "bn_internal.h"
+#include "split_math.h"
+#include "halo_conv.h"
 
 #include <cstdlib>
 
@@ -27,25 +29,6 @@ namespace {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 constexpr int NT = 256;
-
-// Division by a runtime constant d >= 1 for 0 <= n < 2^31: q = (umulhi(n, m) + n) >> s with
-// s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1.  Replaces the ~30-instruction integer division
-// in the im2col decode of every k-tile by three instructions.
-struct FDiv {
-  unsigned m; int s;
-};
-
-__host__ __device__ inline FDiv make_fdiv(int d) {
-  FDiv f;
-  f.s = 0;
-  while ((1 << f.s) < d) ++f.s;
-  f.m = (unsigned)((((unsigned long long)1 << 32) * (((unsigned long long)1 << f.s) - (unsigned)d)) / (unsigned)d + 1);
-  return f;
-}
-
-__device__ __forceinline__ int fdiv(int n, FDiv f) {
-  return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s);
-}
 
 struct ConvArgs {
   int N, H, W, C, OH, OW, K, KH, KW, S, PT, PL, wcin;
@@ -159,24 +142,6 @@ struct Img1 {
 // 2% of the step, so the split truncates.
 //   MATH 2: split once per element at LDS staging, three bf16 planes in LDS;
 //   MATH 3: fp32 LDS image (as MATH 0), split per fragment in registers after the LDS read.
-__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
-  const unsigned u = __float_as_uint(x);
-  h = u & 0xFFFF0000u;
-  const float r = x - __uint_as_float(h);
-  m = __float_as_uint(r) & 0xFFFF0000u;
-  l = __float_as_uint(r - __uint_as_float(m));
-}
-__device__ __forceinline__ unsigned pack_hi16(unsigned a, unsigned b) { return (a >> 16) | (b & 0xFFFF0000u); }
-
-__device__ __forceinline__ void split4x3(f4 v, uint2& hi, uint2& mi, uint2& lo) {
-  unsigned h[4], m[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) split3(v[j], h[j], m[j], l[j]);
-  hi = make_uint2(pack_hi16(h[0], h[1]), pack_hi16(h[2], h[3]));
-  mi = make_uint2(pack_hi16(m[0], m[1]), pack_hi16(m[2], m[3]));
-  lo = make_uint2(pack_hi16(l[0], l[1]), pack_hi16(l[2], l[3]));
-}
-
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 // 8 consecutive-k fp32 values (two f4) -> hi / mid / lo bf16x8 fragments
 __device__ __forceinline__ void split8x3(f4 a, f4 b, bf8& hi, bf8& mi, bf8& lo) {
@@ -1070,10 +1035,19 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl) {
   return b;
 }
 
+// Halo path workspace: split weights + BN partials.  Sized for the bf16x6 math whatever the current mode
+// (a caller may size once and switch tde_set_conv_math later).
+static size_t halo_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
+  HaloPlan hp;
+  if (mode == MODE_WGRAD || !halo_plan(d, mode == MODE_FWD ? 0 : 1, 3, hp)) return 0;
+  return hp.wbytes + (bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0);
+}
+
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   const Plan pl = make_plan(d, mode);
-  if (!bn) return pl.ws_bytes;
-  return pl.ws_bytes + bn_plan(d, mode, pl).part_bytes;
+  const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
+  const size_t halo = halo_ws_bytes(d, mode, bn);
+  return igemm > halo ? igemm : halo;
 }
 
 // prefetch depth (tiles in flight) of the fp32 kernels: 1 for 128-row tiles, 2 for the 64-row tiles of
@@ -1205,6 +1179,24 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
                size_t ws_bytes, void* stream) {
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  HaloPlan hp;
+  if (MODE != MODE_WGRAD && halo_plan(*d, MODE == MODE_FWD ? 0 : 1, g_conv_math, hp)) {
+    // stride-1, few-channel, high-resolution layer: halo-tiled kernel (halo_conv.hip)
+    const size_t pbytes = bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0;
+    if (hp.wbytes + pbytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    char* body = tde_ws_body(ws);
+    double* part = bn ? reinterpret_cast<double*>(body + hp.wbytes) : nullptr;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const float* in = MODE == MODE_FWD ? a.x : a.dy;
+    float* z = MODE == MODE_FWD ? a.y : a.dx;
+    if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, part, st);
+    if (bn) {
+      const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                    bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu};
+      bn_fwd_from_partials_launch(d->N * d->H * d->W, hp.Ncols, z, hp.nparts, part, o, st);
+    }
+    return tde_launch_status();
+  }
   const Plan pl = make_plan(*d, MODE);
   BnPlan bp{};
   if (bn) bp = bn_plan(*d, MODE, pl);
@@ -1277,6 +1269,22 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
                    void* stream) {
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  HaloPlan hp;
+  if (MODE1 == MODE_DGRAD && halo_plan(*d, 1, g_conv_math, hp)) {
+    // data gradient on the halo path, filter gradient on the implicit GEMM (two launches + its reduce)
+    const Plan p2 = make_plan(*d, MODE_WGRAD);
+    if (hp.wbytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    char* body = tde_ws_body(ws);
+    a2.ws = reinterpret_cast<float*>(body + hp.wbytes);
+    a2.splits = p2.splits; a2.kt_per = p2.kt_per; a2.accumulate = acc2; a2.bnp = nullptr;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!skip) {
+      halo_launch(hp, *d, a1.dy, a1.w, a1.dx, acc1, body, nullptr, st);
+      launch_mode<MODE_WGRAD>(p2, a2, st);
+    }
+    if (!skipr) launch_reduce<MODE_WGRAD>(p2, a2, st);
+    return tde_launch_status();
+  }
   const Plan p1 = make_plan(*d, MODE1);
   const bool fuse = g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0;
   const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : make_plan(*d, MODE_WGRAD);
@@ -1305,7 +1313,12 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   const Plan p1 = make_plan(d, mode1);
   const size_t fused = p1.skinny_tm ? 0 : p1.slab_bytes + make_plan(d, MODE_WGRAD, p1.bm, p1.bn).slab_bytes;
   const size_t split = p1.slab_bytes + make_plan(d, MODE_WGRAD).slab_bytes;
-  return (fused > split ? fused : split) + 64;
+  size_t b = fused > split ? fused : split;
+  if (mode1 == MODE_DGRAD) {
+    const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
+    if (h && h + make_plan(d, MODE_WGRAD).slab_bytes > b) b = h + make_plan(d, MODE_WGRAD).slab_bytes;
+  }
+  return b + 64;
 }
 
 static bool bn_ok(const tde_bn_train_t* bn, int C) {

@@ -1,0 +1,32 @@
+// Halo-tiled stride-1 convolution (bf16x6 MFMA) -- internal interface between conv_igemm.hip (the ABI
+// entry points and their planners) and halo_conv.hip (the kernels).
+#pragma once
+#include "tde_common.h"
+
+// Plan of one stride-1 FWD (y = conv(x, w)) or DGRAD (dx = conv(dy, flip(w)^T)) call on the halo path.
+struct HaloPlan {
+  int ok;
+  int mode;               // 0 FWD, 1 DGRAD (of a stride-1 conv)
+  int NW, TN;             // waves per block (pixel rows 2*NW), 16-column MFMA fragments per wave
+  int HWd, HP;            // halo width (16 + KW - 1), halo pixels
+  int CC, nch, SA;        // channels per chunk (multiple of 8), chunks, LDS row stride (u16)
+  int steps, ntap;        // 32-deep k-steps per chunk, KH*KW
+  int KH, KW, PT, PL;     // geometry of the conv as executed (DGRAD: flipped taps and pads)
+  int Cv, ics, ico;       // input view: channels read, cstride, coff
+  int Cred;               // reduction channels with nonzero weights (FWD: w_cin, DGRAD: K)
+  int Ncols, ocs, oco;    // output columns and view
+  int ncolt, NcolsP;      // column tiles of 16*TN, padded column count of the split weights
+  int gx, gy, gz;         // grid
+  size_t wbytes;          // split-weight planes in the workspace
+  size_t lds_bytes;
+  int nparts;             // BN statistics partials (one per pixel tile)
+};
+
+// mode 0 FWD / 1 DGRAD of the conv described by d; math = current conv math.  Returns false when the
+// call should take the implicit-GEMM path.
+bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp);
+
+// Weight split (one launch) + conv (one launch).  ws: >= hp.wbytes of 16-byte aligned workspace;
+// bnp: fp64 BN partials [hp.nparts][2][Ncols] or null.
+void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
+                 int accumulate, void* ws, double* bnp, hipStream_t st);

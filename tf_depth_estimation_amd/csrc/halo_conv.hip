@@ -1,0 +1,433 @@
+// Halo-tiled stride-1 convolution on bf16x6 MFMA (gfx950).
+//
+// Replaces TF's Conv2D / Conv2DBackpropInput for the stride-1, few-channel, high-resolution layers of
+// the reference networks (cnv1b 7x7 32->32 @96x128, cnv2b 5x5 @48x64, icnv1/icnv2/icnv3 3x3 on the
+// decoder concats; nets_optflow_depth.py:89-141).  There the
+// implicit GEMM (conv_igemm.hip) re-gathers its im2col operand once per 32-deep k-tile: every input
+// pixel crosses L2 -> LDS KH*KW times (49x for cnv1b), and that traffic, not the MFMAs, sets the time.
+//
+// Here a block owns a (2*NW) x 16 output-pixel tile of one image and 16*TN output columns:
+//   1. its input halo ((2*NW + KH - 1) x (16 + KW - 1) pixels x one channel chunk) is loaded ONCE,
+//      split into exact bf16 hi/mid/lo planes (split_math.h) and kept in LDS for all KH*KW taps;
+//   2. the weights, pre-split by halo_wprep_kernel into [k-step][plane][column][32] bf16 tiles, stream
+//      through a double-buffered LDS slot, one 32-deep k-step per barrier;
+//   3. each wave owns two 16-pixel rows x all TN column fragments: per k-step it reads its A fragments
+//      straight out of the halo (row = pixel + tap offset) and issues 6 v_mfma_f32_16x16x32_bf16 per
+//      fragment pair (the bf16x6 product, fp32 accumulation).
+// The reduction index is (chunk, tap, channel-in-chunk) with the chunk width a multiple of 8, so the 8
+// consecutive k of one MFMA lane never straddle a tap.  DGRAD is the same kernel on dy with the taps
+// flipped, the pads mirrored and the weights transposed (done by the prep kernel).  Optional fp64 BN
+// statistics partials (one per pixel tile) feed bn_fwd_from_partials_launch exactly like the
+// implicit GEMM's epilogue partials.
+#include "halo_conv.h"
+
+#include <cstdlib>
+#include <type_traits>
+
+#include "split_math.h"
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16;
+// LDS row strides: a 16-lane group of ds_read_b128 fragment reads (rows r16, 16-byte column q) is
+// conflict-free when the row stride in 16-byte units is 2 mod 4 (gfx950 lane groups {0-3,12-15,20-27},
+// ...; an odd stride such as 80 B costs 2 cycles per group -- measured SQ_LDS_BANK_CONFLICT = 50% of the
+// LDS cycles).  B rows: 32 k + 16 pad = 96 bytes.
+constexpr int LDB = 48;
+
+struct HaloArgs {
+  int N, H, W;
+  int HWd, HP, CC, nch, SA, steps, ntap, KW, PT, PL;
+  int Cv, ics, ico, Ncols, ocs, oco, ncolt, NcolsP;
+  int accumulate;
+  FDiv fCC, fKW, fC4, fHWd;
+  const float* in;
+  float* out;
+  const u16* wp;
+  double* bnp;
+};
+
+// Split weights, one contiguous B tile per (k-step g, column tile ct):
+//   wp[(((g * ncolt + ct) * 3 + plane) * NCP + cl) * LDB + rl]   (rl < 32; rl 32..47 = 0, the LDS row pad)
+// g = chunk * steps + step, r = step * 32 + rl = tap * CC + cc within the chunk, reduction channel
+// c = chunk * CC + cc, column col = ct * NCP + cl:
+//   FWD  : B[(tap, c)][col] = w[tap][c][col]                     (w [KH][KW][wcin][K], c < wcin)
+//   DGRAD: B[(tap, k)][col] = w[ntap - 1 - tap][col][k]          (col = dx channel < wcin, k < K)
+// The tile is copied byte-for-byte into its LDS ring slot by LDS-DMA, so this IS the LDS image.
+__global__ void __launch_bounds__(256) halo_wprep_kernel(const float* __restrict__ w, u16* __restrict__ wp, int mode,
+                                                         long total, int steps, int CC, int ntap, int Cred,
+                                                         int Ncols, int NCP, int ncolt, int wcin, int K) {
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int rl = (int)(idx % LDB);
+    long t = idx / LDB;
+    const int cl = (int)(t % NCP);
+    t /= NCP;
+    const int ct = (int)(t % ncolt);
+    const int g = (int)(t / ncolt);
+    const int col = ct * NCP + cl;
+    const int ch = g / steps, s = g - ch * steps;
+    const int r = s * 32 + rl, tap = r / CC, cc = r - tap * CC, c = ch * CC + cc;
+    float v = 0.f;
+    if (rl < 32 && tap < ntap && c < Cred && col < Ncols) {   // rl 32..47: LDS row pad
+      if (mode == 0) v = w[((long)tap * wcin + c) * K + col];
+      else if (col < wcin) v = w[((long)(ntap - 1 - tap) * wcin + col) * K + c];
+    }
+    unsigned h, m, l;
+    split3(v, h, m, l);
+    const long base = ((((long)g * ncolt + ct) * 3) * NCP + cl) * LDB + rl;
+    wp[base] = (u16)(h >> 16);
+    wp[base + (long)NCP * LDB] = (u16)(m >> 16);
+    wp[base + 2l * NCP * LDB] = (u16)(l >> 16);
+  }
+}
+
+// Workgroup barrier that waits only for this wave's LDS operations.  __syncthreads() is a release/acquire
+// fence + s_barrier, and the fence makes the compiler drain every outstanding global load (vmcnt(0))
+// first, which would retire the weight-tile DMAs still in flight.  The "memory" clobber keeps the
+// compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+template <int NW, int TN>
+__global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  constexpr int NT = 64 * NW, NCP = 16 * TN;
+  constexpr int BPL = NCP * LDB, BTILE = 3 * BPL;           // u16 per B tile
+  constexpr int NI = (BTILE * 2 + 1023) / 1024;             // 1-KiB DMA wave-instructions per tile
+  constexpr int DI = (NI + NW - 1) / NW;                    // per wave (uniform: extra ones duplicate)
+  constexpr int BSLOT = NI * 512;                           // u16 per ring slot (whole 1-KiB pieces)
+  constexpr int NSLOT = 3;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r16 = lane & 15, q = lane >> 4;
+  const int x0 = blockIdx.x * 16, y0 = blockIdx.y * (2 * NW);
+  const int n = blockIdx.z / p.ncolt, ct = blockIdx.z - n * p.ncolt;
+  const int col0 = ct * NCP;
+  const int PLANE = p.HP * p.SA;
+  u16* const As = lds;
+  u16* const Bs = lds + 3 * PLANE;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(p.in, (long)p.N * p.H * p.W * p.ics);
+
+  // B tiles reach their ring slot by LDS-DMA (global_load_lds_dwordx4: each wave-instruction copies 1 KiB,
+  // lane i -> slot + 16 i); the tile of step s + 2 is issued while step s computes, and a counted
+  // vmcnt wait + raw barrier retires one tile per step, so two tiles stay in flight across barriers.
+  // Lanes past the tile re-read its last 16 bytes into the slot's tail padding.
+  auto dma_b = [&](int g, int slot) __attribute__((always_inline)) {
+    const u16* src = p.wp + ((long)g * p.ncolt + ct) * BTILE;
+#pragma unroll
+    for (int j = 0; j < DI; ++j) {
+      const int piece = min(wv + j * NW, NI - 1);
+      const int off = min((piece * 64 + lane) * 8, BTILE - 8);   // u16
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + off), (lds_ptr_t)(Bs + slot * BSLOT + piece * 512), 16, 0,
+                                       0);
+    }
+  };
+
+  // halo of channel chunk ch -> three bf16 planes [HP][SA]; 8 loads in flight per thread
+  auto stage_a = [&](int ch) __attribute__((always_inline)) {
+    const int nc4 = p.CC >> 2, total = p.HP * nc4;
+    for (int base = 0; base < total; base += 8 * NT) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * NT + tid;
+        const int hp = fdiv(idx, p.fC4), c4 = idx - hp * nc4;
+        const int hy = fdiv(hp, p.fHWd), hx = hp - hy * p.HWd;
+        const int iy = y0 - p.PT + hy, ix = x0 - p.PL + hx, c = ch * p.CC + 4 * c4;
+        const bool ok = idx < total && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && c < p.Cv;
+        v[u] = bload(rin, ok ? 4 * (((n * p.H + iy) * p.W + ix) * p.ics + p.ico + c) : OOB);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = base + u * NT + tid;
+        if (idx < total) {
+          const int hp = fdiv(idx, p.fC4), c4 = idx - hp * nc4;
+          uint2 hi, mi, lo;
+          split4x3(v[u], hi, mi, lo);
+          u16* d = As + hp * p.SA + 4 * c4;
+          *reinterpret_cast<uint2*>(d) = hi;
+          *reinterpret_cast<uint2*>(d + PLANE) = mi;
+          *reinterpret_cast<uint2*>(d + 2 * PLANE) = lo;
+        }
+      }
+    }
+  };
+
+  f4 acc[2][TN];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // LDS offset (u16) of this lane's A fragment rows at tap (0, 0): pixel rows 2*wv + a, column r16
+  const int arow0 = ((2 * wv) * p.HWd + r16) * p.SA, arow1 = arow0 + p.HWd * p.SA;
+
+  // one k-step s from ring slot `slot`
+  auto compute = [&](int s, int slot) __attribute__((always_inline)) {
+    // reduction index of this lane's 8 k: tap and channel in the chunk (k past the taps: weights are 0)
+    const int r0 = s * 32 + 8 * q;
+    int tap = fdiv(r0, p.fCC), cc = r0 - tap * p.CC;
+    if (tap >= p.ntap) { tap = 0; cc = 0; }
+    const int kh = fdiv(tap, p.fKW), kw = tap - kh * p.KW;
+    const int toff = (kh * p.HWd + kw) * p.SA + cc;
+    bf8 ah[2], am[2], al[2], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const u16* src = As + (a ? arow1 : arow0) + toff;
+      ah[a] = *reinterpret_cast<const bf8*>(src);
+      am[a] = *reinterpret_cast<const bf8*>(src + PLANE);
+      al[a] = *reinterpret_cast<const bf8*>(src + 2 * PLANE);
+    }
+    const u16* bsrc = Bs + slot * BSLOT + r16 * LDB + 8 * q;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      bh[b] = *reinterpret_cast<const bf8*>(bsrc + b * 16 * LDB);
+      bm[b] = *reinterpret_cast<const bf8*>(bsrc + BPL + b * 16 * LDB);
+      bl[b] = *reinterpret_cast<const bf8*>(bsrc + 2 * BPL + b * 16 * LDB);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+      }
+  };
+
+  for (int ch = 0; ch < p.nch; ++ch) {
+    const int g0 = ch * p.steps, gl = g0 + p.steps - 1;
+    if (ch > 0) {
+      vm_wait<0>();     // the previous chunk's trailing DMAs have landed before their slots are reused
+      lds_barrier();    // and nobody still reads its halo or slots
+    }
+    dma_b(g0, 0);
+    dma_b(min(g0 + 1, gl), 1);
+    stage_a(ch);        // its loads are younger than the two DMAs and waited for inside
+    vm_wait<DI>();      // this wave's part of tile 0 has landed (tile 1 may still fly)
+    lds_barrier();
+    int slot = 0;
+    for (int s = 0; s < p.steps; ++s) {
+      // slot (slot + 2) % 3 was read by step s - 1, which every wave finished before the last barrier
+      dma_b(min(g0 + s + 2, gl), slot == 0 ? 2 : slot - 1);
+      compute(s, slot);
+      vm_wait<DI>();    // tile s + 1 landed (tile s + 2 may still fly)
+      lds_barrier();
+      slot = slot == 2 ? 0 : slot + 1;
+    }
+  }
+  vm_wait<0>();
+
+  // ---- epilogue: acc[a][b][r] = out(pixel (y0 + 2*wv + a, x0 + 4q + r), column col0 + 16b + r16)
+  bool rowok[2][4];
+  long rowaddr[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int y = y0 + 2 * wv + a, x = x0 + 4 * q + r;
+      rowok[a][r] = y < p.H && x < p.W;
+      rowaddr[a][r] = ((long)(n * p.H + y) * p.W + x) * p.ocs + p.oco;
+    }
+  if (p.bnp != nullptr) {
+    // fp64 BN statistics partial of this pixel tile, per column (the main loop ended with a barrier)
+    float* red = reinterpret_cast<float*>(lds);   // [2][NW][NCP]
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      float cs = 0.f, cq = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = rowok[a][r] ? acc[a][b][r] : 0.f;
+          cs += v; cq += v * v;
+        }
+      cs += __shfl_xor(cs, 16, 64); cq += __shfl_xor(cq, 16, 64);
+      cs += __shfl_xor(cs, 32, 64); cq += __shfl_xor(cq, 32, 64);
+      if (lane < 16) {
+        red[wv * NCP + b * 16 + lane] = cs;
+        red[(NW + wv) * NCP + b * 16 + lane] = cq;
+      }
+    }
+    __syncthreads();
+    if (tid < NCP && col0 + tid < p.Ncols) {
+      double sv = 0.0, sq = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { sv += red[w * NCP + tid]; sq += red[(NW + w) * NCP + tid]; }
+      const long j = ((long)n * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      p.bnp[j * 2 * p.Ncols + col0 + tid] = sv;
+      p.bnp[j * 2 * p.Ncols + p.Ncols + col0 + tid] = sq;
+    }
+  }
+  if (p.accumulate) {
+    // every old value in flight before the first add (branch-free buffer loads; invalid -> 0, unused)
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out, (long)p.N * p.H * p.W * p.ocs);
+    float old[2][4][TN];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int col = col0 + b * 16 + r16;
+          const bool ok = rowok[a][r] && col < p.Ncols;
+          old[a][r][b] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rout, ok ? (int)(4 * (rowaddr[a][r] + col)) : OOB, 0, 0));
+        }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b][r] += old[a][r][b];
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = col0 + b * 16 + r16;
+        if (rowok[a][r] && col < p.Ncols) p.out[rowaddr[a][r] + col] = acc[a][b][r];
+      }
+}
+
+long env_l(const char* name, long dflt) {
+  const char* v = getenv(name);
+  return v ? atol(v) : dflt;
+}
+const long g_halo = env_l("TDE_HALO", 1);                 // 0: never take the halo path (A/B)
+const long g_halo_min_m = env_l("TDE_HALO_MIN_M", 16384); // output pixels (N*H*W) from which it pays
+const long g_halo_nw = env_l("TDE_HALO_NW", 0);           // force 4 or 8 waves per block
+const long g_halo_lds = env_l("TDE_HALO_LDS_KB", 150) << 10;
+const long g_halo_minch = env_l("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
+
+int lds_stride(int cc) {   // smallest row stride (u16) >= cc whose 16-byte count is 2 mod 4
+  int s = cc;
+  while ((s / 8) % 4 != 2) s += 8;
+  return s;
+}
+
+template <int NW, int TN>
+void launch_t(const HaloPlan& hp, const HaloArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_conv_kernel<NW, TN>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((halo_conv_kernel<NW, TN>), dim3(hp.gx, hp.gy, hp.gz), dim3(64 * NW), hp.lds_bytes, st, a);
+}
+
+}  // namespace
+
+bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
+  hp = HaloPlan{};
+  if (!g_halo || (math != 2 && math != 3) || d.stride != 1 || (mode != 0 && mode != 1)) return false;
+  if (d.OH != d.H || d.OW != d.W || (long)d.N * d.H * d.W < g_halo_min_m) return false;
+  hp.mode = mode;
+  hp.KH = d.KH; hp.KW = d.KW;
+  if (mode == 0) {
+    hp.PT = d.pad_top; hp.PL = d.pad_left;
+    hp.Cv = d.C; hp.ics = d.x_cstride; hp.ico = d.x_coff; hp.Cred = d.w_cin;
+    hp.Ncols = d.K; hp.ocs = d.y_cstride; hp.oco = d.y_coff;
+  } else {
+    hp.PT = d.KH - 1 - d.pad_top; hp.PL = d.KW - 1 - d.pad_left;
+    hp.Cv = d.K; hp.ics = d.y_cstride; hp.ico = d.y_coff; hp.Cred = d.K;
+    hp.Ncols = d.C; hp.ocs = d.x_cstride; hp.oco = d.x_coff;
+  }
+  if (hp.PT < 0 || hp.PL < 0 || hp.PT >= hp.KH || hp.PL >= hp.KW) return false;
+  hp.ntap = d.KH * d.KW;
+  hp.HWd = 16 + d.KW - 1;
+  // columns: TN fragments per block, fewest padded columns (+ a per-tile overhead of 32 columns)
+  long best = -1;
+  for (int tn = 1; tn <= 4; ++tn) {
+    const long nt = tde_cdiv(hp.Ncols, 16 * tn), cost = nt * (16 * tn + 32);
+    if (best < 0 || cost < best) { best = cost; hp.TN = tn; }
+  }
+  hp.ncolt = tde_cdiv(hp.Ncols, 16 * hp.TN);
+  hp.NcolsP = hp.ncolt * 16 * hp.TN;
+  // Tile shape by a throughput model fitted to the measured layers (scripts/conv_micro.py sweep): per-SIMD
+  // MFMA work = rounds of concurrently resident blocks x k-steps x TN, divided by an efficiency that is
+  // low for one wave per SIMD (nothing hides its LDS / barrier latency) -- the grid must also cover the
+  // chip (cnv2b at 16-row tiles is 96 blocks: 8-row tiles won by 1.4x).
+  const int cp8 = (hp.Cv + 7) / 8 * 8;
+  const int nws[2] = {8, 4};
+  const size_t btile = (size_t)3 * 16 * hp.TN * LDB * 2;                              // bytes
+  const size_t ring = 3 * ((btile + 1023) / 1024 * 1024);
+  double best_est = -1.0;
+  for (int i = 0; i < 2; ++i) {
+    const int nw = nws[i];
+    if (g_halo_nw && nw != g_halo_nw) continue;
+    const int hh = 2 * nw + d.KH - 1;
+    int tried = 0;
+    for (int nch = (int)g_halo_minch; nch <= cp8 / 8 && tried < 3; ++nch) {
+      const int cc = ((cp8 + nch - 1) / nch + 7) / 8 * 8;
+      if (nch > 1 && (cp8 + cc - 1) / cc < nch) continue;   // same chunking as a smaller nch
+      const int sa = lds_stride(cc);
+      const size_t lds = (size_t)3 * hh * hp.HWd * sa * 2 + ring;
+      if (lds > (size_t)g_halo_lds) continue;
+      ++tried;
+      const int nchr = (cp8 + cc - 1) / cc;
+      const long blocks = (long)tde_cdiv(d.W, 16) * tde_cdiv(d.H, 2 * nw) * d.N * hp.ncolt;
+      int bpc = (int)((160 * 1024) / lds);
+      if (bpc > 12 / nw) bpc = 12 / nw;            // ~130-170 VGPRs: <= 3 waves per SIMD
+      if (bpc < 1) bpc = 1;
+      const long rounds = (blocks + 256L * bpc - 1) / (256L * bpc);
+      const long res = blocks < 256L * bpc ? (blocks + 255) / 256 : bpc;   // blocks per busy CU
+      const double share = (double)(nw * res) / 4.0;                        // waves per SIMD
+      const double eff = share >= 2.0 ? 1.0 : (share >= 1.0 ? 0.6 : 0.6 * share);
+      const double est = (double)rounds * nchr * tde_cdiv((long)hp.ntap * cc, 32) * hp.TN * share / eff +
+                         2.0 * nchr;   // + halo staging per chunk
+      if (best_est < 0 || est < best_est - 1e-9) {
+        best_est = est;
+        hp.NW = nw; hp.CC = cc; hp.nch = nchr; hp.SA = sa; hp.HP = hh * hp.HWd;
+        hp.lds_bytes = lds; hp.ok = 1;
+      }
+    }
+  }
+  if (!hp.ok) return false;
+  hp.steps = tde_cdiv((long)hp.ntap * hp.CC, 32);
+  hp.gx = tde_cdiv(d.W, 16);
+  hp.gy = tde_cdiv(d.H, 2 * hp.NW);
+  hp.gz = d.N * hp.ncolt;
+  hp.nparts = hp.gx * hp.gy * d.N;
+  hp.wbytes = ((size_t)hp.nch * hp.steps * 3 * hp.NcolsP * LDB * 2 + 255) / 256 * 256;
+  return true;
+}
+
+void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
+                 int accumulate, void* ws, double* bnp, hipStream_t st) {
+  u16* wp = static_cast<u16*>(ws);
+  const long total = (long)hp.nch * hp.steps * hp.NcolsP * LDB;
+  long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(halo_wprep_kernel, dim3((int)blocks), dim3(256), 0, st, w, wp, hp.mode, total, hp.steps, hp.CC,
+                     hp.ntap, hp.Cred, hp.Ncols, 16 * hp.TN, hp.ncolt, d.w_cin, d.K);
+  HaloArgs a{};
+  a.N = d.N; a.H = d.H; a.W = d.W;
+  a.HWd = hp.HWd; a.HP = hp.HP; a.CC = hp.CC; a.nch = hp.nch; a.SA = hp.SA; a.steps = hp.steps; a.ntap = hp.ntap;
+  a.KW = hp.KW; a.PT = hp.PT; a.PL = hp.PL;
+  a.Cv = hp.Cv; a.ics = hp.ics; a.ico = hp.ico; a.Ncols = hp.Ncols; a.ocs = hp.ocs; a.oco = hp.oco;
+  a.ncolt = hp.ncolt; a.NcolsP = hp.NcolsP; a.accumulate = accumulate;
+  a.fCC = make_fdiv(hp.CC); a.fKW = make_fdiv(hp.KW); a.fC4 = make_fdiv(hp.CC / 4); a.fHWd = make_fdiv(hp.HWd);
+  a.in = in; a.out = out; a.wp = wp; a.bnp = bnp;
+  const int key = hp.NW * 10 + hp.TN;
+  switch (key) {
+    case 81: launch_t<8, 1>(hp, a, st); break;
+    case 82: launch_t<8, 2>(hp, a, st); break;
+    case 83: launch_t<8, 3>(hp, a, st); break;
+    case 84: launch_t<8, 4>(hp, a, st); break;
+    case 41: launch_t<4, 1>(hp, a, st); break;
+    case 42: launch_t<4, 2>(hp, a, st); break;
+    case 43: launch_t<4, 3>(hp, a, st); break;
+    default: launch_t<4, 4>(hp, a, st); break;
+  }
+}
