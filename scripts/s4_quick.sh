@@ -1,0 +1,6 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kernels.py -k "conv" > gpurun_out/q_kern.log 2>&1; rc=$?; tail -2 gpurun_out/q_kern.log; [ $rc -le 1 ] || exit $rc
+bash scripts/ab_env.sh "${@:-d:X=1}"

@@ -77,7 +77,10 @@ __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<con
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
 constexpr int BK3 = 32;
-constexpr int LDR = BK3 + 8;   // 80-byte rows: ds_read_b128 fragments hit distinct 16-B slots
+// LDS row strides: the 16 lanes of a ds_read_b128 lane group read rows r16 at 16-byte column q; that is
+// conflict-free when the row stride in 16-byte units is 2 mod 4 (an odd stride, e.g. 80 or 144 bytes,
+// costs 2 LDS cycles per group; halo_conv.hip measured 50% conflict cycles with one)
+constexpr int LDR = BK3 + 16;   // 96-byte bf16 plane rows
 
 __device__ __forceinline__ unsigned bf16_rne_bits(float x) {
   const unsigned u = __float_as_uint(x);
@@ -113,8 +116,10 @@ struct Img3 {
   }
 };
 
-// fp32 image: [row][BK3 + 4] floats (144-byte rows: the 16 rows of a fragment read land on 16
-// distinct 16-B bank slots), read as f4 = the 4 k of one v_mfma_f32_16x16x4_f32 lane.
+// fp32 image: [row][BK3 + 4] floats (144-byte rows), read as f4 = the 4 k of one v_mfma_f32_16x16x4_f32
+// lane (MATH 0) or two f4 at k = 4q and 16 + 4q (MATH 3, see compute()).  144 B is an odd 16-byte count
+// (2-way conflicts per lane group); the conflict-free 160 B was measured 2% slower per step: it pushes
+// the 128x128 double-buffered image to 80 KiB, one workgroup per CU.
 constexpr int LDF = BK3 + 4;
 
 template <int ROWS>
@@ -431,13 +436,15 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         f4 fa[TM][2], fb[TN][2];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
-          fa[a][0] = IA::frag(A, wrow0 + a * 16 + r16, 8 * q);
-          fa[a][1] = IA::frag(A, wrow0 + a * 16 + r16, 8 * q + 4);
+          // lane q feeds MFMA k-slots 8q..8q+7 with image k = 4q..4q+3, 16+4q..16+4q+3 (the same permutation
+          // for A and B, so the contraction is unchanged): 16-byte column q, conflict-free reads
+          fa[a][0] = IA::frag(A, wrow0 + a * 16 + r16, 4 * q);
+          fa[a][1] = IA::frag(A, wrow0 + a * 16 + r16, 16 + 4 * q);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
-          fb[b][0] = IB::frag(Bm, wcol0 + b * 16 + r16, 8 * q);
-          fb[b][1] = IB::frag(Bm, wcol0 + b * 16 + r16, 8 * q + 4);
+          fb[b][0] = IB::frag(Bm, wcol0 + b * 16 + r16, 4 * q);
+          fb[b][1] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 + 4 * q);
         }
         issue();
 #pragma unroll
