@@ -1070,14 +1070,18 @@ static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
 // 10% slower), so narrower tiles run exact fp32 MFMA in that mode.
 static const long g_math3_min_bn = env_long("TDE_MATH3_MIN_BN", 64);
 static const long g_narrow_math = env_long("TDE_NARROW_MATH", 0);   // math of those narrow tiles (0 or 2)
-static int tile_math(int bn) { return (g_conv_math == 3 && bn < g_math3_min_bn) ? (int)g_narrow_math : g_conv_math; }
+static const long g_math3_wgrad_min_bn = env_long("TDE_MATH3_WGRAD_MIN_BN", 64);   // the same for WGRAD alone
+static int tile_math(int bn, int mode = -1) {
+  const long lim = mode == MODE_WGRAD ? g_math3_wgrad_min_bn : g_math3_min_bn;
+  return (g_conv_math == 3 && bn < lim) ? (int)g_narrow_math : g_conv_math;
+}
 
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? 2 : 1);
-  const int math = tile_math(BN);
+  const int math = tile_math(BN, MODE);
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 3 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
