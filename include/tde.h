@@ -57,6 +57,12 @@ typedef struct {
 int tde_abi_version(void);
 const char* tde_status_string(int status);
 
+/* Host-side CRC-32C (Castagnoli) of n bytes, continuing from `crc` (0 to start); the checksum of the
+ * TF tensor-bundle checkpoint format (BundleEntryProto.crc32c, table block trailers) behind
+ * tf.train.Saver (batch_prediction.py:49-55, split_training.py:147-202), used by
+ * tf_depth_estimation_amd/checkpoint.py.  No device work; callable without a GPU. */
+uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
+
 /* ---------------------------------------------------------------- MFMA implicit-GEMM convs
  * slim.conv2d (no bias; the BN that follows owns the shift), nets_optflow_depth.py:88-101,107-142
  * -> TF Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter.

@@ -71,6 +71,7 @@ _SIGS = {
     "tde_cam_coords_bwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P]),
     "tde_pose_dp_to_dt": (c_int, [c_int, P, P, P, P]),
     "tde_abi_version": (c_int, []),
+    "tde_crc32c": (ctypes.c_uint32, [P, c_size_t, ctypes.c_uint32]),
     "tde_status_string": (ctypes.c_char_p, [c_int]),
     "tde_set_conv_math": (c_int, [c_int]),
     "tde_get_conv_math": (c_int, []),
