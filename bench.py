@@ -246,6 +246,9 @@ def main():
                          "precision, or the fp32-accurate 3-way bf16 split (LDS-staged / register-split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
+                         "runs eagerly, RCCL is not captured)")
     ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
                     help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
     args = ap.parse_args()
@@ -271,6 +274,8 @@ def main():
             tr.enable_ddp(world, bucket_mb=args.bucket_mb)
         else:
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
+    if args.sync_bn:
+        tr.enable_sync_bn(world)
     progs = tr.programs()
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
@@ -287,7 +292,7 @@ def main():
     conv_flops = sum(c[1] for c in conv)
     conv_launches = sum(c[2] for c in conv)
 
-    use_graph = not args.no_graph
+    use_graph = not args.no_graph and not args.sync_bn
     if use_graph:
         tr.capture()
     for _ in range(args.warmup):
@@ -342,6 +347,7 @@ def main():
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
+                       "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",

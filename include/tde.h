@@ -169,6 +169,27 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,
                float* dbeta, int accumulate_dbeta, int relu, void* ws, size_t ws_bytes, void* stream);
 
+/* SyncBN (BatchNorm over the batch of ALL data-parallel replicas), in two phases around
+ * the caller's all-reduce of `sums` (fp64 [2][C]):
+ *   forward : tde_bn_sums(mode 0) -> sums = (sum z, sum z^2) over this replica's M rows; all-reduce;
+ *             tde_bn_fwd_from_sums(M, C, M_total, ...) = tde_bn_fwd_train semantics over M_total rows.
+ *   backward: tde_bn_sums(mode 1) -> (sum g, sum g*xhat), g = dy * relu'(y); keep a copy (local), all-reduce
+ *             (global); tde_bn_bwd_from_sums: dz from the global means, dbeta from the LOCAL sum g (the
+ *             data-parallel gradient average divides the summed dbeta by the replica count).
+ * Replaces slim.batch_norm's moments over the single-device batch (nets_optflow_depth.py:82-87) with
+ * moments over the global batch (the reference's own semantics at global batch 64 on one device). */
+int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, int dy_coff,
+                const float* save_mean, const float* save_invstd, const float* beta, int relu, int mode,
+                double* sums, void* ws, size_t ws_bytes, void* stream);
+int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const double* sums, const float* beta,
+                         float eps, float decay, int bessel, float* moving_mean, float* moving_var,
+                         float* save_mean, float* save_invstd, float* y, int y_cstride, int y_coff, int relu,
+                         void* stream);
+int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean,
+                         const float* save_invstd, const float* beta, const float* dy, int dy_cstride, int dy_coff,
+                         const double* global_sums, const double* local_sums, float* dz, float* dbeta,
+                         int accumulate_dbeta, int relu, void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- legacy resizes
  * resize_like -> tf.image.resize_nearest_neighbor (nets_optflow_depth.py:11-16),
  * tf.image.resize_bilinear of the disparity (nets_optflow_depth.py:124,131,138),

@@ -54,3 +54,40 @@ def test_overlapped_exchange_world1_matches_plain(pg, graph):
     p1, g1 = _trainer(True, graph, 3)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
+
+
+def test_sync_bn_world1_step_parity(pg):
+    """SyncBN through the trainer (enable_sync_bn) over a world-1 RCCL group: the all-reduces are the
+    identity, so the eager config-2 step must meet the same bars as the plain step against the float64
+    oracle (loss 1e-5; whole gradient within the fp32 noise model of tests/test_gpu_nets.py -- the BN
+    summation order differs from the fused conv+BN path, and these gradients amplify rounding);
+    capture is refused (RCCL inside the step)."""
+    from oracle import losses as OL
+    from oracle import nets as ON
+    from test_gpu_nets import GRAD_FACTOR, check_grads_global, oracle_params_from
+    from tf_depth_estimation_amd import _api, _lib, train, variables
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    N, H, W = 2, 64, 96
+    tr = train.DepthOnlyTrainer(N, H, W)
+    g = np.random.default_rng(4)
+    x = torch.tensor(g.uniform(-0.5, 0.5, (N, H, W, 3)), dtype=torch.float32)
+    lab = torch.tensor(g.uniform(0.25, 4.0, (N, H, W, 1)), dtype=torch.float32)
+    tr.set_batch(x.cuda(), lab.cuda())
+    tr.enable_sync_bn(1)
+    with pytest.raises(NotImplementedError):
+        tr.capture()
+    Ps = {dt: oracle_params_from(tr.chunk, "", dt) for dt in (torch.float64, torch.float32)}
+    tr.phase_compute()
+    torch.cuda.synchronize()
+    grads = {}
+    for dt, P in Ps.items():
+        lr, _ = OL.loss_depth_only(ON.disp_net(P, x.to(dt), True, scope="model/depth_net"), lab.to(dt))
+        lr.backward()
+        grads[dt] = {k: v.grad for k, v in P.vars.items()}
+        if dt == torch.float64:
+            assert abs(tr.total_loss() - lr.item()) <= 1e-5 * abs(lr.item())
+    check_grads_global({k: tr.chunk.grad_view(k) for k in grads[torch.float64]}, grads[torch.float64],
+                       grads[torch.float32], GRAD_FACTOR[_lib.load().tde_get_conv_math()])
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()

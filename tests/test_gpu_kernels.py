@@ -546,3 +546,60 @@ def test_loss_depth_pyramid_matches_separate_terms(L, recip, nonfinite, acc):
         close(got_g[s][..., 0], base[s][..., 0], what=f"untouched channel scale {s}")
     close(loss, ref_loss, tol=1e-6, what="loss values")
 
+
+
+@pytest.mark.parametrize("M1,M2,C", [(3000, 5000, 32), (700, 900, 64), (4096, 4096, 128)])
+def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
+    """SyncBN phases (tde_bn_sums / tde_bn_fwd_from_sums / tde_bn_bwd_from_sums): two replicas holding
+    rows [0, M1) and [M1, M1 + M2) of one batch, with their sums added as the all-reduce would, reproduce
+    tde_bn_fwd_train / tde_bn_bwd on the whole batch -- statistics, moving averages, y, dz -- and their
+    local dbeta add up to the whole batch's."""
+    lib = L.load()
+    st = L.stream_ptr()
+    M = M1 + M2
+    z = dev(rnd(M, C, seed=31) * 2.0 + 0.3)
+    dy = dev(rnd(M, C, seed=32))
+    beta = dev(rnd(C, seed=33) * 0.2)
+    ws = torch.zeros(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
+    # whole batch
+    mm, mv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    sm = torch.empty(2, C, device="cuda")
+    y = torch.empty(M, C, device="cuda")
+    L.check(lib.tde_bn_fwd_train(M, C, L.ptr(z), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
+                                 L.ptr(sm[1]), L.ptr(y), C, 0, 1, L.ptr(ws), ws.numel() * 4, st))
+    dz = torch.empty(M, C, device="cuda")
+    db = torch.empty(C, device="cuda")
+    L.check(lib.tde_bn_bwd(M, C, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(dy), C, 0, L.ptr(dz),
+                           L.ptr(db), 0, 1, L.ptr(ws), ws.numel() * 4, st))
+    # two replicas
+    parts = [(0, M1), (M1, M2)]
+    sums = [torch.empty(2 * C, dtype=torch.float64, device="cuda") for _ in parts]
+    for (r0, m), s in zip(parts, sums):
+        L.check(lib.tde_bn_sums(m, C, L.ptr(z[r0:]), None, 0, 0, None, None, None, 0, 0, L.ptr(s), L.ptr(ws),
+                                ws.numel() * 4, st))
+    g = sums[0] + sums[1]                                        # the all-reduce
+    y2 = torch.empty(M, C, device="cuda")
+    sm2 = torch.empty(2, 2, C, device="cuda")
+    mm2, mv2 = torch.zeros(2, C, device="cuda"), torch.ones(2, C, device="cuda")
+    for k, (r0, m) in enumerate(parts):
+        L.check(lib.tde_bn_fwd_from_sums(m, C, M, L.ptr(z[r0:]), L.ptr(g), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm2[k]),
+                                         L.ptr(mv2[k]), L.ptr(sm2[k, 0]), L.ptr(sm2[k, 1]), L.ptr(y2[r0:]), C, 0, 1,
+                                         st))
+    for k in range(2):
+        close(sm2[k], sm, tol=1e-6, what="global statistics")
+        close(mm2[k], mm, tol=1e-6, what="moving mean")
+        close(mv2[k], mv, tol=1e-6, what="moving variance")
+    close(y2, y, what="y")
+    ls = [torch.empty(2 * C, dtype=torch.float64, device="cuda") for _ in parts]
+    for (r0, m), s in zip(parts, ls):
+        L.check(lib.tde_bn_sums(m, C, L.ptr(z[r0:]), L.ptr(dy[r0:]), C, 0, L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), 1,
+                                1, L.ptr(s), L.ptr(ws), ws.numel() * 4, st))
+    gb = ls[0] + ls[1]
+    dz2 = torch.empty(M, C, device="cuda")
+    db2 = torch.empty(2, C, device="cuda")
+    for k, (r0, m) in enumerate(parts):
+        L.check(lib.tde_bn_bwd_from_sums(m, C, M, L.ptr(z[r0:]), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta),
+                                         L.ptr(dy[r0:]), C, 0, L.ptr(gb), L.ptr(ls[k]), L.ptr(dz2[r0:]), L.ptr(db2[k]),
+                                         0, 1, L.ptr(ws), ws.numel() * 4, st))
+    close(dz2, dz, what="dz")
+    close(db2[0] + db2[1], db, tol=1e-6, what="dbeta")

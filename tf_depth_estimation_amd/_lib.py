@@ -97,6 +97,11 @@ _SIGS = {
                                  P, c_size_t, P]),
     "tde_bn_fwd_infer": (c_int, [c_int, c_int, P, P, c_float, P, P, P, c_int, c_int, c_int, P]),
     "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, c_size_t, P]),
+    "tde_bn_sums": (c_int, [c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P]),
+    "tde_bn_fwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, c_float, c_float, c_int, P, P, P, P, P,
+                                     c_int, c_int, c_int, P]),
+    "tde_bn_bwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int,
+                                     c_int, P, c_size_t, P]),
     "tde_resize_nearest_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_nearest_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_bilinear_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),

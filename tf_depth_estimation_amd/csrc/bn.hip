@@ -94,7 +94,7 @@ template <int MODE>
 __global__ void __launch_bounds__(1024) bn_finalize_kernel(int M, int C, int nparts, const double* part, float eps,
                                                            float decay, int bessel, float* mm, float* mv,
                                                            float* save_mean, float* save_invstd, float* dbeta,
-                                                           int acc, float* coef) {
+                                                           int acc, float* coef, double* sums = nullptr) {
   __shared__ double sh[2][1024];
   const int cl = threadIdx.x & 3, st = threadIdx.x >> 2;
   const int c = blockIdx.x * 4 + cl;
@@ -124,7 +124,10 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(int M, int C, int npa
   }
   if (threadIdx.x >= 4) return;
   const double s = sh[0][cl], s2 = sh[1][cl];
-  if (MODE == 0) {
+  if (MODE == 2) {   // raw per-channel sums (SyncBN: all-reduced by the caller, then *_from_sums)
+    sums[c] = s;
+    sums[C + c] = s2;
+  } else if (MODE == 0) {
     const double mean = s / M;
     double var = s2 / M - mean * mean;
     if (var < 0) var = 0;
@@ -200,6 +203,36 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
       }
       *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
     }
+  }
+}
+
+// SyncBN second phase: batch statistics from per-channel sums over ALL replicas (count Mt).
+// MODE 0: mean / invstd (+ moving averages) from (sum z, sum z^2).  MODE 1: coef = global (mean g,
+// mean g*xhat) from the all-reduced sums, dbeta from this replica's own sum g (the data-parallel gradient
+// average then divides the summed dbeta by the replica count, as for every other parameter).
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_from_sums_kernel(int C, double Mt, const double* gsum, const double* lsum,
+                                                           float eps, float decay, int bessel, float* mm, float* mv,
+                                                           float* save_mean, float* save_invstd, float* dbeta,
+                                                           int acc, float* coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double s = gsum[c], s2 = gsum[C + c];
+  if (MODE == 0) {
+    const double mean = s / Mt;
+    double var = s2 / Mt - mean * mean;
+    if (var < 0) var = 0;
+    save_mean[c] = (float)mean;
+    save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (mm) {
+      const double vu = (bessel && Mt > 1) ? var * Mt / (Mt - 1) : var;
+      mm[c] -= (mm[c] - (float)mean) * (1.f - decay);
+      mv[c] -= (mv[c] - (float)vu) * (1.f - decay);
+    }
+  } else {
+    if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)lsum[c] : (float)lsum[c];
+    coef[c] = (float)(s / Mt);
+    coef[C + c] = (float)(s2 / Mt);
   }
 }
 
@@ -449,6 +482,61 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
                      save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
   hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, pp.chunks, part, 0.f,
                      0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
+  const int rpb = apply_rows_per_block(M, C);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
+                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb);
+  return tde_launch_status();
+}
+
+
+int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, int dy_coff, const float* save_mean,
+                const float* save_invstd, const float* beta, int relu, int mode, double* sums, void* ws,
+                size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && sums && (mode == 0 || mode == 1));
+  TDE_CHECK_ARG(tde_aligned16(z) && (mode == 0 || (dy && save_mean && save_invstd && beta && tde_aligned16(dy) &&
+                                                   dy_cstride % 4 == 0 && dy_coff % 4 == 0)));
+  if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const BnChunks pp = bn_chunk_plan(M, C, 1);
+  double* part = reinterpret_cast<double*>(tde_ws_body(ws));
+  if (mode == 0)
+    hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0,
+                       nullptr, nullptr, nullptr, 0, pp.rows_per_chunk, part);
+  else
+    hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride,
+                       dy_coff, save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
+  hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, pp.chunks, part, 0.f,
+                     0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, sums);
+  return tde_launch_status();
+}
+
+int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const double* sums, const float* beta, float eps,
+                         float decay, int bessel, float* moving_mean, float* moving_var, float* save_mean,
+                         float* save_invstd, float* y, int y_cstride, int y_coff, int relu, void* stream) {
+  TDE_CHECK_ARG(M > 0 && M_total >= M && C > 0 && C % 4 == 0 && z && sums && beta && save_mean && save_invstd && y);
+  TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) &&
+                tde_aligned16(y) && (moving_mean == nullptr) == (moving_var == nullptr));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(bn_from_sums_kernel<0>, dim3((C + 255) / 256), dim3(256), 0, st, C, (double)M_total, sums,
+                     nullptr, eps, decay, bessel, moving_mean, moving_var, save_mean, save_invstd, nullptr, 0, nullptr);
+  const int rpb = apply_rows_per_block(M, C);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, save_mean, save_invstd,
+                     beta, relu, y, y_cstride, y_coff, rpb);
+  return tde_launch_status();
+}
+
+int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean, const float* save_invstd,
+                         const float* beta, const float* dy, int dy_cstride, int dy_coff, const double* global_sums,
+                         const double* local_sums, float* dz, float* dbeta, int accumulate_dbeta, int relu, void* ws,
+                         size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(M > 0 && M_total >= M && C > 0 && C % 4 == 0 && z && save_mean && save_invstd && beta && dy && dz &&
+                global_sums && local_sums);
+  TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
+  if (ws_bytes < (size_t)2 * C * sizeof(float) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* coef = reinterpret_cast<float*>(tde_ws_body(ws));
+  hipLaunchKernelGGL(bn_from_sums_kernel<1>, dim3((C + 255) / 256), dim3(256), 0, st, C, (double)M_total, global_sums,
+                     local_sums, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                      dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb);

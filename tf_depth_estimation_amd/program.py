@@ -242,6 +242,17 @@ class NetProgram:
         self._ws = {}
         self._sizes = {}
         self.timer = None
+        # SyncBN: bn_sync(t) all-reduces (sums) a float64 device tensor in place across
+        # bn_world data-parallel replicas; None = BatchNorm over the local batch (the default)
+        self.bn_sync, self.bn_world = None, 1
+        self._bn_sums = {}
+
+    def _sums(self, i, K, which):
+        key = (i, which)
+        t = self._bn_sums.get(key)
+        if t is None:
+            t = self._bn_sums[key] = torch.empty(2 * K, dtype=torch.float64, device="cuda")
+        return t
 
     def _span(self, family, flops=0.0, nbytes=0.0):
         return NO_SPAN if self.timer is None else self.timer.span(family, flops, nbytes)
@@ -302,7 +313,19 @@ class NetProgram:
                 beta = self.P(f"{op.layer}/BatchNorm/beta")
                 sm = run.stats[i]
                 mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
-                if is_training and self.timer is None:
+                if is_training and self.bn_sync is not None:
+                    # SyncBN: conv, local (sum z, sum z^2), all-reduce, BN over all replicas' rows
+                    fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
+                    _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
+                    sums = self._sums(i, op.K, 0)
+                    _lib.check(lib.tde_bn_sums(M, op.K, ptr(z), None, 0, 0, None, None, None, 0, 0, ptr(sums), ptr(ws),
+                                               wsb, st), op.layer + " bn sums")
+                    self.bn_sync(sums)
+                    _lib.check(lib.tde_bn_fwd_from_sums(M, op.K, M * self.bn_world, ptr(z), ptr(sums), ptr(beta), 1e-3,
+                                                        op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
+                                                        ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st),
+                               op.layer + " syncbn")
+                elif is_training and self.timer is None:
                     # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
                     # consumes the conv's split-K partials directly
                     bn = _lib.BnTrain(ptr(beta), 1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
@@ -393,12 +416,28 @@ class NetProgram:
                 d = op.desc(N)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
-                with self._span("bn_bwd"):
-                    _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
-                                              ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
-                                              op.dst.buf.cs, op.dst.coff, ptr(dz),
-                                              ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws), wsb, st),
-                               op.layer + " bn_bwd")
+                if self.bn_sync is not None:
+                    # SyncBN backward: local (sum g, sum g*xhat) -> all-reduced copy -> dz from the global means,
+                    # dbeta from the local sum (the gradient all-reduce averages it like every parameter)
+                    ls, gs = self._sums(i, op.K, 1), self._sums(i, op.K, 2)
+                    beta = self.P(f"{op.layer}/BatchNorm/beta")
+                    _lib.check(lib.tde_bn_sums(M, op.K, ptr(run.z[i]), run.vptr(op.dst, True), op.dst.buf.cs,
+                                               op.dst.coff, ptr(sm[0]), ptr(sm[1]), ptr(beta), 1, 1, ptr(ls), ptr(ws),
+                                               wsb, st), op.layer + " bn sums")
+                    gs.copy_(ls)
+                    self.bn_sync(gs)
+                    _lib.check(lib.tde_bn_bwd_from_sums(M, op.K, M * self.bn_world, ptr(run.z[i]), ptr(sm[0]),
+                                                        ptr(sm[1]), ptr(beta), run.vptr(op.dst, True), op.dst.buf.cs,
+                                                        op.dst.coff, ptr(gs), ptr(ls), ptr(dz),
+                                                        ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws),
+                                                        wsb, st), op.layer + " syncbn bwd")
+                else:
+                    with self._span("bn_bwd"):
+                        _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
+                                                  ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
+                                                  op.dst.buf.cs, op.dst.coff, ptr(dz),
+                                                  ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws), wsb,
+                                                  st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
                 if src_needs:

@@ -70,6 +70,19 @@ class Trainer:
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
         return self.grad_sync
 
+    def enable_sync_bn(self, world, group=None):
+        """SyncBN: every BatchNorm of every network normalises over the rows of all `world`
+        replicas (one RCCL all-reduce of fp64 per-channel sums per BN layer and direction) -- the
+        reference's semantics at the global batch.  RCCL is not captured, so the step runs eagerly."""
+        import torch.distributed as dist
+
+        def sync(t):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+        for p in self.programs():
+            p.bn_sync, p.bn_world = sync, world
+        self.sync_bn = True
+
     def programs(self):
         return [p for p in (getattr(self, "prog", None), getattr(self, "single", None), getattr(self, "pair", None))
                 if p is not None]
@@ -90,6 +103,8 @@ class Trainer:
 
     def capture(self, warmup=2):
         """Warm up on a side stream (allocates every lazily created buffer), then record."""
+        if getattr(self, "sync_bn", False):
+            raise NotImplementedError("SyncBN all-reduces inside the forward/backward: run step() eagerly")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
