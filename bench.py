@@ -246,6 +246,8 @@ def main():
                          "precision, or the fp32-accurate 3-way bf16 split (LDS-staged / register-split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--adam-overlap", action="store_true",
+                    help="N = 1: run each gradient bucket's Adam on a side stream as soon as backward finalises it")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
                          "runs eagerly, RCCL is not captured)")
@@ -276,6 +278,8 @@ def main():
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     if args.sync_bn:
         tr.enable_sync_bn(world)
+    if args.adam_overlap and world == 1:
+        tr.enable_adam_overlap()
     progs = tr.programs()
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)

@@ -28,11 +28,12 @@ from . import _lib
 
 
 class Bucket:
-    __slots__ = ("chunk", "lo", "hi", "names", "launched")
+    __slots__ = ("chunk", "lo", "hi", "names", "launched", "opt")
 
     def __init__(self, chunk, lo, hi, names):
         self.chunk, self.lo, self.hi, self.names = chunk, lo, hi, list(names)
         self.launched = False
+        self.opt = None     # the chunk's optimizer when the bucket is an Adam-overlap slice (train.py)
 
     def view(self):
         return self.chunk.grad[self.lo:self.hi]

@@ -28,11 +28,88 @@ class Adam:
         self.t = torch.zeros(1, device="cuda", dtype=torch.float32)
 
     def step(self):
+        self.begin()
+        self.update(0, self.chunk.numel)
+
+    def begin(self):
+        """Advance the device step counter (TF's beta1_power / beta2_power)."""
+        lib, st = _lib.load(), _lib.stream_ptr()
+        _lib.check(lib.tde_adam_step_begin(ptr(self.t), st), "adam step")
+
+    def update(self, lo, hi):
+        """Adam on flat elements [lo, hi) (multiples of 4: parameters start 16-byte aligned)."""
+        import ctypes
         lib, st = _lib.load(), _lib.stream_ptr()
         c = self.chunk
-        _lib.check(lib.tde_adam_step_begin(ptr(self.t), st), "adam step")
-        _lib.check(lib.tde_adam_update(c.numel, ptr(c.flat), ptr(c.grad), ptr(c.adam_m), ptr(c.adam_v), ptr(self.t),
+
+        def at(t):
+            return ctypes.c_void_p(t.data_ptr() + 4 * lo)
+        _lib.check(lib.tde_adam_update(hi - lo, at(c.flat), at(c.grad), at(c.adam_m), at(c.adam_v), ptr(self.t),
                                        self.lr, self.b1, self.b2, self.eps, st), "adam")
+
+
+class AdamOverlap:
+    """Single-GPU overlap of the optimizer with backward: the gradient buffers are cut into buckets
+    (ddp.make_buckets: contiguous slices, last parameters first) and each bucket's Adam runs on a side
+    stream as soon as backward has written its last contribution of the step, so the update of the
+    decoder's and the deep encoder's large layers hides under the remaining backward convs.  Pure
+    kernel work: under capture the side stream becomes a graph branch (fork at each bucket's event,
+    one join before the step ends)."""
+
+    def __init__(self, opts, bucket_mb=16.0, uses=None):
+        from .ddp import make_buckets
+        self.opts = list(opts)
+        self.buckets = []
+        self.by_param = {}
+        for o in self.opts:
+            for b in make_buckets(o.chunk, int(bucket_mb * 2 ** 20)):
+                b.opt = o
+                self.buckets.append(b)
+                for n in b.names:
+                    self.by_param[(id(o.chunk), n)] = b
+        self.uses = {id(o.chunk): (uses or {}).get(id(o.chunk), 1) for o in self.opts}
+        self.side = torch.cuda.Stream()
+
+    def begin_step(self):
+        self.count = {k: 0 for k in self.by_param}
+        self.left = {id(b): len(b.names) for b in self.buckets}
+        self.done = set()
+        for o in self.opts:
+            o.begin()
+
+    def hook(self, chunk):
+        cid = id(chunk)
+
+        def on_grads(names):
+            ready = []
+            for n in names:
+                key = (cid, n)
+                b = self.by_param.get(key)
+                if b is None:
+                    continue
+                self.count[key] += 1
+                if self.count[key] == self.uses[cid]:
+                    self.left[id(b)] -= 1
+                    if self.left[id(b)] == 0:
+                        ready.append(b)
+            if ready:
+                self.launch(ready)
+        return on_grads
+
+    def launch(self, buckets):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            for b in buckets:
+                b.opt.update(b.lo, b.hi)
+                self.done.add(id(b))
+
+    def finish(self):
+        rest = [b for b in self.buckets if id(b) not in self.done]
+        if rest:
+            self.launch(rest)
+        torch.cuda.current_stream().wait_stream(self.side)
 
 
 class AllReduceGrads:
@@ -64,8 +141,31 @@ class Trainer:
     grad_sync = None
     BACKWARD_USES = 1        # backward calls per chunk per step (shared-variable nets call it twice)
 
+    adam_ov = None
+
+    def enable_adam_overlap(self, bucket_mb=16.0):
+        """Run each gradient bucket's Adam on a side stream as soon as backward finalises it (single GPU;
+        with a data-parallel exchange the update must wait for the all-reduce)."""
+        if self.grad_sync is not None:
+            raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
+        opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
+        self.adam_ov = AdamOverlap(opts, bucket_mb, {id(c): self.BACKWARD_USES for c in self.chunks})
+        return self.adam_ov
+
+    def _begin(self):
+        if self.adam_ov is not None:
+            self.adam_ov.begin_step()
+
+    def _update(self):
+        if self.adam_ov is not None:
+            self.adam_ov.finish()
+        else:
+            self.phase_update()
+
     def enable_ddp(self, world, bucket_mb=32.0, group=None):
         from .ddp import GradSync
+        if self.adam_ov is not None:
+            raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
         return self.grad_sync
@@ -89,6 +189,8 @@ class Trainer:
 
     def hook(self, chunk):
         """on_grads callback for NetProgram.backward (None without an overlapped exchange)."""
+        if self.adam_ov is not None:
+            return self.adam_ov.hook(chunk)
         gs = self.grad_sync
         return gs.hook(chunk) if gs is not None and hasattr(gs, "hook") else None
 
@@ -96,10 +198,11 @@ class Trainer:
         gs = self.grad_sync
         if gs is not None and hasattr(gs, "begin_step"):
             gs.begin_step()
+        self._begin()
         self.phase_compute()
         if gs is not None:
             gs()
-        self.phase_update()
+        self._update()
 
     def capture(self, warmup=2):
         """Warm up on a side stream (allocates every lazily created buffer), then record."""
@@ -115,8 +218,9 @@ class Trainer:
         if gs is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                self._begin()
                 self.phase_compute()
-                self.phase_update()
+                self._update()
             self.graphs = [g]
             return self.graphs
         if not hasattr(gs, "begin_step"):       # plain exchange after backward
