@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 2
+#define TDE_ABI_VERSION 3
 
 typedef enum {
   TDE_OK = 0,
@@ -132,6 +132,18 @@ int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float*
 /* deconv forward + BN + ReLU: z_big dense [N*H*W][C] (x_cstride == C, x_coff == 0); workspace op 3. */
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
                         const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream);
+
+/* Inference path with batch norm folded into the conv (batch_prediction.py:41-44,
+ * batch_prediction_optflow.py: disp_net(x, is_training=False), then sess.run per image; replaces the
+ * conv -> FusedBatchNorm(is_training=False) -> Relu triple of slim.conv2d / conv2d_transpose,
+ * nets_optflow_depth.py:82-87).  w / bias from tde_bn_fold; y = relu?(conv(x, w) + bias[col]) written
+ * straight into the output channel view (conv: d's y view; deconv: d's x view, the virtual conv's
+ * input).  One launch per layer (plus the split-K reduce when planned), no pre-BN tensor. */
+int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias,
+                            int relu, float* y, void* ws, size_t ws_bytes, void* stream);
+int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, const float* w,
+                              const float* bias, int relu, float* y_big, void* ws, size_t ws_bytes,
+                              void* stream);
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w,
                           float* dx_small, int accumulate, void* ws, size_t ws_bytes, void* stream);
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small,
@@ -164,6 +176,12 @@ int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps,
 int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps,
                      const float* moving_mean, const float* moving_var, float* y, int y_cstride,
                      int y_coff, int relu, void* stream);
+/* Fold inference BN (beta only, scale=False; eps) into the preceding conv's weights:
+ * w_out = w * rsqrt(mv + eps)[k], bias_out[k] = beta[k] - mm[k] * rsqrt(mv + eps)[k] (fp64 math).
+ * layout 0: conv [taps][cin][K]; layout 1: conv2d_transpose [taps][K][cin].  w_out != w. */
+int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const float* moving_mean,
+                const float* moving_var, const float* beta, float eps, float* w_out, float* bias_out,
+                void* stream);
 /* dz = d(BN+ReLU)/dz given dy (view); dbeta = sum(dy * relu'); accumulate_dbeta adds to dbeta. */
 int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd,
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,

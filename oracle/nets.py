@@ -183,12 +183,12 @@ def depth_net(P, tgt_image, is_training=True, scope="depth_cam_net", levels=4, d
     return disps, pose_final, masks
 
 
-def disp_net_depthflow(P, tgt_image, is_training=True, scope="depth_net"):
+def disp_net_depthflow(P, tgt_image, is_training=True, scope="depth_net", decay=0.999):
     """nets_depth.disp_net (nets_depth.py:76-199): shared encoder, depth decoder
     (sigmoid*10+0.001) and flow decoder (2-ch linear), 8 outputs; the flow decoder's icnv6 layer
     keeps the reference's scope name `icnv6_opt_opt` (:159)."""
     H, W = tgt_image.shape[1], tgt_image.shape[2]
-    c = _Ctx(P, scope, is_training, 0.999, True)
+    c = _Ctx(P, scope, is_training, decay, True)
     feats = _encoder(c, tgt_image)
     cnv7 = c.conv(feats[5], 512, 3, 2, "cnv7")
     cnv7b = c.conv(cnv7, 512, 3, 1, "cnv7b")

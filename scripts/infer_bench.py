@@ -1,0 +1,63 @@
+"""Inference-path measurement: batch_prediction.py's disp_net(is_training=False)
+per-image latency at 224x224 batch 1, plus batched throughput, for the folded-BN graph predictor and the
+unfolded (conv -> BN(moving) -> ReLU) path, graph and eager.  Prints one JSON line.
+
+    python scripts/infer_bench.py [--iters 200] [--warmup 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from tf_depth_estimation_amd import _api, _lib, batch_prediction, variables  # noqa: E402
+from tf_depth_estimation_amd.program import conv_flops  # noqa: E402
+
+
+def timed(pred, x, iters, warmup):
+    for _ in range(warmup):
+        pred(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        pred(x)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def flops(prog, N):
+    from tf_depth_estimation_amd.program import ConvBN, Head
+    return sum(conv_flops(op, N) for op in prog.spec.ops if isinstance(op, (ConvBN, Head)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    args = ap.parse_args()
+    lib = _lib.load()
+    _lib.check(lib.tde_set_conv_math(3))
+    rows = []
+    for net, H, W, B in [("disp_net", 224, 224, 1), ("disp_net", 192, 256, 8), ("disp_net", 192, 256, 64)]:
+        for fold, graph in [(True, True), (False, True), (True, False)]:
+            variables.get_store().reset(seed=1)
+            _api.clear_programs()
+            pred = batch_prediction.Predictor(net, H, W, batch=B, fold_bn=fold, graph=graph)
+            x = torch.rand((B, H, W, 3), device="cuda") - 0.5
+            iters = args.iters if B == 1 else max(20, args.iters // 4)
+            s = timed(pred, x, iters, args.warmup)
+            f = flops(pred.prog, B)
+            rows.append({"net": net, "HxW": f"{H}x{W}", "batch": B, "fold_bn": fold, "hip_graph": graph,
+                         "ms_per_call": round(s * 1e3, 4), "images_per_s": round(B / s, 1),
+                         "conv_tflops": round(f / s / 1e12, 2)})
+            print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    print(json.dumps({"metric": "disp_net inference (batch_prediction.py path)", "math": "bf16x6r",
+                      "data": "synthetic U(-0.5,0.5) images, Glorot weights", "rows": rows}))
+
+
+if __name__ == "__main__":
+    main()

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
 CONV_MATH = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "bf16x6r": 3}
@@ -80,6 +80,9 @@ _SIGS = {
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
     "tde_conv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
     "tde_deconv2d_fwd_bn": (c_int, [P, P, P, P, P, P, c_size_t, P]),
+    "tde_conv2d_fwd_bias_act": (c_int, [P, P, P, P, c_int, P, P, c_size_t, P]),
+    "tde_deconv2d_fwd_bias_act": (c_int, [P, P, P, P, c_int, P, P, c_size_t, P]),
+    "tde_bn_fold": (c_int, [c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P, P]),
     "tde_conv2d_bwd_workspace_size": (c_size_t, [P]),
     "tde_deconv2d_bwd_workspace_size": (c_size_t, [P]),
     "tde_conv2d_bwd": (c_int, [P, P, P, P, P, c_int, P, c_int, P, c_size_t, P]),

@@ -373,6 +373,21 @@ __global__ void __launch_bounds__(256) bn_infer_kernel(int M, int C, const float
   }
 }
 
+// Inference-mode batch norm folded into the preceding conv (batch_prediction.py:41-44 runs disp_net with
+// is_training=False): y = (conv(x, w) - mm) * rsqrt(mv + eps) + beta = conv(x, w * s) + (beta - mm * s),
+// s = rsqrt(mv + eps) per output channel k.  layout 0: conv weights [taps][cin][K] (k = idx % K);
+// layout 1: conv2d_transpose weights [taps][K][cin] (k = (idx / cin) % K).  fp64 scale and products.
+__global__ void __launch_bounds__(256) bn_fold_kernel(long total, int cin, int K, int layout, const float* w,
+                                                      const float* mm, const float* mv, const float* beta,
+                                                      float eps, float* w_out, float* bias_out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int k = layout == 0 ? (int)(i % K) : (int)((i / cin) % K);
+    const double s = 1.0 / sqrt((double)mv[k] + (double)eps);
+    w_out[i] = (float)((double)w[i] * s);
+    if (i < K) bias_out[i] = (float)((double)beta[i] - (double)mm[i] * (1.0 / sqrt((double)mv[i] + (double)eps)));
+  }
+}
+
 int ew_grid(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -460,6 +475,16 @@ int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps,
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(bn_infer_kernel, dim3(ew_grid((long)M * C / 4)), dim3(256), 0, st, M, C, z, moving_mean,
                      moving_var, eps, beta, relu, y, y_cstride, y_coff);
+  return tde_launch_status();
+}
+
+int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const float* moving_mean,
+                const float* moving_var, const float* beta, float eps, float* w_out, float* bias_out, void* stream) {
+  TDE_CHECK_ARG(taps > 0 && cin > 0 && K > 0 && (layout == 0 || layout == 1) && w && moving_mean && moving_var &&
+                beta && w_out && bias_out && w != w_out);
+  const long total = (long)taps * cin * K;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, cin,
+                     K, layout, w, moving_mean, moving_var, beta, eps, w_out, bias_out);
   return tde_launch_status();
 }
 

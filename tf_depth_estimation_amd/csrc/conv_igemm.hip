@@ -40,7 +40,16 @@ struct ConvArgs {
   FDiv fC, fK, fKW, fOW, fOHW;
   double* bnp;  // BN statistics partials [row tile][2][Nn] from the epilogue (FWD/DGRAD, splits == 1)
   int bn_gx;    // row tiles per DGRAD class (grid x)
+  // inference epilogue (FWD / DGRAD outputs only; accumulate == 0): v = conv + bias[col], then ReLU
+  // (BN folded into the weights, tde_conv2d_fwd_bias_act); bias null and relu 0 = plain conv
+  const float* bias; int relu;
 };
+
+// The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
+__device__ __forceinline__ float bias_act(float v, const float* bias, int col, int relu) {
+  if (bias) v += bias[col];
+  return (relu && v < 0.f) ? 0.f : v;
+}
 
 // Per-class geometry of the DGRAD sub-pixel decomposition.
 struct DgClass {
@@ -612,6 +621,19 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + n];
         }
   }
+  if constexpr (MODE != MODE_WGRAD) {
+    if (direct && (p.bias || p.relu)) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int n = n0 + wcol0 + b * 16 + r16;
+        const int nb = n < Nn ? n : 0;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][r] = bias_act(acc[a][b][r], p.bias, nb, p.relu);
+      }
+    }
+  }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -780,7 +802,7 @@ __global__ void __launch_bounds__(NT) skinny_kernel(const ConvArgs p) {
     long off;
     if (direct) off = (long)rr * (MODE == MODE_FWD ? p.ycs : p.xcs) + (MODE == MODE_FWD ? p.yco : p.xco) + col;
     else off = ((long)zsplit * M + rr) * Nn + col;
-    base[off] = (direct && p.accumulate) ? base[off] + v : v;
+    base[off] = direct ? (p.accumulate ? base[off] + v : bias_act(v, p.bias, col, p.relu)) : v;
   }
 }
 
@@ -831,6 +853,12 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
       dst = p.dw + (long)(tap * p.wcin + c) * p.K + col;
     }
     if (p.accumulate) s += ld4(dst);
+    if constexpr (MODE != MODE_WGRAD) {
+      if (p.bias || p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] = bias_act(s[j], p.bias, col + j, p.relu);
+      }
+    }
     *reinterpret_cast<f4*>(dst) = s;
   }
 }
@@ -1200,7 +1228,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     hipStream_t st = static_cast<hipStream_t>(stream);
     const float* in = MODE == MODE_FWD ? a.x : a.dy;
     float* z = MODE == MODE_FWD ? a.y : a.dx;
-    if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, part, st);
+    if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, part, st, a.bias, a.relu);
     if (bn) {
       const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
                     bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu};
@@ -1398,6 +1426,24 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream) {
   return tde_conv2d_bwd_data(d, x_small, w, y_big, accumulate, ws, ws_bytes, stream);
+}
+
+// Folded-BN inference conv: y = relu?(conv(x, w_folded) + bias) into the y view of d.
+int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, int relu,
+                            float* y, void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y) && (relu == 0 || relu == 1));
+  ConvArgs a = make_args(*d);
+  a.x = x; a.w = w; a.y = y; a.bias = bias; a.relu = relu;
+  return run<MODE_FWD>(d, a, 0, nullptr, ws, ws_bytes, stream);
+}
+
+int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, const float* w, const float* bias,
+                              int relu, float* y_big, void* ws, size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big) &&
+                (relu == 0 || relu == 1) && d->w_cin == d->C);
+  ConvArgs a = make_args(*d);
+  a.dy = x_small; a.w = w; a.dx = y_big; a.bias = bias; a.relu = relu;
+  return run<MODE_DGRAD>(d, a, 0, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,

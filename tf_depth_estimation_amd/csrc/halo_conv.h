@@ -27,6 +27,8 @@ struct HaloPlan {
 bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp);
 
 // Weight split (one launch) + conv (one launch).  ws: >= hp.wbytes of 16-byte aligned workspace;
-// bnp: fp64 BN partials [hp.nparts][2][Ncols] or null.
+// bnp: fp64 BN partials [hp.nparts][2][Ncols] or null.  bias / relu: folded-BN inference epilogue
+// (out = relu?(conv + bias[col]); accumulate 0), null / 0 for a plain conv.
 void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
-                 int accumulate, void* ws, double* bnp, hipStream_t st);
+                 int accumulate, void* ws, double* bnp, hipStream_t st, const float* bias = nullptr,
+                 int relu = 0);

@@ -46,6 +46,8 @@ struct HaloArgs {
   float* out;
   const u16* wp;
   double* bnp;
+  const float* bias;   // folded-BN inference epilogue (accumulate == 0); null / 0: plain conv
+  int relu;
 };
 
 // Split weights, one contiguous B tile per (k-step g, column tile ct):
@@ -288,6 +290,20 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b][r] += old[a][r][b];
   }
+  if (p.bias || p.relu) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = col0 + b * 16 + r16;
+      const float bv = (p.bias && col < p.Ncols) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[a][b][r] + bv;
+          acc[a][b][r] = (p.relu && v < 0.f) ? 0.f : v;
+        }
+    }
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -404,7 +420,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
 }
 
 void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
-                 int accumulate, void* ws, double* bnp, hipStream_t st) {
+                 int accumulate, void* ws, double* bnp, hipStream_t st, const float* bias, int relu) {
   u16* wp = static_cast<u16*>(ws);
   const long total = (long)hp.nch * hp.steps * hp.NcolsP * LDB;
   long blocks = (total + 255) / 256;
@@ -418,7 +434,7 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
   a.Cv = hp.Cv; a.ics = hp.ics; a.ico = hp.ico; a.Ncols = hp.Ncols; a.ocs = hp.ocs; a.oco = hp.oco;
   a.ncolt = hp.ncolt; a.NcolsP = hp.NcolsP; a.accumulate = accumulate;
   a.fCC = make_fdiv(hp.CC); a.fKW = make_fdiv(hp.KW); a.fC4 = make_fdiv(hp.CC / 4); a.fHWd = make_fdiv(hp.HWd);
-  a.in = in; a.out = out; a.wp = wp; a.bnp = bnp;
+  a.in = in; a.out = out; a.wp = wp; a.bnp = bnp; a.bias = bias; a.relu = relu;
   const int key = hp.NW * 10 + hp.TN;
   switch (key) {
     case 81: launch_t<8, 1>(hp, a, st); break;

@@ -104,6 +104,16 @@ class ConvBN(Op):
     def zshape(self, N):
         return (N, self.dst.H, self.dst.W, self.K)
 
+    def folded_desc(self, N):
+        """desc() with the output going straight into the consumer's channel view (folded-BN
+        inference: no pre-BN z)."""
+        d = self.desc(N)
+        if self.deconv:
+            d.x_cstride, d.x_coff = self.dst.buf.cs, self.dst.coff
+        else:
+            d.y_cstride, d.y_coff = self.dst.buf.cs, self.dst.coff
+        return d
+
 
 class Head(Op):
     """slim.conv2d(normalizer_fn=None) head with bias: act 1 -> scale*sigmoid(.)+offset, 0 -> linear."""
@@ -246,6 +256,7 @@ class NetProgram:
         # bn_world data-parallel replicas; None = BatchNorm over the local batch (the default)
         self.bn_sync, self.bn_world = None, 1
         self._bn_sums = {}
+        self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
 
     def _sums(self, i, K, which):
         key = (i, which)
@@ -264,6 +275,29 @@ class NetProgram:
     def G(self, name):
         return self.chunk.grad_view(f"{self.prefix}/{name}")
 
+    def fold_bn(self):
+        """Inference weights: each conv/deconv's moving statistics folded into its weights and a bias
+        (tde_bn_fold; batch_prediction.py:41-44 runs disp_net with is_training=False).  A snapshot of the
+        current variables: call again after a checkpoint restore or further training."""
+        lib = _lib.load()
+        st = _lib.stream_ptr()
+        folded = {}
+        for op in self.spec.ops:
+            if not (isinstance(op, ConvBN) and op.bn):
+                continue
+            w = self.P(f"{op.layer}/weights")
+            beta = self.P(f"{op.layer}/BatchNorm/beta")
+            mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
+            kh, kw, a, b = w.shape
+            layout, cin = (1, b) if op.deconv else (0, a)
+            wf = torch.empty_like(w)
+            bf = torch.empty(op.K, dtype=torch.float32, device=w.device)
+            _lib.check(lib.tde_bn_fold(kh * kw, cin, op.K, layout, ptr(w), ptr(mm), ptr(mv), ptr(beta), 1e-3,
+                                       ptr(wf), ptr(bf), st), op.layer + " fold")
+            folded[op.layer] = (wf, bf)
+        self._folded = folded
+        return folded
+
     def _scratch(self, N):
         if N not in self._sizes:
             lib = _lib.load()
@@ -276,6 +310,7 @@ class NetProgram:
                         ws = max(ws, q(ctypes_ref(d), o))
                     qb = lib.tde_deconv2d_bwd_workspace_size if op.deconv else lib.tde_conv2d_bwd_workspace_size
                     ws = max(ws, qb(ctypes_ref(d)))
+                    ws = max(ws, q(ctypes_ref(op.folded_desc(N)), 1 if op.deconv else 0))
                     M = N * op.dst.H * op.dst.W
                     ws = max(ws, lib.tde_bn_workspace_size(M, op.K))
                     dz = max(dz, M * op.K)
@@ -287,8 +322,11 @@ class NetProgram:
         return w.get(ws, dz, "cuda")
 
     # ---------------------------------------------------------------- forward
-    def forward(self, run, x, is_training=True):
-        """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors."""
+    def forward(self, run, x, is_training=True, fold_bn=False):
+        """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors.  fold_bn (inference only):
+        run each conv/deconv + BN + ReLU as ONE bias+ReLU conv on the weights of fold_bn()."""
+        if fold_bn and (is_training or self._folded is None):
+            raise ValueError("fold_bn needs is_training=False and weights folded by fold_bn()")
         N = run.N
         lib = _lib.load()
         st = _lib.stream_ptr()
@@ -313,7 +351,14 @@ class NetProgram:
                 beta = self.P(f"{op.layer}/BatchNorm/beta")
                 sm = run.stats[i]
                 mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
-                if is_training and self.bn_sync is not None:
+                if fold_bn:
+                    wf, bf = self._folded[op.layer]
+                    fd = op.folded_desc(N)
+                    fn = lib.tde_deconv2d_fwd_bias_act if op.deconv else lib.tde_conv2d_fwd_bias_act
+                    with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
+                        _lib.check(fn(ctypes_ref(fd), run.vptr(op.src), ptr(wf), ptr(bf), 1, run.vptr(op.dst), ptr(ws),
+                                      wsb, st), op.layer)
+                elif is_training and self.bn_sync is not None:
                     # SyncBN: conv, local (sum z, sum z^2), all-reduce, BN over all replicas' rows
                     fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
                     _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
