@@ -236,6 +236,16 @@ int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int co
                      void* stream);
 /* mean|nf(label - pred)| (train_depth_only.py:183-184; replace_nonfinite when nonfinite=1,
  * train_depth_then_cam_lr.py:241-243).  label is dense [N,H,W,1]; pred is a 1-channel view. */
+/* DeMoN scale-invariant-gradient loss of compute_loss_single_depth (my_losses.py:78-82, used by
+ * split_training*.py:117): sig = lmbspecialops.scale_invariant_gradient per delta d (host arrays deltas /
+ * weights, <= 8): w_d (f(p+d) - f(p)) / (|f(p+d)| + |f(p)| + sig_epsilon) along x and y (0 where p+d
+ * leaves the image), channels concatenated (depthmotionnet.v2.losses.scale_invariant_gradient); then
+ * pointwise_l2_loss(sig(pred), sig(label), epsilon) = mean_p sqrt(sum_c nf(diff_c)^2 + epsilon), label
+ * under stop_gradient.  label dense [N,H,W,1] (NaN holes allowed); pred a 1-channel view.
+ * lmbspecialops / DeMoN are not vendored in the reference: restated, parity unpinned. */
+int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int coff, const float* label,
+                    int ndeltas, const int* deltas, const float* weights, float sig_epsilon, float epsilon,
+                    float weight, double* loss, float* grad, int g_cstride, int g_coff, void* stream);
 int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, const float* label,
                 int nonfinite, float weight, double* loss, float* grad, int g_cstride, int g_coff,
                 void* stream);

@@ -6,6 +6,10 @@
   * `loss_depth_then_cam_lr`   train_depth_then_cam_lr.py:211-355     (config 4)
   * `loss_refine`              refine_depth.py:185-215                (config 5, scale_factor = 1)
   * `adam_tf`                  tf.train.AdamOptimizer (train_depth_then_cam_lr.py:413-417)
+  * `scale_invariant_gradient`, `pointwise_l2_loss`, `depth_sig_loss`   my_losses.py:78-82 (DeMoN sig
+    loss of compute_loss_single_depth, split_training*.py:117).  lmbspecialops / depthmotionnet are
+    NOT vendored in the reference (Demon_Data_loader.py:9-11): restated from their published
+    definitions (DeMoN, Ummenhofer et al. 2017, eq. 3; depthmotionnet/v2/losses.py), parity unpinned.
 Canonical interpretations of the broken scripts: SURVEY.md Appendix C.
 """
 import numpy as np
@@ -29,6 +33,38 @@ def compute_smooth_loss(pred):
     dx2, dxdy = grad(dx)
     dydx, dy2 = grad(dy)
     return dx2.abs().mean() + dxdy.abs().mean() + dydx.abs().mean() + dy2.abs().mean()
+
+
+def scale_invariant_gradient(f, deltas, weights, epsilon):
+    """f: [N,H,W,1] -> [N,H,W,2*len(deltas)]: per delta d (weight w) the x and y components
+    w (f(p+d) - f(p)) / (|f(p+d)| + |f(p)| + epsilon), 0 where p+d leaves the image (lmbspecialops
+    ScaleInvariantGradient per delta, concatenated along channels as depthmotionnet.v2.losses does)."""
+    f = f[..., 0]
+    out = []
+    for d, w in zip(deltas, weights):
+        gx = torch.zeros_like(f)
+        gy = torch.zeros_like(f)
+        if d < f.shape[2]:
+            a, b = f[:, :, :-d], f[:, :, d:]
+            gx = torch.cat([w * (b - a) / (b.abs() + a.abs() + epsilon), gx[:, :, f.shape[2] - d:]], dim=2)
+        if d < f.shape[1]:
+            a, b = f[:, :-d], f[:, d:]
+            gy = torch.cat([w * (b - a) / (b.abs() + a.abs() + epsilon), gy[:, f.shape[1] - d:]], dim=1)
+        out += [gx, gy]
+    return torch.stack(out, dim=-1)
+
+
+def pointwise_l2_loss(inp, gt, epsilon):
+    """depthmotionnet.v2.losses.pointwise_l2_loss: mean_p sqrt(sum_c nf(inp - stop_gradient(gt))^2 + eps)
+    (channels last here)."""
+    diff = replace_nonfinite(inp - gt.detach())
+    return torch.sqrt((diff ** 2).sum(dim=-1) + epsilon).mean()
+
+
+def depth_sig_loss(pred, label, deltas=(2,), weights=(1.0,), sig_epsilon=1e-3, epsilon=1e-6):
+    """my_losses.py:78-82 with sig_params {'deltas': [2], 'weights': [1], 'epsilon': 0.001}, epsilon 1e-6 (:53)."""
+    return pointwise_l2_loss(scale_invariant_gradient(pred, deltas, weights, sig_epsilon),
+                             scale_invariant_gradient(label, deltas, weights, sig_epsilon), epsilon)
 
 
 def _scale_hw(H, W, s):

@@ -247,3 +247,33 @@ def test_gradcheck_smooth_and_resizes():
     x = t(rng.standard_normal((1, 6, 6, 1))).requires_grad_(True)
     assert torch.autograd.gradcheck(lambda a: L.compute_smooth_loss(T.resize_bilinear_legacy(a, 12, 12)), (x,))
     assert torch.autograd.gradcheck(lambda a: T.resize_nearest_legacy(a, 4, 6).sum(), (x,))
+
+
+# ---------------------------------------------------------------- DeMoN sig loss (my_losses.py:78-82)
+def test_sig_known_values_and_scale_invariance():
+    from oracle import losses as OL
+    f = torch.tensor([[1.0, 3.0, 2.0, 2.0]], dtype=torch.float64).reshape(1, 1, 4, 1)
+    s = OL.scale_invariant_gradient(f, [1, 2], [1.0, 0.5], 0.0)
+    assert s.shape == (1, 1, 4, 4)
+    assert torch.allclose(s[0, 0, :, 0], torch.tensor([2 / 4, -1 / 5, 0.0, 0.0], dtype=torch.float64))
+    assert torch.allclose(s[0, 0, :, 2], torch.tensor([0.5 * 1 / 3, 0.5 * -1 / 5, 0.0, 0.0], dtype=torch.float64))
+    assert torch.all(s[..., 1] == 0) and torch.all(s[..., 3] == 0)       # H = 1: no y neighbours
+    g = torch.rand(2, 7, 9, 1, dtype=torch.float64) + 0.1
+    a = OL.scale_invariant_gradient(g, [1, 2, 4], [1.0, 1.0, 1.0], 0.0)
+    b = OL.scale_invariant_gradient(g * 37.5, [1, 2, 4], [1.0, 1.0, 1.0], 0.0)
+    assert torch.allclose(a, b, rtol=1e-12, atol=1e-14)                  # scale invariance (eps = 0)
+    assert torch.all(OL.scale_invariant_gradient(torch.full((1, 5, 5, 1), 2.0, dtype=torch.float64),
+                                                 [2], [1.0], 1e-3) == 0)
+
+
+def test_sig_loss_nan_holes_and_gradient():
+    from oracle import losses as OL
+    rng = np.random.default_rng(0)
+    pred = torch.tensor(rng.uniform(0.2, 2.0, (2, 6, 7, 1)), dtype=torch.float64, requires_grad=True)
+    lab = torch.tensor(rng.uniform(0.2, 2.0, (2, 6, 7, 1)), dtype=torch.float64)
+    lab[0, 2, 3, 0] = float("nan")
+    v = OL.depth_sig_loss(pred, lab, deltas=(1, 2), weights=(1.0, 0.5))
+    assert torch.isfinite(v)
+    # every pixel whose diffs all involve the hole contributes sqrt(eps) at least; loss >= sqrt(eps)
+    assert v.item() >= 1e-3
+    assert torch.autograd.gradcheck(lambda p: OL.depth_sig_loss(p, lab, deltas=(1, 2), weights=(1.0, 0.5)), (pred,))

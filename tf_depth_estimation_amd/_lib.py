@@ -111,6 +111,8 @@ _SIGS = {
     "tde_resize_bilinear_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_area_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, P, P]),
     "tde_loss_smooth2": (c_int, [c_int, c_int, c_int, P, c_int, c_int, c_int, c_float, P, P, c_int, c_int, P]),
+    "tde_loss_sig_l2": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_float, c_float, c_float, P,
+                                P, c_int, c_int, P]),
     "tde_loss_l1": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, c_int, c_float, P, P, c_int, c_int, P]),
     "tde_adam_step_begin": (c_int, [P, P]),
     "tde_adam_update": (c_int, [c_size_t, P, P, P, P, P, c_float, c_float, c_float, c_float, P]),

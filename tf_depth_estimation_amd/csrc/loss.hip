@@ -88,6 +88,109 @@ __global__ void __launch_bounds__(256) l1_kernel(long total, const float* pred, 
   if (threadIdx.x == 0) atomicAdd(loss, bs * (double)weight / (double)total);
 }
 
+// ------------------------------------------------------------------ DeMoN scale-invariant-gradient loss
+// my_losses.py:78-82 (compute_loss_single_depth; split_training.py:117):
+//   sig(f)[2d](p)   = w_d (f(p + D_d x) - f(p)) / (|f(p + D_d x)| + |f(p)| + eps_s)     (0 off the image)
+//   sig(f)[2d+1](p) = same along y
+//   loss += weight * mean_p sqrt(sum_c nf(sig(pred)_c(p) - sig(label)_c(p))^2 + eps)
+// (lmbspecialops.scale_invariant_gradient per delta, concatenated as depthmotionnet.v2.losses does, and
+// its pointwise_l2_loss: replace_nonfinite of the difference, label under stop_gradient).  The gradient
+// wrt pred at q gathers every sig term that reads f(q): its own (as the centre) and those anchored at
+// q - D_d x / q - D_d y (as the neighbour); the per-pixel L2 factor of those anchors is recomputed.
+constexpr int SIG_MAXD = 8;
+struct SigArgs {
+  int N, H, W, nd;
+  int delta[SIG_MAXD];
+  float wt[SIG_MAXD];
+  float seps, l2eps, weight;
+  const float* pred; int cs, co;
+  const float* label;
+  double* loss;
+  float* g; int gcs, gco;
+};
+
+__device__ __forceinline__ float sig_term(float f0, float f1, float w, float eps) {
+  return w * (f1 - f0) / (fabsf(f1) + fabsf(f0) + eps);
+}
+
+// dL/dsig_c at pixel (n,i,j) for all 2*nd components (0 where the difference is non-finite); returns
+// the pixel's sqrt(.) value.
+__device__ float sig_pixel(const SigArgs& a, int n, int i, int j, float* G) {
+  const long base = (long)(n * a.H + i) * a.W + j;
+  const float p0 = a.pred[base * a.cs + a.co], l0 = a.label[base];
+  float d[2 * SIG_MAXD];
+  float ss = 0.f;
+  for (int k = 0; k < a.nd; ++k) {
+    const int D = a.delta[k];
+    float dx = 0.f, dy = 0.f;   // both sig values are 0 off the image
+    if (j + D < a.W) {
+      const long q = base + D;
+      dx = sig_term(p0, a.pred[q * a.cs + a.co], a.wt[k], a.seps) - sig_term(l0, a.label[q], a.wt[k], a.seps);
+    }
+    if (i + D < a.H) {
+      const long q = base + (long)D * a.W;
+      dy = sig_term(p0, a.pred[q * a.cs + a.co], a.wt[k], a.seps) - sig_term(l0, a.label[q], a.wt[k], a.seps);
+    }
+    if (!isfinite(dx)) dx = 0.f;   // sops.replace_nonfinite (gradient masked too)
+    if (!isfinite(dy)) dy = 0.f;
+    d[2 * k] = dx; d[2 * k + 1] = dy;
+    ss += dx * dx + dy * dy;
+  }
+  const float r = sqrtf(ss + a.l2eps);
+  for (int c = 0; c < 2 * a.nd; ++c) G[c] = d[c] / r;
+  return r;
+}
+
+__global__ void __launch_bounds__(256) sig_l2_kernel(const SigArgs a) {
+  __shared__ double sh[4];
+  const long total = (long)a.N * a.H * a.W;
+  const float wn = (float)(a.weight / (double)total);
+  double lsum = 0.0;
+  float G[2 * SIG_MAXD];
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % a.W);
+    const long t = idx / a.W;
+    const int i = (int)(t % a.H), n = (int)(t / a.H);
+    const float fq = a.pred[idx * a.cs + a.co];
+    const float sq = tde_sign(fq);
+    lsum += sig_pixel(a, n, i, j, G);
+    float gq = 0.f;
+    // q as the centre (f0) of its own terms: dt/df0 = w (-1/D - u sign(f0) / D^2)
+    for (int k = 0; k < a.nd; ++k) {
+      const int D = a.delta[k];
+      if (j + D < a.W) {
+        const float f1 = a.pred[(idx + D) * a.cs + a.co];
+        const float den = fabsf(f1) + fabsf(fq) + a.seps, u = f1 - fq;
+        gq += G[2 * k] * a.wt[k] * (-1.f / den - u * sq / (den * den));
+      }
+      if (i + D < a.H) {
+        const float f1 = a.pred[(idx + (long)D * a.W) * a.cs + a.co];
+        const float den = fabsf(f1) + fabsf(fq) + a.seps, u = f1 - fq;
+        gq += G[2 * k + 1] * a.wt[k] * (-1.f / den - u * sq / (den * den));
+      }
+    }
+    // q as the neighbour (f1) of the terms anchored D to the left / above: dt/df1 = w (1/D - u sign(f1) / D^2)
+    for (int k = 0; k < a.nd; ++k) {
+      const int D = a.delta[k];
+      if (j - D >= 0) {
+        sig_pixel(a, n, i, j - D, G);
+        const float f0 = a.pred[(idx - D) * a.cs + a.co];
+        const float den = fabsf(fq) + fabsf(f0) + a.seps, u = fq - f0;
+        gq += G[2 * k] * a.wt[k] * (1.f / den - u * sq / (den * den));
+      }
+      if (i - D >= 0) {
+        sig_pixel(a, n, i - D, j, G);
+        const float f0 = a.pred[(idx - (long)D * a.W) * a.cs + a.co];
+        const float den = fabsf(fq) + fabsf(f0) + a.seps, u = fq - f0;
+        gq += G[2 * k + 1] * a.wt[k] * (1.f / den - u * sq / (den * den));
+      }
+    }
+    a.g[idx * a.gcs + a.gco] += gq * wn;
+  }
+  const double bs = tde_block_sum_d(lsum, sh);
+  if (threadIdx.x == 0) atomicAdd(a.loss, bs * (double)a.weight / (double)total);
+}
+
 int ew_grid(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
@@ -194,6 +297,25 @@ int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, c
   const long total = (long)N * H * W;
   hipLaunchKernelGGL(l1_kernel, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, pred,
                      cstride, coff, label, nonfinite, weight, loss, grad, g_cstride, g_coff);
+  return tde_launch_status();
+}
+
+int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int coff, const float* label, int ndeltas,
+                    const int* deltas, const float* weights, float sig_epsilon, float epsilon, float weight,
+                    double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && pred && label && loss && grad && ndeltas >= 1 && ndeltas <= SIG_MAXD &&
+                deltas && weights && cstride > coff && g_cstride > g_coff);
+  SigArgs a{};
+  a.N = N; a.H = H; a.W = W; a.nd = ndeltas;
+  for (int k = 0; k < ndeltas; ++k) {
+    TDE_CHECK_ARG(deltas[k] >= 1);
+    a.delta[k] = deltas[k];
+    a.wt[k] = weights[k];
+  }
+  a.seps = sig_epsilon; a.l2eps = epsilon; a.weight = weight;
+  a.pred = pred; a.cs = cstride; a.co = coff; a.label = label; a.loss = loss;
+  a.g = grad; a.gcs = g_cstride; a.gco = g_coff;
+  hipLaunchKernelGGL(sig_l2_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
   return tde_launch_status();
 }
 

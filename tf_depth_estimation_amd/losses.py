@@ -48,6 +48,20 @@ def l1(pred, label, g, weight, acc, slot, nonfinite=False, coff=0):
               dptr(acc, slot), ptr(g), C, coff, _lib.stream_ptr())
 
 
+def sig_l2(pred, label, g, weight, acc, slot, deltas=(2,), weights=(1.0,), sig_epsilon=1e-3, epsilon=1e-6, coff=0):
+    """DeMoN scale-invariant-gradient loss of channel `coff` of pred against label (my_losses.py:78-82):
+    pointwise_l2_loss(scale_invariant_gradient(pred), scale_invariant_gradient(label)) * weight."""
+    N, H, W, C = pred.shape
+    n = len(deltas)
+    if n != len(weights) or not 1 <= n <= 8:
+        raise ValueError("deltas and weights: equal lengths, 1..8 entries")
+    d = (ctypes.c_int * n)(*[int(v) for v in deltas])
+    w = (ctypes.c_float * n)(*[float(v) for v in weights])
+    _lib.call("tde_loss_sig_l2", N, H, W, ptr(pred), C, coff, ptr(label), n, ctypes.cast(d, ctypes.c_void_p),
+              ctypes.cast(w, ctypes.c_void_p), float(sig_epsilon), float(epsilon), float(weight), dptr(acc, slot),
+              ptr(g), C, coff, _lib.stream_ptr())
+
+
 def area(src, dst):
     N, H, W, C = src.shape
     _lib.call("tde_resize_area_fwd", N, H, W, C, ptr(src), dst.shape[1], dst.shape[2], ptr(dst), _lib.stream_ptr())
@@ -107,6 +121,32 @@ class _SmoothLoss(torch.autograd.Function):
     def backward(ctx, dl):
         (g,) = ctx.saved_tensors
         return g * dl
+
+
+class _SigLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, label, deltas, weights, sig_epsilon, epsilon):
+        if pred.dtype != torch.float32 or not pred.is_cuda or pred.shape[-1] != 1:
+            raise TypeError("depth_sig_loss takes a float32 CUDA [N,H,W,1] prediction")
+        pred = pred.contiguous()
+        label = label.contiguous().reshape(pred.shape).float()
+        acc = torch.zeros(1, device=pred.device, dtype=torch.float64)
+        g = torch.zeros_like(pred)
+        sig_l2(pred, label, g, 1.0, acc, 0, deltas, weights, sig_epsilon, epsilon)
+        ctx.save_for_backward(g)
+        return acc[0].float()
+
+    @staticmethod
+    def backward(ctx, dl):
+        (g,) = ctx.saved_tensors
+        return g * dl, None, None, None, None, None
+
+
+def depth_sig_loss(pred, label, deltas=(2,), weights=(1.0,), sig_epsilon=1e-3, epsilon=1e-6):
+    """my_losses.py:78-82: pointwise_l2_loss(scale_invariant_gradient(pred), scale_invariant_gradient(label))
+    with sig_params {'deltas': [2], 'weights': [1], 'epsilon': 0.001} and epsilon 1e-6 (:53) by default;
+    the label may hold NaN holes (replace_nonfinite).  Differentiable wrt pred (one fused HIP pass)."""
+    return _SigLoss.apply(pred, label, tuple(deltas), tuple(weights), sig_epsilon, epsilon)
 
 
 def compute_smooth_loss(pred):
