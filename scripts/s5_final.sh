@@ -1,0 +1,9 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest -q --timeout 200 --timeout-method thread tests -m gpu > gpurun_out/s5f_gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/s5f_gpu_tests.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s5f_smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/s5f_smoke.log
+bash scripts/round_profile.sh r01s5 || exit $?
+timeout -k 10 300 python scripts/infer_bench.py > gpurun_out/infer_r01s5.json 2> gpurun_out/infer_r01s5.err || exit $?

@@ -1082,7 +1082,10 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   const Plan pl = make_plan(d, mode);
   const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
   const size_t halo = halo_ws_bytes(d, mode, bn);
-  return igemm > halo ? igemm : halo;
+  size_t b = igemm > halo ? igemm : halo;
+  HwgPlan wp;
+  if (mode == MODE_WGRAD && hwg_plan(d, wp) && wp.part_bytes > b) b = wp.part_bytes;
+  return b;
 }
 
 // prefetch depth (tiles in flight) of the fp32 kernels: 1 for 128-row tiles, 2 for the 64-row tiles of
@@ -1218,6 +1221,13 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
                size_t ws_bytes, void* stream) {
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  HwgPlan wp;
+  if (MODE == MODE_WGRAD && hwg_plan(*d, wp)) {
+    // stride-1, narrow, high-resolution layer: halo-tiled filter gradient (halo_wgrad.hip)
+    if (wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    if (!skip) hwg_launch(wp, *d, a.x, a.dy, a.dw, accumulate, tde_ws_body(ws), static_cast<hipStream_t>(stream));
+    return tde_launch_status();
+  }
   HaloPlan hp;
   if (MODE != MODE_WGRAD && halo_plan(*d, MODE == MODE_FWD ? 0 : 1, g_conv_math, hp)) {
     // stride-1, few-channel, high-resolution layer: halo-tiled kernel (halo_conv.hip)
@@ -1309,6 +1319,26 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   HaloPlan hp;
+  HwgPlan wp;
+  if (MODE1 == MODE_DGRAD && hwg_plan(*d, wp)) {
+    // filter gradient on the halo-tiled WGRAD kernel; data gradient on the halo path or the implicit GEMM
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool hd = halo_plan(*d, 1, g_conv_math, hp);
+    const Plan p1 = hd ? Plan{} : make_plan(*d, MODE1);
+    const size_t b1 = hd ? hp.wbytes : p1.slab_bytes;
+    if (b1 + wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    char* body = tde_ws_body(ws);
+    if (hd) {
+      if (!skip) halo_launch(hp, *d, a1.dy, a1.w, a1.dx, acc1, body, nullptr, st);
+    } else {
+      a1.ws = reinterpret_cast<float*>(body);
+      a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
+      if (!skip) launch_mode<MODE1>(p1, a1, st);
+      if (!skipr) launch_reduce<MODE1>(p1, a1, st);
+    }
+    if (!skip) hwg_launch(wp, *d, a2.x, a2.dy, a2.dw, acc2, body + b1, st);
+    return tde_launch_status();
+  }
   if (MODE1 == MODE_DGRAD && halo_plan(*d, 1, g_conv_math, hp)) {
     // data gradient on the halo path, filter gradient on the implicit GEMM (two launches + its reduce)
     const Plan p2 = make_plan(*d, MODE_WGRAD);
@@ -1356,6 +1386,11 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   if (mode1 == MODE_DGRAD) {
     const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
     if (h && h + make_plan(d, MODE_WGRAD).slab_bytes > b) b = h + make_plan(d, MODE_WGRAD).slab_bytes;
+    HwgPlan wp;
+    if (hwg_plan(d, wp)) {
+      const size_t b1 = h > p1.slab_bytes ? h : p1.slab_bytes;   // halo or igemm data gradient (math-dependent)
+      if (b1 + wp.part_bytes > b) b = b1 + wp.part_bytes;
+    }
   }
   return b + 64;
 }

@@ -32,3 +32,18 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp);
 void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
                  int accumulate, void* ws, double* bnp, hipStream_t st, const float* bias = nullptr,
                  int relu = 0);
+
+// Halo-tiled filter gradient (halo_wgrad.hip) of a stride-1 conv with K <= 32 output channels at high
+// resolution: partial dW per (pixel chunk, kernel row) in fp32 MFMA, then a fixed-order chunk reduce.
+struct HwgPlan {
+  int ok;
+  int CF, NF, nitems;     // 16-channel input / output fragments, (kw, cf, nf) items per block
+  int CPS, KPS;           // LDS row strides (floats)
+  int ntw, chunks;        // 64-pixel segments per output row, pixel chunks (grid x; grid y = KH)
+  long ntiles;
+  size_t lds_bytes, part_bytes;
+};
+bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp);
+// dw (+)= dL/dW from x (view of d) and dy (y view of d); ws >= hp.part_bytes (16-byte aligned).
+void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, const float* dy, float* dw,
+                int accumulate, void* ws, hipStream_t st);
