@@ -6,9 +6,9 @@
 // a (taps*C) x K GEMM over ~1e5 pixels with a 128 x 32 tile: its im2col operand re-reads every input pixel
 // from L2 once per tap (49x for cnv1b), and with K = 16/32 the tile is too narrow for the bf16x6 path,
 // so those layers ran at 30-50 TF/s.  Here:
-//   * block = (kernel row kh, pixel chunk); it walks 64-pixel output row segments of its chunk;
-//   * per segment the ONE input row the kernel row reads (64 + KW - 1 pixels x C channels) and the dy
-//     segment (64 x K) are staged in LDS (register prefetch of the next segment overlaps the MFMAs);
+//   * block = (kernel row kh, pixel chunk); it walks 128-pixel output row segments of its chunk;
+//   * per segment the ONE input row the kernel row reads (128 + KW - 1 pixels x C channels) and the dy
+//     segment (128 x K) are staged in LDS (register prefetch of the next segment overlaps the MFMAs);
 //   * wave w owns (kw, channel fragment, column fragment) items w, w+4, ...: per 4-pixel k-step one
 //     v_mfma_f32_16x16x4_f32 per item -- A = x[pixel + kw][c] straight out of the halo row at the tap
 //     offset (any offset: 4-byte LDS reads), B = dy[pixel][n] shared by all items of a column fragment;
@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int TP = 64;        // output pixels per row segment
+constexpr int TP = 128;       // output pixels per row segment
 constexpr int MAXI = 8;       // (kw, cf, nf) items per wave
 constexpr int XQ = 8;         // f4 prefetch registers per thread: input row
 constexpr int DQ = 4;         // f4 prefetch registers per thread: dy segment
@@ -232,10 +232,10 @@ bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp) {
   if (d.x_cstride % 4 || d.x_coff % 4 || d.y_cstride % 4 || d.y_coff % 4) return false;
   const int CF = (d.C + 15) / 16, NF = (d.K + 15) / 16;
   const int nitems = d.KW * CF * NF;
-  // measured (scripts/conv_micro.py, TDE_HWG_DIAG): the fp32-MFMA loop runs at ~57% of its peak and the
-  // per-segment staging + partial reduce cost ~50 us on cnv1b, so the kernel only beats the implicit GEMM
-  // where the MFMA work per segment is large (cnv1b: 192 vs 201 us; icnv1 / icnv2 with 6 / 30 items of 3x3
-  // taps: 1.3x / 1.25x slower) -- >= 25 items (7 per wave) unless TDE_HWG_MIN_ITEMS says otherwise
+  // measured (scripts/conv_micro.py, TDE_HWG_DIAG): the fp32-MFMA loop runs at ~56% of its peak and the
+  // per-segment staging + partial reduce cost ~45 us on cnv1b, so the kernel only beats the implicit GEMM
+  // where the MFMA work per segment is large (cnv1b: 180 vs 201 us; icnv1 with 6 items of 3x3 taps: 93 vs
+  // 79 us) -- >= 25 items (7 per wave) unless TDE_HWG_MIN_ITEMS says otherwise
   if (nitems > 4 * MAXI || nitems < g_hwg_min_items) return false;
   if ((TP + d.KW - 1) * CF * 4 > 256 * XQ || TP * NF * 4 > 256 * DQ) return false;
   hp.ok = 1;
