@@ -93,9 +93,9 @@ CONV_CASES = [
     (2, 90, 100, 65, 68, 32, 3, 1, 132, 64),        # icnv2-like: 2 chunks, offset view; DGRAD 2 column tiles
     (1, 128, 136, 64, 64, 64, 5, 1, 64, 0),         # cnv2b-like: 5x5, 2 chunks, 64 columns
     (1, 120, 140, 129, 132, 64, 3, 1, 132, 0),      # icnv3-like: 3 chunks; DGRAD 3 column tiles
-    # halo-tiled WGRAD (halo_wgrad.hip: stride 1, K <= 32, >= 16384 pixels) -- the cnv1b / icnv1 /
-    # icnv2-like cases above take it too
-    (2, 96, 100, 16, 16, 16, 5, 1, 24, 8),          # 5x5, one fragment each way, ragged 64-px segments
+    # halo-tiled WGRAD (halo_wgrad.hip: stride 1, K <= 32, >= 16384 pixels, >= 25 MFMA items): the cnv1b-like
+    # case above; these two run it with TDE_HWG_MIN_ITEMS=1 (tuning runs) and the implicit GEMM by default
+    (2, 96, 100, 16, 16, 16, 5, 1, 24, 8),          # 5x5, one fragment each way, ragged 128-px segments
     (4, 64, 70, 44, 44, 12, 1, 1, 48, 0),           # 1x1, K = 12 (partial column fragment), 3 channel frags
 ]
 

@@ -12,6 +12,8 @@
 //           deterministic fixed-order reduction over chunks.
 #include "tde_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct HeadArgs {
@@ -374,15 +376,20 @@ struct WgPlan {
   int chunks, ppc, tgroups;
 };
 
+// pixels per thread lane at least: 2 (config-2 step, scripts/layer_profile.py: disp2/3/4 backward 50/42/40 ->
+// 41/32/27 us against 8; disp1 unchanged) -- more blocks for the low-resolution heads
+static const long g_head_ppl = []() { const char* v = getenv("TDE_HEAD_PPL"); return v ? atol(v) : 2L; }();
+static const long g_head_blocks = []() { const char* v = getenv("TDE_HEAD_BLOCKS"); return v ? atol(v) : 2048L; }();
+
 WgPlan wg_plan(const tde_conv_desc_t* d) {
   WgPlan w;
   const long M = (long)d->N * d->OH * d->OW;
   const int TT = d->K == 1 ? 9 : (d->K == 2 ? 5 : 2);
   w.tgroups = (d->KH * d->KW + TT - 1) / TT;
   const int P = 256 / (d->C / 4);
-  // >= 8 pixels per thread lane, ~2048 blocks in total, <= WG_MAX_CHUNKS partial rows
-  long chunks = (2048 + w.tgroups - 1) / w.tgroups;
-  const long maxc = (M + 8l * P - 1) / (8l * P);
+  // >= g_head_ppl pixels per thread lane, ~2048 blocks in total, <= WG_MAX_CHUNKS partial rows
+  long chunks = (g_head_blocks + w.tgroups - 1) / w.tgroups;
+  const long maxc = (M + g_head_ppl * P - 1) / (g_head_ppl * P);
   if (chunks > maxc) chunks = maxc;
   if (chunks > WG_MAX_CHUNKS) chunks = WG_MAX_CHUNKS;
   if (chunks < 1) chunks = 1;
