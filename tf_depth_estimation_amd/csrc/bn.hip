@@ -15,6 +15,8 @@
 
 #include "bn_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -408,15 +410,21 @@ int finalize_blocks(int C) { return C / 4; }
 }  // namespace
 
 // ------------------------------------------------------------------ internal launchers (bn_internal.h)
+static long bn_env(const char* n, long d) { const char* v = getenv(n); return v ? atol(v) : d; }
+// elements per partial-sum block and row chunks at most: 8K / 1024 (config-2 step: BN backward 473 -> 441 us
+// against 16K / 256, which left the 192x256 and 96x128 layers at <= 256 blocks on 256 CUs)
+static const long g_bn_elems = bn_env("TDE_BN_ELEMS", 8192);
+static const long g_bn_maxch = bn_env("TDE_BN_MAXCH", 1024);
+
 BnChunks bn_chunk_plan(long M, int C, int work_mult) {
-  // ~16K elements (x work_mult, e.g. split-K slabs) per block, <= 256 chunks
+  // ~g_bn_elems elements (x work_mult, e.g. split-K slabs) per block, <= g_bn_maxch chunks
   BnChunks p;
   const int cq = C / 4;
   p.groups = (cq + 15) / 16;
   const int nq = cq < 16 ? cq : 16;
   const int ty_n = 256 / nq;
-  long ch = M * (long)C * (work_mult > 1 ? work_mult : 1) / 16384 / p.groups;
-  if (ch > 256) ch = 256;
+  long ch = M * (long)C * (work_mult > 1 ? work_mult : 1) / g_bn_elems / p.groups;
+  if (ch > g_bn_maxch) ch = g_bn_maxch;
   if (ch < 1) ch = 1;
   long rpc = (M + ch - 1) / ch;
   rpc = (rpc + ty_n - 1) / ty_n * ty_n;
