@@ -102,8 +102,10 @@ __global__ void __launch_bounds__(256) bilinear_bwd_kernel(int N, int H, int W, 
     const int iw = (int)(pix % W);
     const long t = pix / W;
     const int ih = (int)(t % H), n = (int)(t / H);
-    const int oh0 = max(0, (int)floorf((ih - 1) / sy) - 1), oh1 = min(OH - 1, (int)ceilf((ih + 1) / sy) + 1);
-    const int ow0 = max(0, (int)floorf((iw - 1) / sx) - 1), ow1 = min(OW - 1, (int)ceilf((iw + 1) / sx) + 1);
+    // contributors have floor(o * s) in {i - 1, i} (or the clamped last row): o in [(i - 1) / s, (i + 1) / s];
+    // the exact tap tests below decide, the window only has to contain them (25 candidates at x2, not 49)
+    const int oh0 = max(0, (int)floorf((ih - 1) / sy)), oh1 = min(OH - 1, (int)ceilf((ih + 1) / sy));
+    const int ow0 = max(0, (int)floorf((iw - 1) / sx)), ow1 = min(OW - 1, (int)ceilf((iw + 1) / sx));
     float s = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh) {
       const Lerp ly = lerp_src(oh, sy, H);
