@@ -63,3 +63,23 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+
+
+def test_inference_and_sig_loss_entry_points_validate_arguments():
+    """The folded-BN inference convs, the BN fold and the DeMoN sig loss reject bad arguments on the host,
+    before any device work (status -1 = TDE_ERR_ARG)."""
+    from tf_depth_estimation_amd import _lib
+    lib = _lib.load()
+    d = _lib.ConvDesc()
+    assert lib.tde_conv2d_fwd_bias_act(ctypes.byref(d), None, None, None, 1, None, None, 0, None) == -1
+    assert lib.tde_deconv2d_fwd_bias_act(ctypes.byref(d), None, None, None, 1, None, None, 0, None) == -1
+    assert lib.tde_bn_fold(0, 4, 4, 0, None, None, None, None, 1e-3, None, None, None) == -1
+    assert lib.tde_bn_fold(9, 4, 4, 2, None, None, None, None, 1e-3, None, None, None) == -1
+    deltas = (ctypes.c_int * 1)(2)
+    weights = (ctypes.c_float * 1)(1.0)
+    assert lib.tde_loss_sig_l2(1, 8, 8, None, 1, 0, None, 1, ctypes.cast(deltas, ctypes.c_void_p),
+                               ctypes.cast(weights, ctypes.c_void_p), 1e-3, 1e-6, 1.0, None, None, 1, 0, None) == -1
+    # relu must be 0 or 1 even with an otherwise valid descriptor
+    d = _lib.ConvDesc(N=1, H=8, W=8, C=4, OH=8, OW=8, K=4, KH=3, KW=3, stride=1, pad_top=1, pad_left=1, w_cin=4,
+                      x_cstride=4, x_coff=0, y_cstride=4, y_coff=0)
+    assert lib.tde_conv2d_fwd_bias_act(ctypes.byref(d), None, None, None, 2, None, None, 0, None) == -1
