@@ -3,6 +3,8 @@
 // pass over the prediction: the loss is the top of the graph, so its backward needs no saved state.
 #include "tde_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 // value of the smoothed map at (n,i,j): pred or 1/pred (train_depth_then_cam_lr.py:217 smooths 1/disp)
@@ -191,9 +193,11 @@ __global__ void __launch_bounds__(256) sig_l2_kernel(const SigArgs a) {
   if (threadIdx.x == 0) atomicAdd(a.loss, bs * (double)a.weight / (double)total);
 }
 
+// grid-stride loss kernels end every block in fp64 atomics on one accumulator: a few hundred blocks, not
+// thousands (the same contention measured on depth_pyramid_kernel)
 int ew_grid(long n) {
   long b = (n + 255) / 256;
-  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+  return (int)(b > 512 ? 512 : (b < 1 ? 1 : b));
 }
 
 // ------------------------------------------------------------------ fused multi-scale depth loss head
@@ -206,8 +210,16 @@ struct PyrArgs {
   tde_depth_loss_t a;
   int bstart[TDE_MAX_SCALES + 1];   // first block of each scale (a block works on ONE scale, so the
                                     // per-scale parameters are indexed uniformly: scalar loads)
+  float w1[TDE_MAX_SCALES], w23[TDE_MAX_SCALES], w4[TDE_MAX_SCALES];   // smooth weights / term counts
+  double l1d[TDE_MAX_SCALES];       // depth-L1 weight / pixel count (value, fp64)
+  float l1f[TDE_MAX_SCALES];        // the same rounded to float (gradient)
 };
 
+// Each pixel's smoothness value + gradient needs f on its 3x3 neighbourhood plus (i, j+-2) and (i+-2, j):
+// those 13 values are loaded once into registers (clamped addresses; the edge tests below decide which
+// terms exist) and every second difference is formed from them in the same fp32 order as t_dx2 / t_dxdy /
+// t_dydx / t_dy2 (the same fp32 expressions as the per-term evaluation).  32-bit index math; the
+// per-scale weights are precomputed on the host exactly as before (double, then rounded to float).
 __global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
   __shared__ double sh[4];
   const tde_depth_loss_t& a = P.a;
@@ -216,57 +228,95 @@ __global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
   while ((int)blockIdx.x >= P.bstart[s + 1]) ++s;
   s = __builtin_amdgcn_readfirstlane(s);
   const int H = a.H >> s, W = a.W >> s;
-  const long total = (long)a.N * H * W;
+  const int total = a.N * H * W;
   const int nb = P.bstart[s + 1] - P.bstart[s];
-  for (long loc = (blockIdx.x - P.bstart[s]) * (long)blockDim.x + threadIdx.x; loc < total;
-       loc += (long)nb * blockDim.x) {
-    const int j = (int)(loc % W);
-    const long t = loc / W;
-    const int i = (int)(t % H), n = (int)(t / H);
-    const Map f{a.pred[s], H, W, a.pred_cs[s], a.pred_co[s], a.recip};
+  const float* pr = a.pred[s];
+  const int pcs = a.pred_cs[s], pco = a.pred_co[s];
+  const bool smooth = a.smooth_w[s] != 0.f && H >= 3 && W >= 3;
+  const float w1 = P.w1[s], w23 = P.w23[s], w4 = P.w4[s];
+  for (int loc = (blockIdx.x - P.bstart[s]) * 256 + threadIdx.x; loc < total; loc += nb * 256) {
+    const int t = loc / W;
+    const int j = loc - t * W;
+    const int n = t / H, i = t - n * H;
+    const int rowb = n * H;
+    auto F = [&](int ii, int jj) __attribute__((always_inline)) {
+      ii = min(max(ii, 0), H - 1);
+      jj = min(max(jj, 0), W - 1);
+      const float v = pr[((rowb + ii) * W + jj) * pcs + pco];
+      return a.recip ? 1.f / v : v;
+    };
+    const float pv = pr[(loc)*pcs + pco];
     float gf = 0.f;
-    if (a.smooth_w[s] != 0.f && H >= 3 && W >= 3) {
-      const double n1 = (double)a.N * H * (W - 2), n23 = (double)a.N * (H - 1) * (W - 1), n4 = (double)a.N * (H - 2) * W;
-      const float w1 = (float)(a.smooth_w[s] / n1), w23 = (float)(a.smooth_w[s] / n23), w4 = (float)(a.smooth_w[s] / n4);
+    if (smooth) {
+      // f[r][c] = f(i + r - 1, j + c - 1) on the 3x3 block; fxm2/fxp2 = f(i, j-+2), fym2/fyp2 = f(i-+2, j)
+      float f[3][3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) f[r][c] = F(i + r - 1, j + c - 1);
+      const float fxm2 = F(i, j - 2), fxp2 = F(i, j + 2), fym2 = F(i - 2, j), fyp2 = F(i + 2, j);
+      // t_dx2(i, jj) = (f(i,jj+2) - f(i,jj+1)) - (f(i,jj+1) - f(i,jj))
+      const float dx2_0 = (fxp2 - f[1][2]) - (f[1][2] - f[1][1]);         // jj = j
+      const float dx2_m1 = (f[1][2] - f[1][1]) - (f[1][1] - f[1][0]);     // jj = j - 1
+      const float dx2_m2 = (f[1][1] - f[1][0]) - (f[1][0] - fxm2);        // jj = j - 2
+      const float dy2_0 = (fyp2 - f[2][1]) - (f[2][1] - f[1][1]);
+      const float dy2_m1 = (f[2][1] - f[1][1]) - (f[1][1] - f[0][1]);
+      const float dy2_m2 = (f[1][1] - f[0][1]) - (f[0][1] - fym2);
+      // t_dxdy(a,b) = (f(a+1,b+1) - f(a+1,b)) - (f(a,b+1) - f(a,b)); t_dydx(a,b) = (f(a+1,b+1) - f(a,b+1)) - (f(a+1,b) - f(a,b))
+#define DXDY(r, c) ((f[r + 1][c + 1] - f[r + 1][c]) - (f[r][c + 1] - f[r][c]))
+#define DYDX(r, c) ((f[r + 1][c + 1] - f[r][c + 1]) - (f[r + 1][c] - f[r][c]))
+      const float xy00 = DXDY(1, 1), yx00 = DYDX(1, 1);   // anchor (i, j)
+      const float xy0m = DXDY(1, 0), yx0m = DYDX(1, 0);   // (i, j - 1)
+      const float xym0 = DXDY(0, 1), yxm0 = DYDX(0, 1);   // (i - 1, j)
+      const float xymm = DXDY(0, 0), yxmm = DYDX(0, 0);   // (i - 1, j - 1)
+#undef DXDY
+#undef DYDX
       float lv = 0.f;
-      if (j < W - 2) lv += fabsf(t_dx2(f, n, i, j)) * w1;
-      if (i < H - 1 && j < W - 1) lv += (fabsf(t_dxdy(f, n, i, j)) + fabsf(t_dydx(f, n, i, j))) * w23;
-      if (i < H - 2) lv += fabsf(t_dy2(f, n, i, j)) * w4;
+      if (j < W - 2) lv += fabsf(dx2_0) * w1;
+      if (i < H - 1 && j < W - 1) lv += (fabsf(xy00) + fabsf(yx00)) * w23;
+      if (i < H - 2) lv += fabsf(dy2_0) * w4;
       ls += lv;
-      if (j < W - 2) gf += tde_sign(t_dx2(f, n, i, j)) * w1;
-      if (j >= 1 && j - 1 < W - 2) gf -= 2.f * tde_sign(t_dx2(f, n, i, j - 1)) * w1;
-      if (j >= 2) gf += tde_sign(t_dx2(f, n, i, j - 2)) * w1;
-      if (i < H - 2) gf += tde_sign(t_dy2(f, n, i, j)) * w4;
-      if (i >= 1 && i - 1 < H - 2) gf -= 2.f * tde_sign(t_dy2(f, n, i - 1, j)) * w4;
-      if (i >= 2) gf += tde_sign(t_dy2(f, n, i - 2, j)) * w4;
-      if (i < H - 1 && j < W - 1) gf += (tde_sign(t_dxdy(f, n, i, j)) + tde_sign(t_dydx(f, n, i, j))) * w23;
-      if (i < H - 1 && j >= 1) gf -= (tde_sign(t_dxdy(f, n, i, j - 1)) + tde_sign(t_dydx(f, n, i, j - 1))) * w23;
-      if (i >= 1 && j < W - 1) gf -= (tde_sign(t_dxdy(f, n, i - 1, j)) + tde_sign(t_dydx(f, n, i - 1, j))) * w23;
-      if (i >= 1 && j >= 1) gf += (tde_sign(t_dxdy(f, n, i - 1, j - 1)) + tde_sign(t_dydx(f, n, i - 1, j - 1))) * w23;
-      if (a.recip) {
-        const float p = a.pred[s][((long)(n * H + i) * W + j) * a.pred_cs[s] + a.pred_co[s]];
-        gf *= -1.f / (p * p);
-      }
+      if (j < W - 2) gf += tde_sign(dx2_0) * w1;
+      if (j >= 1 && j - 1 < W - 2) gf -= 2.f * tde_sign(dx2_m1) * w1;
+      if (j >= 2) gf += tde_sign(dx2_m2) * w1;
+      if (i < H - 2) gf += tde_sign(dy2_0) * w4;
+      if (i >= 1 && i - 1 < H - 2) gf -= 2.f * tde_sign(dy2_m1) * w4;
+      if (i >= 2) gf += tde_sign(dy2_m2) * w4;
+      if (i < H - 1 && j < W - 1) gf += (tde_sign(xy00) + tde_sign(yx00)) * w23;
+      if (i < H - 1 && j >= 1) gf -= (tde_sign(xy0m) + tde_sign(yx0m)) * w23;
+      if (i >= 1 && j < W - 1) gf -= (tde_sign(xym0) + tde_sign(yxm0)) * w23;
+      if (i >= 1 && j >= 1) gf += (tde_sign(xymm) + tde_sign(yxmm)) * w23;
+      if (a.recip) gf *= -1.f / (pv * pv);
     }
-    const float pv = a.pred[s][((long)(n * H + i) * W + j) * a.pred_cs[s] + a.pred_co[s]];
     if (a.l1_w[s] != 0.f) {
       const int fct = 1 << s;
       float lab;
       if (s == 0) {
-        lab = a.label[((long)n * a.H + i) * a.W + j];
+        lab = a.label[(n * a.H + i) * a.W + j];
       } else {
+        // the 2^s x 2^s box (<= 8 x 8): every load issued before the first add (a runtime-bounded loop
+        // would serialise one L2 round trip per pixel), then summed in the u-major order of
+        // tde_resize_area_fwd
+        const float* lb = a.label + (n * a.H + i * fct) * a.W + j * fct;
+        float box[8][8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int v = 0; v < 8; ++v) box[u][v] = (u < fct && v < fct) ? lb[u * a.W + v] : 0.f;
         float sum = 0.f;
-        for (int u = 0; u < fct; ++u)
-          for (int v = 0; v < fct; ++v) sum += a.label[((long)n * a.H + i * fct + u) * a.W + j * fct + v];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int v = 0; v < 8; ++v)
+            if (u < fct && v < fct) sum += box[u][v];
         lab = sum * (1.f / (float)(fct * fct));
       }
       float d = lab - pv;
       if (a.nonfinite && !isfinite(d)) d = 0.f;   // replace_nonfinite: value and gradient masked
-      const double tot = (double)a.N * H * W;
-      ll += fabsf(d) * ((double)a.l1_w[s] / tot);
-      gf += -tde_sign(d) * (float)(a.l1_w[s] / tot);
+      ll += fabsf(d) * P.l1d[s];
+      gf += -tde_sign(d) * P.l1f[s];
     }
-    float* gp = a.grad[s] + ((long)(n * H + i) * W + j) * a.g_cs[s] + a.g_co[s];
+    float* gp = a.grad[s] + loc * a.g_cs[s] + a.g_co[s];
     *gp = a.grad_accumulate ? *gp + gf : gf;
   }
   const double bs = tde_block_sum_d(ls, sh);
@@ -319,6 +369,10 @@ int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int cof
   return tde_launch_status();
 }
 
+// blocks per scale at most: every block ends in two fp64 atomics on the same two accumulators
+// (rocprofv3, config 2: 4096 -> 61 us, 512 -> 38 us, 128 -> 30 us per step)
+static const long g_pyr_maxb = []() { const char* v = getenv("TDE_PYR_MAXB"); return v ? atol(v) : 128L; }();
+
 int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
   PyrArgs P;
@@ -327,9 +381,26 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   for (int s = 0; s < a->nscales; ++s) {
     TDE_CHECK_ARG(a->pred[s] && a->grad[s] && (a->H >> s) > 0 && (a->W >> s) > 0);
     TDE_CHECK_ARG(a->l1_w[s] == 0.f || (a->label && a->H % (1 << s) == 0 && a->W % (1 << s) == 0));
-    P.bstart[s + 1] = P.bstart[s] + ew_grid((long)a->N * (a->H >> s) * (a->W >> s));
+    long nbk = ew_grid((long)a->N * (a->H >> s) * (a->W >> s));
+    if (nbk > g_pyr_maxb) nbk = g_pyr_maxb;
+    P.bstart[s + 1] = P.bstart[s] + (int)nbk;
   }
   for (int s = a->nscales; s < TDE_MAX_SCALES; ++s) P.bstart[s + 1] = P.bstart[s];
+  long cs = 1;
+  for (int s = 0; s < a->nscales; ++s) cs = a->pred_cs[s] > cs ? a->pred_cs[s] : cs;
+  for (int s = 0; s < a->nscales; ++s) cs = a->g_cs[s] > cs ? a->g_cs[s] : cs;
+  TDE_CHECK_ARG((long)a->N * a->H * a->W * cs < 0x7fffffffL);   // 32-bit pixel / element indices
+  for (int s = 0; s < TDE_MAX_SCALES; ++s) {
+    const int H = a->H >> s, W = a->W >> s;
+    const double n1 = (double)a->N * H * (W - 2), n23 = (double)a->N * (H - 1) * (W - 1),
+                 n4 = (double)a->N * (H - 2) * W, tot = (double)a->N * H * W;
+    const bool on = s < a->nscales;
+    P.w1[s] = on ? (float)(a->smooth_w[s] / n1) : 0.f;
+    P.w23[s] = on ? (float)(a->smooth_w[s] / n23) : 0.f;
+    P.w4[s] = on ? (float)(a->smooth_w[s] / n4) : 0.f;
+    P.l1d[s] = on ? (double)a->l1_w[s] / tot : 0.0;
+    P.l1f[s] = on ? (float)(a->l1_w[s] / tot) : 0.f;
+  }
   hipLaunchKernelGGL(depth_pyramid_kernel, dim3(P.bstart[a->nscales]), dim3(256), 0,
                      static_cast<hipStream_t>(stream), P);
   return tde_launch_status();
