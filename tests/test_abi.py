@@ -83,3 +83,39 @@ def test_inference_and_sig_loss_entry_points_validate_arguments():
     d = _lib.ConvDesc(N=1, H=8, W=8, C=4, OH=8, OW=8, K=4, KH=3, KW=3, stride=1, pad_top=1, pad_left=1, w_cin=4,
                       x_cstride=4, x_coff=0, y_cstride=4, y_coff=0)
     assert lib.tde_conv2d_fwd_bias_act(ctypes.byref(d), None, None, None, 2, None, None, 0, None) == -1
+
+
+def test_depth_pyramid_entry_point_validates_arguments():
+    """tde_loss_depth_pyramid rejects, on the host: a channel offset outside its view (the kernel's
+    loc * cs + co offsets assume 0 <= co < cs), a smoothness term on a scale below 3 x 3 pixels (the
+    reference's reduce_mean over an empty dx2 / dy2 is NaN; tde_loss_smooth2's contract) and a depth-L1 term
+    at a size not divisible by 2^s.  A valid descriptor with null device pointers for the loss accumulators
+    is still rejected only for its real defects (status -1 = TDE_ERR_ARG, no device work)."""
+    from tf_depth_estimation_amd import _lib
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(64)   # any non-null address: validation returns before device work
+
+    def desc(**kw):
+        a = _lib.DepthLoss()
+        a.N, a.H, a.W, a.nscales = 2, 24, 32, 4
+        for s in range(4):
+            a.pred[s] = ctypes.addressof(buf)
+            a.grad[s] = ctypes.addressof(buf)
+            a.pred_cs[s], a.pred_co[s], a.g_cs[s], a.g_co[s] = 3, 1, 2, 1
+            a.smooth_w[s], a.l1_w[s] = 1.0, 1.0
+        a.label = ctypes.addressof(buf)
+        for k, v in kw.items():
+            k, s = k.rsplit("_", 1) if k[-1].isdigit() else (k, None)
+            if s is None:
+                setattr(a, k, v)
+            else:
+                getattr(a, k)[int(s)] = v
+        return a
+
+    for bad in (dict(pred_co_2=3), dict(pred_co_0=-1), dict(g_co_1=2), dict(g_co_3=-4)):
+        assert lib.tde_loss_depth_pyramid(ctypes.byref(desc(**bad)), None) == -1, bad
+    # 12 x 16 at scale 3 is 1 x 2 pixels: smoothness rejected, depth-L1 alone accepted by validation
+    a = desc(H=12, W=16, l1_w_3=0.0)
+    assert lib.tde_loss_depth_pyramid(ctypes.byref(a), None) == -1
+    # H = 26 is not divisible by 4: the scale-2 depth-L1 box is ragged
+    assert lib.tde_loss_depth_pyramid(ctypes.byref(desc(H=26)), None) == -1

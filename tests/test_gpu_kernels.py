@@ -447,10 +447,11 @@ def test_resize_area(L):
         close(y.cpu()[m], r[m], what=f"area {f}")
 
 
-@pytest.mark.parametrize("recip", [0, 1])
-def test_loss_smooth2(L, recip):
+# the second shape has 2 x 192 x 256 = 98304 pixels per call x 2 (N=4): > 131072 = 512 blocks x 256, so the
+# grid-stride loop of the capped (<= 512-block) loss grids runs more than one iteration per thread
+@pytest.mark.parametrize("recip,N,H,W", [(0, 2, 12, 16), (1, 2, 12, 16), (0, 4, 192, 256), (1, 4, 192, 256)])
+def test_loss_smooth2(L, recip, N, H, W):
     lib = L.load()
-    N, H, W = 2, 12, 16
     p = rnd(N, H, W, 1, seed=18, lo=0.3, hi=2.0)
     cs, co = 3, 1
     gp = torch.zeros(N, H, W, cs, device="cuda")
@@ -466,10 +467,9 @@ def test_loss_smooth2(L, recip):
     close(g[..., co:co + 1], pr.grad, what="smooth grad")
 
 
-@pytest.mark.parametrize("nonfinite", [0, 1])
-def test_loss_l1(L, nonfinite):
+@pytest.mark.parametrize("nonfinite,N,H,W", [(0, 2, 12, 16), (1, 2, 12, 16), (1, 4, 192, 256)])
+def test_loss_l1(L, nonfinite, N, H, W):
     lib = L.load()
-    N, H, W = 2, 12, 16
     p = rnd(N, H, W, 1, seed=19)
     lab = rnd(N, H, W, 1, seed=20)
     if nonfinite:
@@ -503,13 +503,16 @@ def test_adam_matches_tf_form(L):
     close(gp - dev(p0), pr["p"] - p0, tol=1e-4, what="adam delta")
 
 
-@pytest.mark.parametrize("recip,nonfinite,acc", [(0, 0, 0), (1, 1, 1), (0, 1, 0)])
-def test_loss_depth_pyramid_matches_separate_terms(L, recip, nonfinite, acc):
+# 2 x 192 x 256 is the production shape: scale 0 needs 384 blocks and is capped at 128 (TDE_PYR_MAXB), so
+# every thread of the capped scales walks the `loc += nb * 256` grid stride several times and the block ->
+# scale lookup (bstart) spans capped and uncapped scales
+@pytest.mark.parametrize("recip,nonfinite,acc,N,H,W", [(0, 0, 0, 2, 24, 32), (1, 1, 1, 2, 24, 32), (0, 1, 0, 2, 24, 32),
+                                                       (0, 1, 0, 2, 192, 256), (1, 0, 1, 2, 192, 256)])
+def test_loss_depth_pyramid_matches_separate_terms(L, recip, nonfinite, acc, N, H, W):
     """tde_loss_depth_pyramid (all scales, one launch) == tde_resize_area_fwd + tde_loss_smooth2 +
     tde_loss_l1 per scale, values and gradients, including the write (acc=0) and add modes."""
     lib = L.load()
     st = L.stream_ptr()
-    N, H, W = 2, 24, 32
     preds = [dev(rnd(N, H >> s, W >> s, 3, seed=40 + s, lo=0.2, hi=2.0)) for s in range(4)]
     label = rnd(N, H, W, 1, seed=50, lo=0.25, hi=4.0)
     if nonfinite:

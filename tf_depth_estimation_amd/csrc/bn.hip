@@ -410,7 +410,9 @@ int finalize_blocks(int C) { return C / 4; }
 }  // namespace
 
 // ------------------------------------------------------------------ internal launchers (bn_internal.h)
-static long bn_env(const char* n, long d) { const char* v = getenv(n); return v ? atol(v) : d; }
+// tuning knobs; a missing, non-numeric or non-positive value means the default (a 0 would divide by zero in
+// bn_chunk_plan)
+static long bn_env(const char* n, long d) { return tde_env_pos(n, d); }
 // elements per partial-sum block and row chunks at most: 8K / 1024 (config-2 step: BN backward 473 -> 441 us
 // against 16K / 256, which left the 192x256 and 96x128 layers at <= 256 blocks on 256 CUs)
 static const long g_bn_elems = bn_env("TDE_BN_ELEMS", 8192);

@@ -942,10 +942,13 @@ static long env_long(const char* name, long dflt) {
 }
 // 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6 (process-wide, see tde_set_conv_math; TDE_CONV_MATH sets the initial
 // mode for A/B runs).  Default 3: the exact three-way split, the fastest mode within the parity bars.
-static int g_conv_math = (int)env_long("TDE_CONV_MATH", 3);
-static const long g_split_target = env_long("TDE_SPLIT_TARGET", 512);   // blocks to aim for
-static const long g_split_minkt = env_long("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
-static const long g_split_slab = env_long("TDE_SPLIT_SLAB_MB", 128) << 20;
+static int g_conv_math = []() {
+  const long m = env_long("TDE_CONV_MATH", 3);
+  return (int)(m >= 0 && m <= 3 ? m : 3);
+}();
+static const long g_split_target = tde_env_pos("TDE_SPLIT_TARGET", 512);   // blocks to aim for
+static const long g_split_minkt = tde_env_pos("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
+static const long g_split_slab = tde_env_pos("TDE_SPLIT_SLAB_MB", 128) << 20;
 // tile / split overrides for kernel exploration (scripts/conv_micro.py); 0 = planner's choice
 static const long g_force_bn = env_long("TDE_FORCE_BN", 0);
 static const long g_force_bm = env_long("TDE_FORCE_BM", 0);

@@ -320,10 +320,10 @@ long env_l(const char* name, long dflt) {
   return v ? atol(v) : dflt;
 }
 const long g_halo = env_l("TDE_HALO", 1);                 // 0: never take the halo path (A/B)
-const long g_halo_min_m = env_l("TDE_HALO_MIN_M", 16384); // output pixels (N*H*W) from which it pays
+const long g_halo_min_m = tde_env_pos("TDE_HALO_MIN_M", 16384); // output pixels (N*H*W) from which it pays
 const long g_halo_nw = env_l("TDE_HALO_NW", 0);           // force 4 or 8 waves per block
-const long g_halo_lds = env_l("TDE_HALO_LDS_KB", 150) << 10;
-const long g_halo_minch = env_l("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
+const long g_halo_lds = tde_env_pos("TDE_HALO_LDS_KB", 150) << 10;
+const long g_halo_minch = tde_env_pos("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
 
 int lds_stride(int cc) {   // smallest row stride (u16) >= cc whose 16-byte count is 2 mod 4
   int s = cc;

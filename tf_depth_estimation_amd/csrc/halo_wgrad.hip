@@ -211,8 +211,8 @@ long env_hwg(const char* name, long dflt) {
   return v ? std::atol(v) : dflt;
 }
 const long g_hwg = env_hwg("TDE_HWG", 1);                 // 0: never (A/B)
-const long g_hwg_blocks = env_hwg("TDE_HWG_BLOCKS", 768);  // grid size to aim for
-const long g_hwg_min_m = env_hwg("TDE_HWG_MIN_M", 16384);
+const long g_hwg_blocks = tde_env_pos("TDE_HWG_BLOCKS", 768);  // grid size to aim for
+const long g_hwg_min_m = tde_env_pos("TDE_HWG_MIN_M", 16384);
 const long g_hwg_diag = env_hwg("TDE_HWG_DIAG", 0);
 const long g_hwg_min_items = env_hwg("TDE_HWG_MIN_ITEMS", 25);
 

@@ -378,8 +378,8 @@ struct WgPlan {
 
 // pixels per thread lane at least: 2 (config-2 step, scripts/layer_profile.py: disp2/3/4 backward 50/42/40 ->
 // 41/32/27 us against 8; disp1 unchanged) -- more blocks for the low-resolution heads
-static const long g_head_ppl = []() { const char* v = getenv("TDE_HEAD_PPL"); return v ? atol(v) : 2L; }();
-static const long g_head_blocks = []() { const char* v = getenv("TDE_HEAD_BLOCKS"); return v ? atol(v) : 2048L; }();
+static const long g_head_ppl = tde_env_pos("TDE_HEAD_PPL", 2);
+static const long g_head_blocks = tde_env_pos("TDE_HEAD_BLOCKS", 2048);
 
 WgPlan wg_plan(const tde_conv_desc_t* d) {
   WgPlan w;

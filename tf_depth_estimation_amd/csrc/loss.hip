@@ -371,7 +371,8 @@ int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int cof
 
 // blocks per scale at most: every block ends in two fp64 atomics on the same two accumulators
 // (rocprofv3, config 2: 4096 -> 61 us, 512 -> 38 us, 128 -> 30 us per step)
-static const long g_pyr_maxb = []() { const char* v = getenv("TDE_PYR_MAXB"); return v ? atol(v) : 128L; }();
+// (TDE_PYR_MAXB tuning knob; a missing, non-numeric or non-positive value means the default)
+static const long g_pyr_maxb = tde_env_pos("TDE_PYR_MAXB", 128);
 
 int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
@@ -381,8 +382,13 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   for (int s = 0; s < a->nscales; ++s) {
     TDE_CHECK_ARG(a->pred[s] && a->grad[s] && (a->H >> s) > 0 && (a->W >> s) > 0);
     TDE_CHECK_ARG(a->l1_w[s] == 0.f || (a->label && a->H % (1 << s) == 0 && a->W % (1 << s) == 0));
+    // compute_smooth_loss takes reduce_mean over dx2 / dy2, which are empty below 3 rows / columns (the
+    // reference's value is NaN there): same contract as tde_loss_smooth2
+    TDE_CHECK_ARG(a->smooth_w[s] == 0.f || ((a->H >> s) >= 3 && (a->W >> s) >= 3));
+    // the kernel's element offsets loc * cs + co assume 0 <= co < cs for every view
+    TDE_CHECK_ARG(a->pred_co[s] >= 0 && a->pred_co[s] < a->pred_cs[s] && a->g_co[s] >= 0 && a->g_co[s] < a->g_cs[s]);
     long nbk = ew_grid((long)a->N * (a->H >> s) * (a->W >> s));
-    if (nbk > g_pyr_maxb) nbk = g_pyr_maxb;
+    nbk = nbk > g_pyr_maxb ? g_pyr_maxb : (nbk < 1 ? 1 : nbk);
     P.bstart[s + 1] = P.bstart[s] + (int)nbk;
   }
   for (int s = a->nscales; s < TDE_MAX_SCALES; ++s) P.bstart[s + 1] = P.bstart[s];

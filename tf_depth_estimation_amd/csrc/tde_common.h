@@ -23,6 +23,15 @@ static inline int tde_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 static inline char* tde_ws_body(void* ws) { return static_cast<char*>(ws); }
 
+// Tuning knob that must be positive (tile counts, chunk sizes, block caps): a missing, non-numeric, zero or
+// negative value means the default, so a bad setting can neither divide by zero nor empty a grid.
+#include <cstdlib>
+static inline long tde_env_pos(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  const long x = v ? std::atol(v) : 0L;
+  return x > 0 ? x : dflt;
+}
+
 // Raw buffer resource over n floats (byte range clamped below 2^31 so OOB is always out of range;
 // 0x00020000 = DATA_FORMAT 32 for gfx9-family raw buffers).  An access at byte offset OOB reads zero:
 // branch-free predicated loads.
