@@ -241,9 +241,10 @@ def main():
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--math", default="bf16x6r", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r"],
+    ap.add_argument("--math", default="fp16x3", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r", "fp16x3"],
                     help="conv arithmetic (include/tde.h tde_set_conv_math): exact fp32 MFMA, bf16x3 split "
-                         "precision, or the fp32-accurate 3-way bf16 split (LDS-staged / register-split)")
+                         "precision, the fp32-accurate 3-way bf16 split (LDS-staged / register-split) or the "
+                         "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
     ap.add_argument("--adam-overlap", action="store_true",
@@ -322,14 +323,16 @@ def main():
 
     if rank == 0:
         if args.math != "fp32":
-            # 3 or 6 bf16 MFMAs per fp32 product: the algorithmic fp32 FLOPs are counted once and priced
-            # against the dense bf16 MFMA peak divided by the MFMAs per product (the rate at which this
-            # arithmetic can retire fp32 products), so frac = fraction of the bf16 MFMA pipe doing useful work
-            per = 3 if args.math == "bf16x3" else 6
-            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> (conv fwd+dgrad+wgrad, {args.math}: "
-                           f"{per} x v_mfma_f32_16x16x32_bf16 per fp32 product)")
+            # 3 or 6 bf16/fp16 MFMAs per fp32 product: the algorithmic fp32 FLOPs are counted once and priced
+            # against the dense bf16/fp16 MFMA peak (the same rate) divided by the MFMAs per product (the rate
+            # at which this arithmetic can retire fp32 products), so frac = fraction of the matrix pipe doing
+            # useful work
+            per = 6 if args.math in ("bf16x6", "bf16x6r") else 3
+            ins = "v_mfma_f32_16x16x32_f16" if args.math == "fp16x3" else "v_mfma_f32_16x16x32_bf16"
+            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> + halo_conv_kernel (conv fwd+dgrad+wgrad, "
+                           f"{args.math}: {per} x {ins} per fp32 product)")
             peak = round(BF16_MFMA_PEAK / per, 1)
-            peak_note = f"dense bf16 MFMA peak {BF16_MFMA_PEAK} TFLOP/s / {per} MFMAs per fp32 product"
+            peak_note = f"dense bf16/fp16 MFMA peak {BF16_MFMA_PEAK} TFLOP/s / {per} MFMAs per fp32 product"
         else:
             kernel_name, peak = "igemmx_kernel<0,...> (conv fwd+dgrad+wgrad, fp32 MFMA 16x16x4)", FP32_MFMA_PEAK_TFLOPS
             peak_note = "dense fp32 MFMA peak"

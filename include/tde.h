@@ -31,7 +31,11 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 3
+#define TDE_ABI_VERSION 4
+
+/* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
+ * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
+#define TDE_BOUND_SLOTS 16
 
 typedef enum {
   TDE_OK = 0,
@@ -52,6 +56,16 @@ typedef struct {
   int w_cin;               /* input channels of the weight tensor (<= C); rows ci >= w_cin are zero */
   int x_cstride, x_coff;   /* channel view of x (and of dx) */
   int y_cstride, y_coff;   /* channel view of y (and of dy) */
+  /* Optional operand bounds for conv math 4 (fp16x3; ignored by the other modes): device pointers to
+   * TDE_BOUND_SLOTS floats whose maximum is >= max|.| of the operand read through the x view, the y view,
+   * and of the weights (a single bound: slot 0, the others 0).  The split
+   * scales an operand by 2^(14 - e) (e = frexp exponent of its bound) so it fits fp16 with full precision
+   * down to 2^-16 of the bound.  NULL: x / y operands are split unscaled (full precision for
+   * 2^-3 <= |v| < 2^15: activations, images) and weights by 2^8 (|w| < 256).  Gradient operands (dy of a
+   * conv, dy_big of a deconv) must carry a bound -- tde_bn_bwd writes one (dz_absmax). */
+  const float* x_absmax;
+  const float* y_absmax;
+  const float* w_absmax;
 } tde_conv_desc_t;
 
 int tde_abi_version(void);
@@ -76,7 +90,10 @@ uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
  *       of order <= 2^-14 on v_mfma_f32_16x16x32_bf16, fp32 accumulation (dropped terms < 2^-21 of
  *       |x*y|), split once at LDS staging;
  *   3 = bf16x6 split per fragment in registers (fp32 LDS image); tiles narrower than 64 columns run
- *       mode 0.  DEFAULT: held to the same parity bars as mode 0 and the fastest. */
+ *       mode 0.  Held to the same parity bars as mode 0;
+ *   4 = fp16x3: each operand scaled by a power of two (see x_absmax above) and split into fp16 hi + lo
+ *       (11 + 11 significant bits), products hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_f16 with fp32
+ *       accumulation (<= ~3 * 2^-22 relative per product), half the MFMAs of bf16x6.  DEFAULT. */
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
@@ -182,10 +199,14 @@ int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps,
 int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const float* moving_mean,
                 const float* moving_var, const float* beta, float eps, float* w_out, float* bias_out,
                 void* stream);
-/* dz = d(BN+ReLU)/dz given dy (view); dbeta = sum(dy * relu'); accumulate_dbeta adds to dbeta. */
+/* dz = d(BN+ReLU)/dz given dy (view); dbeta = sum(dy * relu'); accumulate_dbeta adds to dbeta.
+ * dz_absmax (nullable): TDE_BOUND_SLOTS device floats whose max is raised to max|dz| (atomic max; the caller
+ * zeroes them first) -- the bound of dz as the gradient operand of the conv backward in conv math 4
+ * (tde_conv_desc_t.y_absmax). */
 int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd,
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,
-               float* dbeta, int accumulate_dbeta, int relu, void* ws, size_t ws_bytes, void* stream);
+               float* dbeta, int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes,
+               void* stream);
 
 /* SyncBN (BatchNorm over the batch of ALL data-parallel replicas), in two phases around
  * the caller's all-reduce of `sums` (fp64 [2][C]):
@@ -206,7 +227,8 @@ int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const doubl
 int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean,
                          const float* save_invstd, const float* beta, const float* dy, int dy_cstride, int dy_coff,
                          const double* global_sums, const double* local_sums, float* dz, float* dbeta,
-                         int accumulate_dbeta, int relu, void* ws, size_t ws_bytes, void* stream);
+                         int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes,
+                         void* stream);
 
 /* ---------------------------------------------------------------- legacy resizes
  * resize_like -> tf.image.resize_nearest_neighbor (nets_optflow_depth.py:11-16),

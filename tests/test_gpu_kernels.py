@@ -100,11 +100,12 @@ CONV_CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["fp32", "bf16x3", "bf16x6", "bf16x6r"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["fp32", "bf16x3", "bf16x6", "bf16x6r", "fp16x3"])
 def conv_tol(request, L):
-    """Conv arithmetic mode (include/tde.h tde_set_conv_math) -> tolerance: exact fp32 MFMA and the
-    exact-split bf16x6 modes (dropped terms < 2^-21 per product) 1e-5; bf16x3 (~2^-16 per product,
-    fp32 accumulation) 1e-4 relative-to-max."""
+    """Conv arithmetic mode (include/tde.h tde_set_conv_math) -> tolerance: exact fp32 MFMA, the
+    exact-split bf16x6 modes (dropped terms < 2^-21 per product) and fp16x3 (<= ~3 * 2^-22 per product; the
+    O(1) test operands need no bound) 1e-5; bf16x3 (~2^-16 per product, fp32 accumulation) 1e-4
+    relative-to-max."""
     lib = L.load()
     prev = lib.tde_get_conv_math()
     L.check(lib.tde_set_conv_math(request.param))
@@ -159,6 +160,58 @@ DECONV_CASES = [
     (2, 2, 2, 512, 512, 3),
     (1, 12, 16, 256, 128, 3),
 ]
+
+
+F16_SCALE_CASES = [
+    # N, H, W, C, K, k, s: implicit GEMM (split-K), skinny, halo (FWD/DGRAD), halo WGRAD
+    (4, 24, 32, 256, 128, 3, 1),
+    (8, 3, 4, 512, 512, 3, 1),
+    (2, 96, 128, 32, 32, 7, 1),
+    (2, 13, 17, 32, 64, 5, 2),
+]
+
+
+@pytest.mark.parametrize("case", F16_SCALE_CASES)
+@pytest.mark.parametrize("mag", [1e-9, 3e4])
+def test_conv_fp16x3_operand_bounds(L, case, mag):
+    """fp16x3 (math 4) with operands far outside fp16's comfortable range -- gradients of ~1e-9 (all below
+    fp16's smallest normal) and activations of ~3e4 (near its overflow) -- and weights at 1e-3 scale: with
+    their bounds in the descriptor (x_absmax / y_absmax / w_absmax) every GEMM meets the 1e-5 bar of the other
+    exact modes; the power-of-two operand scaling is undone exactly."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, H, W, C, K, k, s = case
+    OH, pt, _ = T.same_pad(H, k, s)
+    OW, pl, _ = T.same_pad(W, k, s)
+    x = rnd(N, H, W, C, seed=31) * mag
+    w = rnd(k, k, C, K, seed=32) * 1e-3
+    dy = rnd(N, OH, OW, K, seed=33) * mag
+    bounds = torch.zeros(3, L.BOUND_SLOTS, device="cuda")   # one value per bound, in a middle slot
+    bounds[:, 5] = torch.tensor([x.abs().max().item(), dy.abs().max().item(), w.abs().max().item()])
+    d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
+                  w_cin=C, x_cstride=C, x_coff=0, y_cstride=K, y_coff=0)
+    d.x_absmax, d.y_absmax, d.w_absmax = bounds[0].data_ptr(), bounds[1].data_ptr(), bounds[2].data_ptr()
+    ws = ws_for(L, d)
+    prev = lib.tde_get_conv_math()
+    L.check(lib.tde_set_conv_math(4))
+    try:
+        gx, gw, gdy = dev(x), dev(w), dev(dy)
+        gy = torch.empty(N, OH, OW, K, device="cuda")
+        gdx, gdw = torch.empty(N, H, W, C, device="cuda"), torch.empty(k, k, C, K, device="cuda")
+        L.check(lib.tde_conv2d_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(gy), 0, L.ptr(ws), ws.numel() * 4, st))
+        L.check(lib.tde_conv2d_bwd_data(ctypes.byref(d), L.ptr(gdy), L.ptr(gw), L.ptr(gdx), 0, L.ptr(ws),
+                                        ws.numel() * 4, st))
+        L.check(lib.tde_conv2d_bwd_filter(ctypes.byref(d), L.ptr(gx), L.ptr(gdy), L.ptr(gdw), 0, L.ptr(ws),
+                                          ws.numel() * 4, st))
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.tde_set_conv_math(prev))
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = T.conv2d_same(xr, wr, s)
+    yr.backward(dy)
+    for got, ref, what in ((gy, yr, "fwd"), (gdx, xr.grad, "dgrad"), (gdw, wr.grad, "wgrad")):
+        sc = ref.abs().max().item()   # relative to max (close()'s absolute floor would hide 1e-9 data)
+        close(got.double() / sc, ref / sc, what=f"fp16x3 {what}")
 
 
 @pytest.mark.parametrize("case", DECONV_CASES)
@@ -397,9 +450,11 @@ def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     gdy[:, yco:yco + C] = dev(dy)
     dz = torch.empty(M, C, device="cuda")
     dbeta = torch.zeros(C, device="cuda")
+    amax = torch.zeros(L.BOUND_SLOTS, device="cuda")
     L.check(lib.tde_bn_bwd(M, C, L.ptr(gz), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(gb), L.ptr(gdy), ycs, yco, L.ptr(dz),
-                           L.ptr(dbeta), 1, 1, L.ptr(ws), ws.numel() * 4, st))
+                           L.ptr(dbeta), 1, 1, L.ptr(amax), L.ptr(ws), ws.numel() * 4, st))
     close(dz, zr.grad.reshape(M, C), tol=5e-5, what="bn dz")
+    assert amax.max().item() == dz.abs().max().item(), "dz_absmax: max|dz| over the slots"
     dbr = (dy * (yr.detach().reshape(M, C) > 0)).sum(0)
     close(dbeta, dbr, tol=5e-5, what="dbeta")
     yi = torch.zeros(M, ycs, device="cuda")
@@ -577,7 +632,7 @@ def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
     dz = torch.empty(M, C, device="cuda")
     db = torch.empty(C, device="cuda")
     L.check(lib.tde_bn_bwd(M, C, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(dy), C, 0, L.ptr(dz),
-                           L.ptr(db), 0, 1, L.ptr(ws), ws.numel() * 4, st))
+                           L.ptr(db), 0, 1, None, L.ptr(ws), ws.numel() * 4, st))
     # two replicas
     parts = [(0, M1), (M1, M2)]
     sums = [torch.empty(2 * C, dtype=torch.float64, device="cuda") for _ in parts]
@@ -604,9 +659,11 @@ def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
     gb = ls[0] + ls[1]
     dz2 = torch.empty(M, C, device="cuda")
     db2 = torch.empty(2, C, device="cuda")
+    amax2 = torch.zeros(L.BOUND_SLOTS, device="cuda")
     for k, (r0, m) in enumerate(parts):
         L.check(lib.tde_bn_bwd_from_sums(m, C, M, L.ptr(z[r0:]), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta),
                                          L.ptr(dy[r0:]), C, 0, L.ptr(gb), L.ptr(ls[k]), L.ptr(dz2[r0:]), L.ptr(db2[k]),
-                                         0, 1, L.ptr(ws), ws.numel() * 4, st))
+                                         0, 1, L.ptr(amax2), L.ptr(ws), ws.numel() * 4, st))
     close(dz2, dz, what="dz")
+    assert amax2.max().item() == dz2.abs().max().item(), "dz_absmax over both replicas' calls"
     close(db2[0] + db2[1], db, tol=1e-6, what="dbeta")

@@ -63,7 +63,7 @@ C4_TERMS = {
 }
 
 
-@pytest.fixture(params=[0, 3], ids=["fp32", "bf16x6r"])
+@pytest.fixture(params=[0, 3, 4], ids=["fp32", "bf16x6r", "fp16x3"])
 def step_math(request):
     from tf_depth_estimation_amd import _lib
     lib = _lib.load()

@@ -12,10 +12,11 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
+BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
-CONV_MATH = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "bf16x6r": 3}
+CONV_MATH = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "bf16x6r": 3, "fp16x3": 4}
 
 c_int, c_float, c_size_t, c_void_p, c_double_p = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p,
                                                   ctypes.POINTER(ctypes.c_double))
@@ -24,7 +25,8 @@ c_int, c_float, c_size_t, c_void_p, c_double_p = (ctypes.c_int, ctypes.c_float, 
 class ConvDesc(ctypes.Structure):
     """Mirror of tde_conv_desc_t (include/tde.h)."""
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "OH", "OW", "K", "KH", "KW", "stride", "pad_top",
-                                     "pad_left", "w_cin", "x_cstride", "x_coff", "y_cstride", "y_coff")]
+                                     "pad_left", "w_cin", "x_cstride", "x_coff", "y_cstride", "y_coff")] + \
+               [("x_absmax", c_void_p), ("y_absmax", c_void_p), ("w_absmax", c_void_p)]
 
 
 P = c_void_p
@@ -99,12 +101,12 @@ _SIGS = {
     "tde_bn_fwd_train": (c_int, [c_int, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, c_int, c_int, c_int,
                                  P, c_size_t, P]),
     "tde_bn_fwd_infer": (c_int, [c_int, c_int, P, P, c_float, P, P, P, c_int, c_int, c_int, P]),
-    "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, c_size_t, P]),
+    "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, P, c_size_t, P]),
     "tde_bn_sums": (c_int, [c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P]),
     "tde_bn_fwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, c_float, c_float, c_int, P, P, P, P, P,
                                      c_int, c_int, c_int, P]),
     "tde_bn_bwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int,
-                                     c_int, P, c_size_t, P]),
+                                     c_int, P, P, c_size_t, P]),
     "tde_resize_nearest_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_nearest_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_bilinear_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),

@@ -176,16 +176,34 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float
   }
 }
 
+// max|dz| of a block's values into one of the TDE_BOUND_SLOTS slots of amax (slot = block % slots, so that
+// at most blocks / 16 atomics contend for an address; a bound is the max of its slots): the fp16x3 conv
+// math's operand bound of the gradient (tde_conv_desc_t.y_absmax).  uint order = float order for
+// non-negative floats; fmaxf from 0 keeps NaN out of the bound.  Every thread of the block must call it.
+__device__ __forceinline__ void block_absmax_to(float m, float* amax) {
+  __shared__ float wmx[4];
+  if (amax == nullptr) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]));
+    if (m > 0.f) atomicMax(reinterpret_cast<unsigned*>(amax + (blockIdx.x & (TDE_BOUND_SLOTS - 1))), __float_as_uint(m));
+  }
+}
+
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const float* z, const float* dy, int dycs,
                                                            int dyco, const float* mean, const float* invstd,
                                                            const float* beta, const float* coef, int relu,
-                                                           float* dz, int rows_per_block) {
+                                                           float* dz, int rows_per_block, float* amax) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
-  if (cq < 256 && threadIdx.x >= rstep * cq) return;
+  const bool active = cq >= 256 || threadIdx.x < rstep * cq;
   const int rl = cq >= 256 ? 0 : threadIdx.x / cq;
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
-  for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); qq < cq; qq += (cq >= 256 ? 256 : cq)) {
+  float mx = 0.f;
+  for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); active && qq < cq; qq += (cq >= 256 ? 256 : cq)) {
     const int c = 4 * qq;
     const f4 mu = *reinterpret_cast<const f4*>(mean + c);
     const f4 is = *reinterpret_cast<const f4*>(invstd + c);
@@ -202,10 +220,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
         const float xh = (zv[j] - mu[j]) * is[j];
         const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
         o[j] = is[j] * (g - mg[j] - xh * mgx[j]);
+        mx = fmaxf(mx, fabsf(o[j]));
       }
       *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
     }
   }
+  block_absmax_to(mx, amax);
 }
 
 // SyncBN second phase: batch statistics from per-channel sums over ALL replicas (count Mt).
@@ -303,7 +323,7 @@ __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const f
 __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const float* z, const float* mean,
                                                            const float* invstd, const float* beta, const float* dy,
                                                            int dycs, int dyco, float* dz, float* dbeta, int acc,
-                                                           int relu) {
+                                                           int relu, float* amax) {
   __shared__ double sh[2][4][4];
   __shared__ float s_mg[4], s_mgx[4];
   const int c = blockIdx.x * 4;
@@ -344,16 +364,21 @@ __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const f
     if (dbeta) dbeta[c + j] = acc ? dbeta[c + j] + (float)s : (float)s;
   }
   __syncthreads();
+  float mx = 0.f;
 #pragma unroll
   for (int i = 0; i < SMALL_R; ++i) {
     const int r = threadIdx.x + 256 * i;
     if (r < M) {
       f4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
+      for (int j = 0; j < 4; ++j) {
+        o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
+        mx = fmaxf(mx, fabsf(o[j]));
+      }
       *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
     }
   }
+  block_absmax_to(mx, amax);
 }
 
 __global__ void __launch_bounds__(256) bn_infer_kernel(int M, int C, const float* z, const float* mm,
@@ -500,14 +525,14 @@ int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const floa
 
 int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd, const float* beta,
                const float* dy, int dy_cstride, int dy_coff, float* dz, float* dbeta, int accumulate_dbeta, int relu,
-               void* ws, size_t ws_bytes, void* stream) {
+               float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && save_mean && save_invstd && beta && dy && dz);
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (M <= BN_SMALL_M) {
     hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M, C, z, save_mean, save_invstd, beta, dy,
-                       dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu);
+                       dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax);
     return tde_launch_status();
   }
   const BnChunks pp = bn_chunk_plan(M, C, 1);
@@ -519,7 +544,7 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
                      0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb);
+                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
   return tde_launch_status();
 }
 
@@ -562,8 +587,8 @@ int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const doubl
 
 int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean, const float* save_invstd,
                          const float* beta, const float* dy, int dy_cstride, int dy_coff, const double* global_sums,
-                         const double* local_sums, float* dz, float* dbeta, int accumulate_dbeta, int relu, void* ws,
-                         size_t ws_bytes, void* stream) {
+                         const double* local_sums, float* dz, float* dbeta, int accumulate_dbeta, int relu,
+                         float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(M > 0 && M_total >= M && C > 0 && C % 4 == 0 && z && save_mean && save_invstd && beta && dy && dz &&
                 global_sums && local_sums);
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
@@ -574,7 +599,7 @@ int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float
                      local_sums, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb);
+                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
   return tde_launch_status();
 }
 

@@ -43,6 +43,9 @@ struct ConvArgs {
   // inference epilogue (FWD / DGRAD outputs only; accumulate == 0): v = conv + bias[col], then ReLU
   // (BN folded into the weights, tde_conv2d_fwd_bias_act); bias null and relu 0 = plain conv
   const float* bias; int relu;
+  // fp16x3 (math 4) operand bounds |x| <= *bound of the x view, the y view and the weights (null: unscaled
+  // x / y, fixed weight scale; split_math.h)
+  const float* xmax; const float* ymax; const float* wmax;
 };
 
 // The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
@@ -193,6 +196,8 @@ template <int ROWS>
 struct ImgSel<2, ROWS> { using type = Img6<ROWS>; using T = u16; };
 template <int ROWS>
 struct ImgSel<3, ROWS> { using type = Img1<ROWS>; using T = float; };
+template <int ROWS>
+struct ImgSel<4, ROWS> { using type = Img1<ROWS>; using T = float; };
 
 // MATH 0: exact fp32 (2 x 4 v_mfma_f32_16x16x4_f32 per 32-deep k-tile); MATH 1: bf16x3.
 template <int MATH, int BM, int BN>
@@ -219,6 +224,13 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+
+  // fp16x3 operand scales (powers of two): A = x (FWD, WGRAD) or dy (DGRAD), B = w (FWD, DGRAD) or dy (WGRAD)
+  float sA = 1.f, sB = 1.f;
+  if constexpr (MATH == 4) {
+    sA = f16x3_scale(MODE == MODE_DGRAD ? p.ymax : p.xmax, 1.f);
+    sB = MODE == MODE_WGRAD ? f16x3_scale(p.ymax, 1.f) : f16x3_scale(p.wmax, F16X3_WSCALE);
+  }
 
   int M, Nn, Kd;
   DgClass g{};
@@ -425,6 +437,33 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
+    } else if constexpr (MATH == 4) {
+      // fp16x3: fp32 LDS image as MATH 3, each fragment scaled and split into fp16 hi / lo in registers
+      f4 fa[TM][2], fb[TN][2];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        fa[a][0] = IA::frag(A, wrow0 + a * 16 + r16, 4 * q);
+        fa[a][1] = IA::frag(A, wrow0 + a * 16 + r16, 16 + 4 * q);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        fb[b][0] = IB::frag(Bm, wcol0 + b * 16 + r16, 4 * q);
+        fb[b][1] = IB::frag(Bm, wcol0 + b * 16 + r16, 16 + 4 * q);
+      }
+      issue();
+      h8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) split8x2h(fa[a][0], fa[a][1], sA, ah[a], al[a]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) split8x2h(fb[b][0], fb[b][1], sB, bh[b], bl[b]);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
     } else if constexpr (MATH == 2 || MATH == 3) {
       bf8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
       if constexpr (MATH == 2) {
@@ -533,6 +572,15 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         if (++kt >= kt1) break;
       }
     }
+  }
+
+  if constexpr (MATH == 4) {
+    // undo the operand scales (a power of two: exact) before any statistics, partial or store
+    const float inv = 1.f / (sA * sB);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
   }
 
   // ---- batch-norm statistics of the output tile (slim.batch_norm after this conv, bn.hip): per-channel
@@ -940,11 +988,12 @@ static long env_long(const char* name, long dflt) {
   const char* v = getenv(name);
   return v ? atol(v) : dflt;
 }
-// 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6 (process-wide, see tde_set_conv_math; TDE_CONV_MATH sets the initial
-// mode for A/B runs).  Default 3: the exact three-way split, the fastest mode within the parity bars.
+// 0 fp32 MFMA, 1 bf16x3, 2/3 bf16x6, 4 fp16x3 (process-wide, see tde_set_conv_math; TDE_CONV_MATH sets the
+// initial mode for A/B runs).  Default 4: the scaled two-way fp16 split, the fastest mode within the parity
+// bars (half the MFMAs of bf16x6 at the same accuracy class).
 static int g_conv_math = []() {
-  const long m = env_long("TDE_CONV_MATH", 3);
-  return (int)(m >= 0 && m <= 3 ? m : 3);
+  const long m = env_long("TDE_CONV_MATH", 4);
+  return (int)(m >= 0 && m <= 4 ? m : 4);
 }();
 static const long g_split_target = tde_env_pos("TDE_SPLIT_TARGET", 512);   // blocks to aim for
 static const long g_split_minkt = tde_env_pos("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
@@ -1073,12 +1122,18 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl) {
   return b;
 }
 
-// Halo path workspace: split weights + BN partials.  Sized for the bf16x6 math whatever the current mode
+// Halo path workspace: split weights + BN partials.  Sized for both split maths whatever the current mode
 // (a caller may size once and switch tde_set_conv_math later).
 static size_t halo_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
-  HaloPlan hp;
-  if (mode == MODE_WGRAD || !halo_plan(d, mode == MODE_FWD ? 0 : 1, 3, hp)) return 0;
-  return hp.wbytes + (bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0);
+  // the larger of the bf16x6 and fp16x3 plans (planes and LDS budget differ, so may the tile shape)
+  size_t b = 0;
+  for (int math = 3; math <= 4; ++math) {
+    HaloPlan hp;
+    if (mode == MODE_WGRAD || !halo_plan(d, mode == MODE_FWD ? 0 : 1, math, hp)) continue;
+    const size_t m = hp.wbytes + (bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0);
+    b = m > b ? m : b;
+  }
+  return b;
 }
 
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
@@ -1105,7 +1160,10 @@ static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
 static const long g_math3_min_bn = env_long("TDE_MATH3_MIN_BN", 64);
 static const long g_narrow_math = env_long("TDE_NARROW_MATH", 0);   // math of those narrow tiles (0 or 2)
 static const long g_math3_wgrad_min_bn = env_long("TDE_MATH3_WGRAD_MIN_BN", 64);   // the same for WGRAD alone
+// fp16x3 (math 4): split cost per fragment ~half of bf16x6's; narrow-tile threshold measured separately
+static const long g_math4_min_bn = env_long("TDE_MATH4_MIN_BN", 16);
 static int tile_math(int bn, int mode = -1) {
+  if (g_conv_math == 4) return bn < g_math4_min_bn ? 0 : 4;
   const long lim = mode == MODE_WGRAD ? g_math3_wgrad_min_bn : g_math3_min_bn;
   return (g_conv_math == 3 && bn < lim) ? (int)g_narrow_math : g_conv_math;
 }
@@ -1118,6 +1176,8 @@ static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   const int math = tile_math(BN, MODE);
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  else if (math == 4 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
+  else if (math == 4) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 3 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
   else if (math == 3) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (pf == 2) hipLaunchKernelGGL((igemmx_kernel<0, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
@@ -1194,6 +1254,7 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
   a.xcs = d.x_cstride; a.xco = d.x_coff; a.ycs = d.y_cstride; a.yco = d.y_coff;
   a.fC = make_fdiv(d.C); a.fK = make_fdiv(d.K); a.fKW = make_fdiv(d.KW); a.fOW = make_fdiv(d.OW);
   a.fOHW = make_fdiv(d.OH * d.OW);
+  a.xmax = d.x_absmax; a.ymax = d.y_absmax; a.wmax = d.w_absmax;
   return a;
 }
 
@@ -1292,6 +1353,9 @@ static void launch_bwd2_cfg(const Plan& p1, const ConvArgs& a1, const Plan& p2, 
                        p1.gy, p2.gx, p2.gy, nd);
   else if (math == 3)
     hipLaunchKernelGGL((igemm_bwd2_kernel<3, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
+                       p1.gy, p2.gx, p2.gy, nd);
+  else if (math == 4)
+    hipLaunchKernelGGL((igemm_bwd2_kernel<4, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
                        p1.gy, p2.gx, p2.gy, nd);
   else
     hipLaunchKernelGGL((igemm_bwd2_kernel<0, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
@@ -1409,7 +1473,7 @@ static bool bn_ok(const tde_bn_train_t* bn, int C) {
 extern "C" {
 
 int tde_set_conv_math(int mode) {
-  if (mode < 0 || mode > 3) return TDE_ERR_ARG;
+  if (mode < 0 || mode > 4) return TDE_ERR_ARG;
   g_conv_math = mode;
   return TDE_OK;
 }

@@ -7,6 +7,7 @@
 struct HaloPlan {
   int ok;
   int mode;               // 0 FWD, 1 DGRAD (of a stride-1 conv)
+  int planes;             // split planes: 3 bf16 (bf16x6, math 2/3), 2 fp16 (fp16x3, math 4)
   int NW, TN;             // waves per block (pixel rows 2*NW), 16-column MFMA fragments per wave
   int HWd, HP;            // halo width (16 + KW - 1), halo pixels
   int CC, nch, SA;        // channels per chunk (multiple of 8), chunks, LDS row stride (u16)

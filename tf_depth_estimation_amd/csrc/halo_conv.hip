@@ -48,6 +48,8 @@ struct HaloArgs {
   double* bnp;
   const float* bias;   // folded-BN inference epilogue (accumulate == 0); null / 0: plain conv
   int relu;
+  const float* inmax;  // fp16x3 (math 4): bounds of the input view and of the weights (split_math.h)
+  const float* wmax;
 };
 
 // Split weights, one contiguous B tile per (k-step g, column tile ct):
@@ -57,9 +59,12 @@ struct HaloArgs {
 //   FWD  : B[(tap, c)][col] = w[tap][c][col]                     (w [KH][KW][wcin][K], c < wcin)
 //   DGRAD: B[(tap, k)][col] = w[ntap - 1 - tap][col][k]          (col = dx channel < wcin, k < K)
 // The tile is copied byte-for-byte into its LDS ring slot by LDS-DMA, so this IS the LDS image.
+//   planes 3: bf16x6 hi / mid / lo (split3); planes 2: fp16x3 hi / lo of w * f16x3_scale(wmax) (split4x2h)
 __global__ void __launch_bounds__(256) halo_wprep_kernel(const float* __restrict__ w, u16* __restrict__ wp, int mode,
                                                          long total, int steps, int CC, int ntap, int Cred,
-                                                         int Ncols, int NCP, int ncolt, int wcin, int K) {
+                                                         int Ncols, int NCP, int ncolt, int wcin, int K, int planes,
+                                                         const float* wmax) {
+  const float ws = planes == 2 ? f16x3_scale(wmax, F16X3_WSCALE) : 1.f;
   for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int rl = (int)(idx % LDB);
     long t = idx / LDB;
@@ -75,12 +80,19 @@ __global__ void __launch_bounds__(256) halo_wprep_kernel(const float* __restrict
       if (mode == 0) v = w[((long)tap * wcin + c) * K + col];
       else if (col < wcin) v = w[((long)(ntap - 1 - tap) * wcin + col) * K + c];
     }
-    unsigned h, m, l;
-    split3(v, h, m, l);
-    const long base = ((((long)g * ncolt + ct) * 3) * NCP + cl) * LDB + rl;
-    wp[base] = (u16)(h >> 16);
-    wp[base + (long)NCP * LDB] = (u16)(m >> 16);
-    wp[base + 2l * NCP * LDB] = (u16)(l >> 16);
+    const long base = ((((long)g * ncolt + ct) * planes) * NCP + cl) * LDB + rl;
+    if (planes == 2) {
+      const float x = v * ws;
+      const _Float16 h = (_Float16)x, l = (_Float16)(x - (float)h);
+      wp[base] = __builtin_bit_cast(u16, h);
+      wp[base + (long)NCP * LDB] = __builtin_bit_cast(u16, l);
+    } else {
+      unsigned h, m, l;
+      split3(v, h, m, l);
+      wp[base] = (u16)(h >> 16);
+      wp[base + (long)NCP * LDB] = (u16)(m >> 16);
+      wp[base + 2l * NCP * LDB] = (u16)(l >> 16);
+    }
   }
 }
 
@@ -96,11 +108,13 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
-template <int NW, int TN>
+// MATH 3: bf16x6 (three bf16 planes, 6 MFMAs per fragment pair); MATH 4: fp16x3 (two fp16 planes, 3 MFMAs)
+template <int NW, int TN, int MATH>
 __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  constexpr int PL = MATH == 4 ? 2 : 3;                      // planes
   constexpr int NT = 64 * NW, NCP = 16 * TN;
-  constexpr int BPL = NCP * LDB, BTILE = 3 * BPL;           // u16 per B tile
+  constexpr int BPL = NCP * LDB, BTILE = PL * BPL;          // u16 per B tile
   constexpr int NI = (BTILE * 2 + 1023) / 1024;             // 1-KiB DMA wave-instructions per tile
   constexpr int DI = (NI + NW - 1) / NW;                    // per wave (uniform: extra ones duplicate)
   constexpr int BSLOT = NI * 512;                           // u16 per ring slot (whole 1-KiB pieces)
@@ -111,7 +125,9 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
   const int col0 = ct * NCP;
   const int PLANE = p.HP * p.SA;
   u16* const As = lds;
-  u16* const Bs = lds + 3 * PLANE;
+  u16* const Bs = lds + PL * PLANE;
+  const float sIn = MATH == 4 ? f16x3_scale(p.inmax, 1.f) : 1.f;
+  const float sW = MATH == 4 ? f16x3_scale(p.wmax, F16X3_WSCALE) : 1.f;
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(p.in, (long)p.N * p.H * p.W * p.ics);
 
   // B tiles reach their ring slot by LDS-DMA (global_load_lds_dwordx4: each wave-instruction copies 1 KiB,
@@ -129,7 +145,7 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
     }
   };
 
-  // halo of channel chunk ch -> three bf16 planes [HP][SA]; 8 loads in flight per thread
+  // halo of channel chunk ch -> PL split planes [HP][SA]; 8 loads in flight per thread
   auto stage_a = [&](int ch) __attribute__((always_inline)) {
     const int nc4 = p.CC >> 2, total = p.HP * nc4;
     for (int base = 0; base < total; base += 8 * NT) {
@@ -148,12 +164,19 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
         const int idx = base + u * NT + tid;
         if (idx < total) {
           const int hp = fdiv(idx, p.fC4), c4 = idx - hp * nc4;
-          uint2 hi, mi, lo;
-          split4x3(v[u], hi, mi, lo);
           u16* d = As + hp * p.SA + 4 * c4;
-          *reinterpret_cast<uint2*>(d) = hi;
-          *reinterpret_cast<uint2*>(d + PLANE) = mi;
-          *reinterpret_cast<uint2*>(d + 2 * PLANE) = lo;
+          if constexpr (MATH == 4) {
+            h4 hi, lo;
+            split4x2h(v[u], sIn, hi, lo);
+            *reinterpret_cast<h4*>(d) = hi;
+            *reinterpret_cast<h4*>(d + PLANE) = lo;
+          } else {
+            uint2 hi, mi, lo;
+            split4x3(v[u], hi, mi, lo);
+            *reinterpret_cast<uint2*>(d) = hi;
+            *reinterpret_cast<uint2*>(d + PLANE) = mi;
+            *reinterpret_cast<uint2*>(d + 2 * PLANE) = lo;
+          }
         }
       }
     }
@@ -176,6 +199,30 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
     if (tap >= p.ntap) { tap = 0; cc = 0; }
     const int kh = fdiv(tap, p.fKW), kw = tap - kh * p.KW;
     const int toff = (kh * p.HWd + kw) * p.SA + cc;
+    if constexpr (MATH == 4) {
+      h8 ah[2], al[2], bh[TN], bl[TN];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const u16* src = As + (a ? arow1 : arow0) + toff;
+        ah[a] = *reinterpret_cast<const h8*>(src);
+        al[a] = *reinterpret_cast<const h8*>(src + PLANE);
+      }
+      const u16* bsrc = Bs + slot * BSLOT + r16 * LDB + 8 * q;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        bh[b] = *reinterpret_cast<const h8*>(bsrc + b * 16 * LDB);
+        bl[b] = *reinterpret_cast<const h8*>(bsrc + BPL + b * 16 * LDB);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
+      return;
+    }
     bf8 ah[2], am[2], al[2], bh[TN], bm[TN], bl[TN];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -226,6 +273,13 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
     }
   }
   vm_wait<0>();
+  if constexpr (MATH == 4) {
+    const float inv = 1.f / (sIn * sW);   // power of two: exact
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
+  }
 
   // ---- epilogue: acc[a][b][r] = out(pixel (y0 + 2*wv + a, x0 + 4q + r), column col0 + 16b + r16)
   bool rowok[2][4];
@@ -331,24 +385,31 @@ int lds_stride(int cc) {   // smallest row stride (u16) >= cc whose 16-byte coun
   return s;
 }
 
-template <int NW, int TN>
-void launch_t(const HaloPlan& hp, const HaloArgs& a, hipStream_t st) {
+template <int NW, int TN, int MATH>
+void launch_m(const HaloPlan& hp, const HaloArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_conv_kernel<NW, TN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&halo_conv_kernel<NW, TN, MATH>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((halo_conv_kernel<NW, TN>), dim3(hp.gx, hp.gy, hp.gz), dim3(64 * NW), hp.lds_bytes, st, a);
+  hipLaunchKernelGGL((halo_conv_kernel<NW, TN, MATH>), dim3(hp.gx, hp.gy, hp.gz), dim3(64 * NW), hp.lds_bytes, st,
+                     a);
+}
+template <int NW, int TN>
+void launch_t(const HaloPlan& hp, const HaloArgs& a, hipStream_t st) {
+  if (hp.planes == 2) launch_m<NW, TN, 4>(hp, a, st);
+  else launch_m<NW, TN, 3>(hp, a, st);
 }
 
 }  // namespace
 
 bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
   hp = HaloPlan{};
-  if (!g_halo || (math != 2 && math != 3) || d.stride != 1 || (mode != 0 && mode != 1)) return false;
+  if (!g_halo || (math != 2 && math != 3 && math != 4) || d.stride != 1 || (mode != 0 && mode != 1)) return false;
   if (d.OH != d.H || d.OW != d.W || (long)d.N * d.H * d.W < g_halo_min_m) return false;
   hp.mode = mode;
+  hp.planes = math == 4 ? 2 : 3;
   hp.KH = d.KH; hp.KW = d.KW;
   if (mode == 0) {
     hp.PT = d.pad_top; hp.PL = d.pad_left;
@@ -376,7 +437,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
   // chip (cnv2b at 16-row tiles is 96 blocks: 8-row tiles won by 1.4x).
   const int cp8 = (hp.Cv + 7) / 8 * 8;
   const int nws[2] = {8, 4};
-  const size_t btile = (size_t)3 * 16 * hp.TN * LDB * 2;                              // bytes
+  const size_t btile = (size_t)hp.planes * 16 * hp.TN * LDB * 2;                      // bytes
   const size_t ring = 3 * ((btile + 1023) / 1024 * 1024);
   double best_est = -1.0;
   for (int i = 0; i < 2; ++i) {
@@ -388,7 +449,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
       const int cc = ((cp8 + nch - 1) / nch + 7) / 8 * 8;
       if (nch > 1 && (cp8 + cc - 1) / cc < nch) continue;   // same chunking as a smaller nch
       const int sa = lds_stride(cc);
-      const size_t lds = (size_t)3 * hh * hp.HWd * sa * 2 + ring;
+      const size_t lds = (size_t)hp.planes * hh * hp.HWd * sa * 2 + ring;
       if (lds > (size_t)g_halo_lds) continue;
       ++tried;
       const int nchr = (cp8 + cc - 1) / cc;
@@ -415,7 +476,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
   hp.gy = tde_cdiv(d.H, 2 * hp.NW);
   hp.gz = d.N * hp.ncolt;
   hp.nparts = hp.gx * hp.gy * d.N;
-  hp.wbytes = ((size_t)hp.nch * hp.steps * 3 * hp.NcolsP * LDB * 2 + 255) / 256 * 256;
+  hp.wbytes = ((size_t)hp.nch * hp.steps * hp.planes * hp.NcolsP * LDB * 2 + 255) / 256 * 256;
   return true;
 }
 
@@ -426,7 +487,7 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
   long blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(halo_wprep_kernel, dim3((int)blocks), dim3(256), 0, st, w, wp, hp.mode, total, hp.steps, hp.CC,
-                     hp.ntap, hp.Cred, hp.Ncols, 16 * hp.TN, hp.ncolt, d.w_cin, d.K);
+                     hp.ntap, hp.Cred, hp.Ncols, 16 * hp.TN, hp.ncolt, d.w_cin, d.K, hp.planes, d.w_absmax);
   HaloArgs a{};
   a.N = d.N; a.H = d.H; a.W = d.W;
   a.HWd = hp.HWd; a.HP = hp.HP; a.CC = hp.CC; a.nch = hp.nch; a.SA = hp.SA; a.steps = hp.steps; a.ntap = hp.ntap;
@@ -435,6 +496,8 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
   a.ncolt = hp.ncolt; a.NcolsP = hp.NcolsP; a.accumulate = accumulate;
   a.fCC = make_fdiv(hp.CC); a.fKW = make_fdiv(hp.KW); a.fC4 = make_fdiv(hp.CC / 4); a.fHWd = make_fdiv(hp.HWd);
   a.in = in; a.out = out; a.wp = wp; a.bnp = bnp; a.bias = bias; a.relu = relu;
+  a.inmax = hp.mode == 0 ? d.x_absmax : d.y_absmax;
+  a.wmax = d.w_absmax;
   const int key = hp.NW * 10 + hp.TN;
   switch (key) {
     case 81: launch_t<8, 1>(hp, a, st); break;

@@ -41,3 +41,48 @@ __device__ __forceinline__ void split4x3(f4 v, uint2& hi, uint2& mi, uint2& lo) 
   lo = make_uint2(pack_hi16(l[0], l[1]), pack_hi16(l[2], l[3]));
 }
 
+
+// ---------------------------------------------------------------- fp16x3 (conv math 4)
+// Two-way fp16 split of a SCALED fp32 value x*s: hi = fp16_rne(x*s), lo = fp16_rne(x*s - hi).  hi carries
+// 11 significant bits, the exact remainder is rounded to another 11, so |x*s - hi - lo| <= 2^-22 |x*s| while
+// lo is a normal fp16 (|x*s| >= 2^-3), and <= 2^-25 absolute below that (fp16 subnormal half-quantum).  The
+// product keeps hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_f16 (fp32 accumulation): the dropped lo*lo
+// and the two split residuals are <= ~3 * 2^-22 of |x*y| (bf16x6: < 2^-21) at HALF the MFMAs of bf16x6.
+// fp16's range (max 65504) is what the power-of-two operand scale s handles: s = 2^(14 - e) puts an
+// operand with |x| <= bound (frexp exponent e) below 2^14, so nothing overflows and everything down to
+// 2^-16 of the bound keeps the full 22 bits; the accumulator is multiplied by 1/(s_a s_b) (exact).
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+// fixed scale of an operand with no bound: weights (|w| < 256 with full precision down to |w| ~ 5e-4)
+constexpr float F16X3_WSCALE = 256.f;
+
+__device__ __forceinline__ float f16x3_scale(const float* bound, float dflt) {
+  if (bound == nullptr) return dflt;
+  float m = bound[0];   // TDE_BOUND_SLOTS slots (one scalar load), the bound is their max
+#pragma unroll
+  for (int i = 1; i < TDE_BOUND_SLOTS; ++i) m = fmaxf(m, bound[i]);
+  int e;
+  (void)frexpf(m, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);   // 2^(14 - e) stays a finite normal float
+  return ldexpf(1.f, 14 - e);
+}
+
+__device__ __forceinline__ void split4x2h(f4 v, float s, h4& hi, h4& lo) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j] * s;
+    const _Float16 h = (_Float16)x;
+    hi[j] = h;
+    lo[j] = (_Float16)(x - (float)h);
+  }
+}
+
+// 8 consecutive-k fp32 values (two f4) -> hi / lo fp16x8 fragments
+__device__ __forceinline__ void split8x2h(f4 a, f4 b, float s, h8& hi, h8& lo) {
+  h4 h0, l0, h1, l1;
+  split4x2h(a, s, h0, l0);
+  split4x2h(b, s, h1, l1);
+  hi = h8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+  lo = h8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+}

@@ -232,11 +232,17 @@ class NetRun:
                 self.stats[i] = torch.empty((2, op.K), device=device, dtype=torch.float32)
             elif isinstance(op, ConvBN):
                 self.z[i] = None
+        # per-op bound max|dz| of the BN backward's output (tde_bn_bwd dz_absmax), the gradient operand bound
+        # of the conv backward in fp16x3 conv math (tde_conv_desc_t); zeroed at the start of every backward
+        self.absmax = torch.zeros((max(len(prog.spec.ops), 1), _lib.BOUND_SLOTS), device=device, dtype=torch.float32)
         self.grad = None
 
     def vptr(self, v, grad=False):
         t = (self.grad if grad else self.act)[v.buf.name]
         return ptr(t)
+
+    def absmax_ptr(self, i):
+        return self.absmax[i].data_ptr()
 
     def view_tensor(self, v, grad=False):
         t = (self.grad if grad else self.act)[v.buf.name]
@@ -294,7 +300,11 @@ class NetProgram:
             bf = torch.empty(op.K, dtype=torch.float32, device=w.device)
             _lib.check(lib.tde_bn_fold(kh * kw, cin, op.K, layout, ptr(w), ptr(mm), ptr(mv), ptr(beta), 1e-3,
                                        ptr(wf), ptr(bf), st), op.layer + " fold")
-            folded[op.layer] = (wf, bf)
+            # folded weights are w * rsqrt(moving_var + eps): their bound for the fp16x3 split (a layer with a
+            # small moving variance can exceed the fixed 2^8 weight scale's range)
+            wb = torch.zeros(_lib.BOUND_SLOTS, dtype=torch.float32, device=w.device)
+            wb[0] = wf.abs().amax()
+            folded[op.layer] = (wf, bf, wb)
         self._folded = folded
         return folded
 
@@ -352,8 +362,9 @@ class NetProgram:
                 sm = run.stats[i]
                 mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
                 if fold_bn:
-                    wf, bf = self._folded[op.layer]
+                    wf, bf, wb = self._folded[op.layer]
                     fd = op.folded_desc(N)
+                    fd.w_absmax = wb.data_ptr()
                     fn = lib.tde_deconv2d_fwd_bias_act if op.deconv else lib.tde_conv2d_fwd_bias_act
                     with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
                         _lib.check(fn(ctypes_ref(fd), run.vptr(op.src), ptr(wf), ptr(bf), 1, run.vptr(op.dst), ptr(ws),
@@ -452,6 +463,7 @@ class NetProgram:
         ws, dz = self._scratch(N)
         wsb = ws.numel() * 4
         iv = spec.input_view
+        _lib.check(lib.tde_zero_bytes(run.absmax.numel() * 4, ptr(run.absmax), st), "zero dz bounds")
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             if self.timer is not None:
@@ -459,6 +471,11 @@ class NetProgram:
             src_needs = need_input_grad or op.src.buf is not spec.input
             if isinstance(op, ConvBN):
                 d = op.desc(N)
+                # dz (the conv's output gradient) is the y view of a conv's descriptor, the x view of a deconv's
+                if op.deconv:
+                    d.x_absmax = run.absmax_ptr(i)
+                else:
+                    d.y_absmax = run.absmax_ptr(i)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
                 if self.bn_sync is not None:
@@ -474,15 +491,15 @@ class NetProgram:
                     _lib.check(lib.tde_bn_bwd_from_sums(M, op.K, M * self.bn_world, ptr(run.z[i]), ptr(sm[0]),
                                                         ptr(sm[1]), ptr(beta), run.vptr(op.dst, True), op.dst.buf.cs,
                                                         op.dst.coff, ptr(gs), ptr(ls), ptr(dz),
-                                                        ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws),
-                                                        wsb, st), op.layer + " syncbn bwd")
+                                                        ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,
+                                                        run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " syncbn bwd")
                 else:
                     with self._span("bn_bwd"):
                         _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
                                                   ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
                                                   op.dst.buf.cs, op.dst.coff, ptr(dz),
-                                                  ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1, ptr(ws), wsb,
-                                                  st), op.layer + " bn_bwd")
+                                                  ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,
+                                                  run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
                 if src_needs:
