@@ -1136,13 +1136,23 @@ static size_t halo_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   return b;
 }
 
+// halo-WGRAD partials: the larger of the fp32 and fp16x3 plans (0: neither applies)
+static size_t hwg_ws_bytes(const tde_conv_desc_t& d) {
+  size_t b = 0;
+  for (int math = 3; math <= 4; ++math) {
+    HwgPlan wp;
+    if (hwg_plan(d, wp, math) && wp.part_bytes > b) b = wp.part_bytes;
+  }
+  return b;
+}
+
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   const Plan pl = make_plan(d, mode);
   const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
   const size_t halo = halo_ws_bytes(d, mode, bn);
   size_t b = igemm > halo ? igemm : halo;
   HwgPlan wp;
-  if (mode == MODE_WGRAD && hwg_plan(d, wp) && wp.part_bytes > b) b = wp.part_bytes;
+  if (mode == MODE_WGRAD && hwg_ws_bytes(d) > b) b = hwg_ws_bytes(d);
   return b;
 }
 
@@ -1286,7 +1296,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   HwgPlan wp;
-  if (MODE == MODE_WGRAD && hwg_plan(*d, wp)) {
+  if (MODE == MODE_WGRAD && hwg_plan(*d, wp, g_conv_math)) {
     // stride-1, narrow, high-resolution layer: halo-tiled filter gradient (halo_wgrad.hip)
     if (wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
     if (!skip) hwg_launch(wp, *d, a.x, a.dy, a.dw, accumulate, tde_ws_body(ws), static_cast<hipStream_t>(stream));
@@ -1387,7 +1397,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   HaloPlan hp;
   HwgPlan wp;
-  if (MODE1 == MODE_DGRAD && hwg_plan(*d, wp)) {
+  if (MODE1 == MODE_DGRAD && hwg_plan(*d, wp, g_conv_math)) {
     // filter gradient on the halo-tiled WGRAD kernel; data gradient on the halo path or the implicit GEMM
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool hd = halo_plan(*d, 1, g_conv_math, hp);
@@ -1453,10 +1463,10 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   if (mode1 == MODE_DGRAD) {
     const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
     if (h && h + make_plan(d, MODE_WGRAD).slab_bytes > b) b = h + make_plan(d, MODE_WGRAD).slab_bytes;
-    HwgPlan wp;
-    if (hwg_plan(d, wp)) {
+    const size_t hw = hwg_ws_bytes(d);
+    if (hw) {
       const size_t b1 = h > p1.slab_bytes ? h : p1.slab_bytes;   // halo or igemm data gradient (math-dependent)
-      if (b1 + wp.part_bytes > b) b = b1 + wp.part_bytes;
+      if (b1 + hw > b) b = b1 + hw;
     }
   }
   return b + 64;

@@ -38,13 +38,14 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
 // resolution: partial dW per (pixel chunk, kernel row) in fp32 MFMA, then a fixed-order chunk reduce.
 struct HwgPlan {
   int ok;
+  int f16;                // fp16x3 kernel (math 4): CF / NF / nitems = (kw, cf) items / CPS, KPS in fp16 elements
   int CF, NF, nitems;     // 16-channel input / output fragments, (kw, cf, nf) items per block
   int CPS, KPS;           // LDS row strides (floats)
   int ntw, chunks;        // 64-pixel segments per output row, pixel chunks (grid x; grid y = KH)
   long ntiles;
   size_t lds_bytes, part_bytes;
 };
-bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp);
+bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp, int math);
 // dw (+)= dL/dW from x (view of d) and dy (y view of d); ws >= hp.part_bytes (16-byte aligned).
 void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, const float* dy, float* dw,
                 int accumulate, void* ws, hipStream_t st);

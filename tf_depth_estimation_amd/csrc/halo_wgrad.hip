@@ -20,6 +20,8 @@
 
 #include <cstdlib>
 
+#include "split_math.h"
+
 namespace {
 
 constexpr int TP = 128;       // output pixels per row segment
@@ -45,15 +47,18 @@ __device__ __forceinline__ void tile_coords(const HwgArgs& a, int t, int& n, int
 }
 
 // per-thread (pixel, channel) coordinates of its prefetch quads: constant over the tiles
-struct Quads {
-  int xhp[XQ], xc[XQ], dp[DQ], dc[DQ];
+template <int XQN, int DQN>
+struct QuadsT {
+  int xhp[XQN], xc[XQN], dp[DQN], dc[DQN];
 };
+using Quads = QuadsT<XQ, DQ>;
 
 // global -> registers: this thread's quads of the input row (kernel row kh) and the dy segment of tile t.
 // Branch-free raw buffer loads (out of the image / past the row -> offset OOB -> 0), all in flight at once;
 // the w_cin channel mask is applied when the registers are stored to LDS.
-__device__ __forceinline__ void prefetch(const HwgArgs& a, const Quads& q, __amdgpu_buffer_rsrc_t rx,
-                                         __amdgpu_buffer_rsrc_t rd, int kh, int t, f4 (&xr)[XQ], f4 (&dr)[DQ]) {
+template <int XQN, int DQN>
+__device__ __forceinline__ void prefetch(const HwgArgs& a, const QuadsT<XQN, DQN>& q, __amdgpu_buffer_rsrc_t rx,
+                                         __amdgpu_buffer_rsrc_t rd, int kh, int t, f4 (&xr)[XQN], f4 (&dr)[DQN]) {
   const bool tv = t < a.ntiles && !(a.diag & 2);
   int n = 0, oh = 0, ow0 = 0;
   if (tv) tile_coords(a, t, n, oh, ow0);
@@ -61,14 +66,14 @@ __device__ __forceinline__ void prefetch(const HwgArgs& a, const Quads& q, __amd
   const bool rowok = tv && (unsigned)ih < (unsigned)a.H;
   const int xrow = ((n * a.H + ih) * a.W) * a.xcs + a.xco;
 #pragma unroll
-  for (int i = 0; i < XQ; ++i) {
+  for (int i = 0; i < XQN; ++i) {
     const int iw = ow0 - a.PL + q.xhp[i];
     const bool ok = rowok && (unsigned)iw < (unsigned)a.W;      // xhp < 0: past this thread's quads
     xr[i] = bload(rx, ok ? 4 * (xrow + iw * a.xcs + q.xc[i]) : OOB);
   }
   const int drow = ((n * a.H + oh) * a.W) * a.ycs + a.yco;
 #pragma unroll
-  for (int i = 0; i < DQ; ++i) {
+  for (int i = 0; i < DQN; ++i) {
     const bool ok = tv && q.dp[i] >= 0 && ow0 + q.dp[i] < a.W;
     dr[i] = bload(rd, ok ? 4 * (drow + (ow0 + q.dp[i]) * a.ycs + q.dc[i]) : OOB);
   }
@@ -179,6 +184,176 @@ __global__ void __launch_bounds__(256) hwg_kernel(const HwgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ fp16x3 variant (conv math 4)
+// Same blocking (block = (kernel row, pixel chunk), 128-pixel output row segments, input row + dy segment
+// staged once per segment), but the operands are split into power-of-two-scaled fp16 hi / lo planes at
+// staging (split_math.h) and each 32-pixel k-step of an item is 3 v_mfma_f32_16x16x32_f16 instead of 8
+// v_mfma_f32_16x16x4_f32 (5.3x the product rate).  The contraction runs over pixels, but the LDS images
+// stay pixel-major ([pixel][channel], as loaded): fragments are read with ds_read_b64_tr_b16, which hands
+// lane i of a 16-lane group column i (= channel / output column i) of a 4-pixel x 16-column block, so the
+// tap shift kw is just a row offset.  k order inside a 32-pixel step (identical for A and B): element j of
+// lane group g is pixel 4g + j (j < 4) or 16 + 4g + j - 4; a 32-lane half then reads 8 consecutive rows,
+// conflict-free with a row stride of an odd multiple of 32 bytes (odd16 fp16 elements).
+// A wave owns NA (kw, channel fragment) items and computes each against all NF column fragments.
+struct HwhArgs {
+  int N, H, W, C, K, KH, KW, PT, PL, wcin;
+  int CF, NF, XS, DS, nA, ntw, chunks;
+  int ntiles;
+  const float* x; int xcs, xco;
+  const float* dy; int ycs, yco;
+  float* part;
+  const float* xmax; const float* dmax;   // operand bounds (tde_conv_desc_t x_absmax / y_absmax) or null
+};
+
+typedef unsigned short u16;
+typedef __fp16 hp4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+typedef __attribute__((address_space(3))) hp4* lds_hp4_t;
+
+// one 8-element fp16 fragment (k = 32-pixel step starting at pixel row `row0` of the plane, columns col0..+15)
+__device__ __forceinline__ h8 tr_frag(const u16* plane, int S, int row0, int col0, int g, int li) {
+  const int qq = li >> 2, p = li & 3;
+  const u16* a0 = plane + (row0 + 4 * g + qq) * S + col0 + 4 * p;
+  const hp4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hp4_t)(a0));
+  const hp4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hp4_t)(a0 + 16 * S));
+  const h4 l4 = __builtin_bit_cast(h4, lo), h4v = __builtin_bit_cast(h4, hi);
+  return h8{l4[0], l4[1], l4[2], l4[3], h4v[0], h4v[1], h4v[2], h4v[3]};
+}
+
+constexpr int XQ16 = 12, DQ16 = 4;   // most prefetch quads per thread (input row, dy segment)
+
+// XQN input-row quads per thread (4, 8 or 12: as few registers as the row needs), DQN = 2 NF dy quads
+template <int NA, int NF, int XQN>
+__global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
+  constexpr int DQN = 2 * NF;
+  extern __shared__ __attribute__((aligned(16))) u16 lds16[];
+  const int XP = (TP + a.KW - 1) * a.XS, DP = TP * a.DS;
+  u16* const xh = lds16;
+  u16* const xl = xh + XP;
+  u16* const dh = xl + XP;
+  u16* const dl = dh + DP;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int kh = blockIdx.y;
+  // only the real channel quads are staged: the pad channels / columns of the last fragment hold whatever the
+  // LDS holds, which reaches only dW rows c >= C and columns n >= K (dropped)
+  const int cq = a.C / 4, nq = a.K / 4;
+  const float sx = f16x3_scale(a.xmax, 1.f), sd = f16x3_scale(a.dmax, 1.f);
+  int akw[NA], acol[NA];
+#pragma unroll
+  for (int m = 0; m < NA; ++m) {
+    const int ia = wv + 4 * m;
+    const int ic = ia < a.nA ? ia : 0;   // dummy items read item 0 (every lane takes part: EXEC all ones)
+    akw[m] = ic / a.CF;
+    acol[m] = (ic - akw[m] * a.CF) * 16;
+  }
+  f4 acc[NA][NF];
+#pragma unroll
+  for (int m = 0; m < NA; ++m)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[m][f] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 xr[XQN], dr[DQN];
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (long)a.N * a.H * a.W * a.xcs);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (long)a.N * a.H * a.W * a.ycs);
+  // the fp32 kernel's prefetch (same quads; HwgArgs view of the geometry)
+  HwgArgs ga{};
+  ga.N = a.N; ga.H = a.H; ga.W = a.W; ga.C = a.C; ga.K = a.K; ga.KW = a.KW; ga.PT = a.PT; ga.PL = a.PL;
+  ga.ntw = a.ntw; ga.ntiles = a.ntiles; ga.xcs = a.xcs; ga.xco = a.xco; ga.ycs = a.ycs; ga.yco = a.yco;
+  QuadsT<XQN, DQN> q;
+  {
+    const int nx = (TP + a.KW - 1) * cq;
+#pragma unroll
+    for (int i = 0; i < XQN; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int hp = e / cq, c = 4 * (e - hp * cq);
+      const bool ok = e < nx;
+      q.xhp[i] = ok ? hp : -(1 << 20);
+      q.xc[i] = c;
+    }
+#pragma unroll
+    for (int i = 0; i < DQN; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int p = e / nq, c = 4 * (e - p * nq);
+      const bool ok = e < TP * nq;
+      q.dp[i] = ok ? p : -1;
+      q.dc[i] = c;
+    }
+  }
+  int t = blockIdx.x;
+  prefetch(ga, q, rx, rd, kh, t, xr, dr);
+  for (; t < a.ntiles; t += a.chunks) {
+    int n, oh, ow0;
+    tile_coords(ga, t, n, oh, ow0);
+    const bool live = (unsigned)(oh + kh - a.PT) < (unsigned)a.H;   // uniform over the block
+    __syncthreads();                                   // the previous segment's reads are done
+#pragma unroll
+    for (int i = 0; i < XQN; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < (TP + a.KW - 1) * cq) {
+        const int hp = e / cq, c = 4 * (e - hp * cq);
+        f4 v = xr[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j >= a.wcin) v[j] = 0.f;
+        h4 hi, lo;
+        split4x2h(v, sx, hi, lo);
+        *reinterpret_cast<h4*>(xh + hp * a.XS + c) = hi;
+        *reinterpret_cast<h4*>(xl + hp * a.XS + c) = lo;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DQN; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (e < TP * nq) {
+        const int p = e / nq, c = 4 * (e - p * nq);
+        h4 hi, lo;
+        split4x2h(dr[i], sd, hi, lo);
+        *reinterpret_cast<h4*>(dh + p * a.DS + c) = hi;
+        *reinterpret_cast<h4*>(dl + p * a.DS + c) = lo;
+      }
+    }
+    __syncthreads();
+    prefetch(ga, q, rx, rd, kh, t + a.chunks, xr, dr);   // next segment's loads in flight under the MFMAs
+    if (!live) continue;
+#pragma unroll 1
+    for (int s0 = 0; s0 < TP; s0 += 32) {
+      h8 bh[NF], bl[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        bh[f] = tr_frag(dh, a.DS, s0, 16 * f, g, li);
+        bl[f] = tr_frag(dl, a.DS, s0, 16 * f, g, li);
+      }
+#pragma unroll
+      for (int m = 0; m < NA; ++m) {
+        const h8 ah = tr_frag(xh, a.XS, s0 + akw[m], acol[m], g, li);
+        const h8 al = tr_frag(xl, a.XS, s0 + akw[m], acol[m], g, li);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[f], acc[m][f], 0, 0, 0);
+          acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[f], acc[m][f], 0, 0, 0);
+          acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[f], acc[m][f], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // lane (li, g) holds dW[kw][c = cf*16 + 4g + r][n = nf*16 + li] (scaled); partial [chunk][kh][kw][wcin][K]
+  const float inv = 1.f / (sx * sd);   // power of two: exact
+  float* out = a.part + ((long)blockIdx.x * a.KH + kh) * a.KW * a.wcin * a.K;
+#pragma unroll
+  for (int m = 0; m < NA; ++m) {
+    const int ia = wv + 4 * m;
+    if (ia >= a.nA) continue;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int nn = f * 16 + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = acol[m] + 4 * g + j;
+        if (c < a.wcin && nn < a.K) out[((long)akw[m] * a.wcin + c) * a.K + nn] = acc[m][f][j] * inv;
+      }
+    }
+  }
+}
+
 // dw[e] (+)= sum over chunks of part[chunk][e] (e = ((kh*KW + kw)*wcin + c)*K + n): a block is 16 output
 // quads x 16 z-lanes; lane z sums chunks z, z+16, ... and the 16 lanes of a quad are combined through LDS
 // in lane order (fixed order: deterministic).
@@ -215,6 +390,8 @@ const long g_hwg_blocks = tde_env_pos("TDE_HWG_BLOCKS", 768);  // grid size to a
 const long g_hwg_min_m = tde_env_pos("TDE_HWG_MIN_M", 16384);
 const long g_hwg_diag = env_hwg("TDE_HWG_DIAG", 0);
 const long g_hwg_min_items = env_hwg("TDE_HWG_MIN_ITEMS", 25);
+const long g_hwh = env_hwg("TDE_HWH", 1);                 // 0: fp32 halo WGRAD also in math 4 (A/B)
+const long g_hwh_min_items = env_hwg("TDE_HWH_MIN_ITEMS", 1);
 
 int odd16(int c) {   // smallest odd multiple of 16 >= c
   int f = (c + 15) / 16;
@@ -224,9 +401,34 @@ int odd16(int c) {   // smallest odd multiple of 16 >= c
 
 }  // namespace
 
-bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp) {
+bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp, int math) {
   hp = HwgPlan{};
   if (!g_hwg || d.stride != 1 || d.OH != d.H || d.OW != d.W) return false;
+  if (math == 4 && g_hwh) {
+    // fp16x3 kernel: (kw, channel fragment) items per wave x all column fragments
+    if ((long)d.N * d.H * d.W < g_hwg_min_m) return false;
+    if (d.K > 32 || d.K % 4 || d.C % 4 || d.C > 128 || d.KW > 7 || d.KH > 7) return false;
+    if (d.x_cstride % 4 || d.x_coff % 4 || d.y_cstride % 4 || d.y_coff % 4) return false;
+    const int CF = (d.C + 15) / 16, NF = (d.K + 15) / 16;
+    const int nA = d.KW * CF;
+    if (nA > 4 * 8 || nA * NF < g_hwh_min_items) return false;
+    if ((TP + d.KW - 1) * (d.C / 4) > 256 * XQ16 || TP * (d.K / 4) > 256 * 2 * NF) return false;
+    hp.ok = 1; hp.f16 = 1;
+    hp.CF = CF; hp.NF = NF; hp.nitems = nA;
+    hp.CPS = odd16(CF * 16);   // fp16 elements per LDS row
+    hp.KPS = odd16(NF * 16);
+    hp.ntw = (d.W + TP - 1) / TP;
+    hp.ntiles = (long)d.N * d.H * hp.ntw;
+    long chunks = (g_hwg_blocks + d.KH - 1) / d.KH;
+    const long maxc = (hp.ntiles + 3) / 4;
+    if (chunks > maxc) chunks = maxc;
+    if (chunks < 1) chunks = 1;
+    hp.chunks = (int)chunks;
+    // two fp16 planes each of the input row and the dy segment
+    hp.lds_bytes = (size_t)(2 * (TP + d.KW - 1) * hp.CPS + 2 * TP * hp.KPS) * sizeof(u16);
+    hp.part_bytes = ((size_t)chunks * d.KH * d.KW * d.w_cin * d.K * sizeof(float) + 255) / 256 * 256;
+    return true;
+  }
   if ((long)d.N * d.H * d.W < g_hwg_min_m) return false;
   if (d.K > 32 || d.K % 4 || d.C % 4 || d.C > 128 || d.KW > 7 || d.KH > 7) return false;
   if (d.x_cstride % 4 || d.x_coff % 4 || d.y_cstride % 4 || d.y_coff % 4) return false;
@@ -254,8 +456,47 @@ bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp) {
   return true;
 }
 
+template <int NA, int XQN>
+void launch_hwh_x(const HwgPlan& hp, const HwhArgs& a, dim3 grid, hipStream_t st) {
+  if (hp.NF == 1) hipLaunchKernelGGL((hwh_kernel<NA, 1, XQN>), grid, dim3(256), hp.lds_bytes, st, a);
+  else hipLaunchKernelGGL((hwh_kernel<NA, 2, XQN>), grid, dim3(256), hp.lds_bytes, st, a);
+}
+template <int NA>
+void launch_hwh(const HwgPlan& hp, const HwhArgs& a, dim3 grid, hipStream_t st) {
+  const int need = ((TP + a.KW - 1) * (a.C / 4) + 255) / 256;
+  if (need <= 4) launch_hwh_x<NA, 4>(hp, a, grid, st);
+  else if (need <= 8) launch_hwh_x<NA, 8>(hp, a, grid, st);
+  else launch_hwh_x<NA, 12>(hp, a, grid, st);
+}
+
 void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, const float* dy, float* dw,
                 int accumulate, void* ws, hipStream_t st) {
+  if (hp.f16) {
+    HwhArgs a{};
+    a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.K = d.K; a.KH = d.KH; a.KW = d.KW;
+    a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
+    a.CF = hp.CF; a.NF = hp.NF; a.XS = hp.CPS; a.DS = hp.KPS; a.nA = hp.nitems; a.ntw = hp.ntw;
+    a.chunks = hp.chunks; a.ntiles = (int)hp.ntiles;
+    a.x = x; a.xcs = d.x_cstride; a.xco = d.x_coff;
+    a.dy = dy; a.ycs = d.y_cstride; a.yco = d.y_coff;
+    a.part = static_cast<float*>(ws);
+    a.xmax = d.x_absmax; a.dmax = d.y_absmax;
+    const dim3 grid(hp.chunks, d.KH);
+    switch ((hp.nitems + 3) / 4) {
+      case 1: launch_hwh<1>(hp, a, grid, st); break;
+      case 2: launch_hwh<2>(hp, a, grid, st); break;
+      case 3: launch_hwh<3>(hp, a, grid, st); break;
+      case 4: launch_hwh<4>(hp, a, grid, st); break;
+      case 5: launch_hwh<5>(hp, a, grid, st); break;
+      case 6: launch_hwh<6>(hp, a, grid, st); break;
+      case 7: launch_hwh<7>(hp, a, grid, st); break;
+      default: launch_hwh<8>(hp, a, grid, st); break;
+    }
+    const long E4 = (long)d.KH * d.KW * d.w_cin * d.K / 4;
+    hipLaunchKernelGGL(hwg_reduce_kernel, dim3((int)((E4 + 15) / 16)), dim3(256), 0, st, a.part, hp.chunks, E4, dw,
+                       accumulate);
+    return;
+  }
   HwgArgs a{};
   a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.K = d.K; a.KH = d.KH; a.KW = d.KW;
   a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
