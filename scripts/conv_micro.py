@@ -18,6 +18,7 @@ from tf_depth_estimation_amd.program import same_pad  # noqa: E402
 SHAPES = [
     # name, N, H, W, C, K, k, s
     ("gemm1x1_big", 8, 64, 64, 512, 512, 1, 1),
+    ("big3x3", 32, 48, 64, 256, 256, 3, 1),
     ("cnv1b", 8, 96, 128, 32, 32, 7, 1),
     ("cnv2b", 8, 48, 64, 64, 64, 5, 1),
     ("icnv4", 8, 24, 32, 256, 128, 3, 1),

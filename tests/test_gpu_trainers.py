@@ -265,7 +265,7 @@ def test_adam_overlap_matches_plain(cfg, graph):
     final only at its net's second backward call) scatters the consistency-loss gradient with float
     atomics, so two runs differ in rounding (BN backward amplifies it to ~1e-3 relative on the gradient): one step,
     the overlapped run's first moments and parameter updates must be as close to a plain run as two plain
-    runs are to each other (4x their measured run-to-run difference)."""
+    runs are to each other (4x their measured run-to-run difference, at least 5e-3)."""
     from tf_depth_estimation_amd import _api, train, variables
     steps = 3 if cfg == "config2" else 1
 
@@ -306,5 +306,7 @@ def test_adam_overlap_matches_plain(cfg, graph):
     for (_, ma, _, da), (_, m2, _, d2), (_, mb, _, db) in zip(plain, plain2, ov):
         noise_m = ((ma - m2).norm() / ma.norm()).item()          # run-to-run (atomics) noise of the step
         noise_d = ((da - d2).norm() / da.norm()).item()
-        assert ((ma - mb).norm() / ma.norm()).item() <= max(1e-6, 4 * noise_m)
-        assert ((da - db).norm() / da.norm()).item() <= max(1e-4, 4 * noise_d)
+        # one pair of plain runs samples that noise once; it ranged 1e-4 .. 1.5e-3 relative over runs, so the
+        # floor is 5e-3 (a missed or doubled bucket differs by O(1))
+        assert ((ma - mb).norm() / ma.norm()).item() <= max(5e-3, 4 * noise_m)
+        assert ((da - db).norm() / da.norm()).item() <= max(5e-3, 4 * noise_d)
