@@ -186,6 +186,35 @@ struct Img6 {
   }
 };
 
+// fp16x3 staged image (MATH 4): each scaled fp32 operand element is split ONCE, at LDS staging, into fp16
+// hi / lo planes [row][32 k] (64-byte rows) -- not once per reading wave per k-tile, which made the split's
+// VALU work (~3 instructions per element, 2 waves reading every element) the limiter of the whole k-loop
+// (313 VALU vs 48 MFMAs per wave per 128x128 k-tile).  The four 16-byte k-chunks of a row are XOR-swizzled
+// by (row >> 2) & 3, so the 16 lanes of a ds_read_b128 lane group (16 rows, one chunk) cover all 64 banks.
+// TDE_F16_STAGE=0 builds the previous register-split variant (fp32 image) for A/B runs.
+#ifndef TDE_F16_STAGE
+#define TDE_F16_STAGE 1
+#endif
+template <int ROWS>
+struct Img2h {
+  static constexpr int PLANE = ROWS * 32;   // u16 elements per plane
+  static constexpr int SIZE = 2 * PLANE;    // hi + lo
+  __device__ static __forceinline__ int off(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 2) & 3)) << 3); }
+  __device__ static __forceinline__ void put(u16* s, int row, int k, f4 v, float sc) {
+    h4 hi, lo;
+    split4x2h(v, sc, hi, lo);
+    const int o = off(row, k >> 3) + (k & 7);
+    *reinterpret_cast<h4*>(s + o) = hi;
+    *reinterpret_cast<h4*>(s + PLANE + o) = lo;
+  }
+  __device__ static __forceinline__ h8 hi(const u16* s, int row, int q) {
+    return *reinterpret_cast<const h8*>(s + off(row, q));
+  }
+  __device__ static __forceinline__ h8 lo(const u16* s, int row, int q) {
+    return *reinterpret_cast<const h8*>(s + PLANE + off(row, q));
+  }
+};
+
 template <int MATH, int ROWS>
 struct ImgSel;
 template <int ROWS>
@@ -196,8 +225,13 @@ template <int ROWS>
 struct ImgSel<2, ROWS> { using type = Img6<ROWS>; using T = u16; };
 template <int ROWS>
 struct ImgSel<3, ROWS> { using type = Img1<ROWS>; using T = float; };
+#if TDE_F16_STAGE
+template <int ROWS>
+struct ImgSel<4, ROWS> { using type = Img2h<ROWS>; using T = u16; };
+#else
 template <int ROWS>
 struct ImgSel<4, ROWS> { using type = Img1<ROWS>; using T = float; };
+#endif
 
 // MATH 0: exact fp32 (2 x 4 v_mfma_f32_16x16x4_f32 per 32-deep k-tile); MATH 1: bf16x3.
 template <int MATH, int BM, int BN>
@@ -308,7 +342,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     const int kbase = kt * BK3;
     // k decode shared by every A slot (and the DGRAD B slots): s & 7 == tid & 7 for all slots
     const int kq = kbase + 4 * (tid & 7);
-    int t_h = 0, t_w = 0, koff = 0, kx = 0;
+    int t_h = 0, t_w = 0, koff = 0, kx = 0, dg_wtap = 0;
     if constexpr (MODE == MODE_FWD) {
       const int tap = fdiv(kq, p.fC), c = kq - tap * p.C;
       t_h = fdiv(tap, p.fKW); t_w = tap - t_h * p.KW;
@@ -318,6 +352,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       kx = kq - tap * p.K;                       // output channel co
       t_h = fdiv(tap, fntw); t_w = tap - t_h * g.ntw;
       koff = -(t_h * p.OW + t_w) * p.ycs + kx;
+      // weight offset of this thread's (tap, co) shared by all its B slots (which differ in ci only)
+      dg_wtap = ((g.khs + p.S * t_h) * p.KW + g.kws + p.S * t_w) * p.wcin * p.K + kx;
     }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -353,14 +389,14 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const int n = n0 + 4 * (s % (BN / 4)), k0 = kbase + 4 * (s / (BN / 4));
         const int tap = fdiv(k0, p.fC), c0 = k0 - tap * p.C;   // k0..k0+3 share the tap (C % 4 == 0)
         const bool ok = slot && n < Nn && k0 < Kd;
+        const int wo = (tap * p.wcin + c0) * p.K + n;            // weight row k0, column n (one multiply)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          rb[i][j] = bload(rw, ok && c0 + j < p.wcin ? 4 * ((tap * p.wcin + c0 + j) * p.K + n) : OOB);
+          rb[i][j] = bload(rw, ok && c0 + j < p.wcin ? 4 * (wo + j * p.K) : OOB);
       } else if constexpr (MODE == MODE_DGRAD) {
         const int ci = n0 + (s >> 3);
-        const int kh = g.khs + p.S * t_h, kw = g.kws + p.S * t_w;
         const bool ok = slot && kq < Kd && ci < p.wcin;
-        rb[i][0] = bload(rw, ok ? 4 * (((kh * p.KW + kw) * p.wcin + ci) * p.K + kx) : OOB);
+        rb[i][0] = bload(rw, ok ? 4 * (dg_wtap + ci * p.K) : OOB);
       } else {
         const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
         const bool ok = slot && n < Nn;
@@ -371,6 +407,15 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     }
   };
 
+  // staging store of one 4-k row segment (the staged fp16x3 image splits here, with the operand's scale)
+  auto putA = [&](ET* A, int row, int k, f4 v) {
+    if constexpr (MATH == 4 && TDE_F16_STAGE) IA::put(A, row, k, v, sA);
+    else IA::put(A, row, k, v);
+  };
+  auto putB = [&](ET* Bm, int row, int k, f4 v) {
+    if constexpr (MATH == 4 && TDE_F16_STAGE) IB::put(Bm, row, k, v, sB);
+    else IB::put(Bm, row, k, v);
+  };
   auto store_tiles = [&](int buf, auto& ra, auto& rb) {
     ET* A = As0 + buf * IA::SIZE;
     ET* Bm = Bs0 + buf * IB::SIZE;
@@ -382,9 +427,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const int r0 = 4 * (s % (BM / 4)), k0 = 4 * (s / (BM / 4));
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          IA::put(A, r0 + rr, k0, f4{ra[i][0][rr], ra[i][1][rr], ra[i][2][rr], ra[i][3][rr]});
+          putA(A, r0 + rr, k0, f4{ra[i][0][rr], ra[i][1][rr], ra[i][2][rr], ra[i][3][rr]});
       } else {
-        IA::put(A, s >> 3, 4 * (s & 7), ra[i][0]);
+        putA(A, s >> 3, 4 * (s & 7), ra[i][0]);
       }
     }
 #pragma unroll
@@ -395,9 +440,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const int r0 = 4 * (s % (BN / 4)), k0 = 4 * (s / (BN / 4));
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          IB::put(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
+          putB(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
       } else {
-        IB::put(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
+        putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
       }
     }
   };
@@ -437,8 +482,30 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
+    } else if constexpr (MATH == 4 && TDE_F16_STAGE) {
+      // fp16x3, staged image: hi / lo fragments straight from the planes (k-chunk q = k 8q..8q+7 for A and B)
+      h8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+        al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+        bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
+      }
+      issue();
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
     } else if constexpr (MATH == 4) {
-      // fp16x3: fp32 LDS image as MATH 3, each fragment scaled and split into fp16 hi / lo in registers
+      // fp16x3 (TDE_F16_STAGE=0): fp32 LDS image as MATH 3, each fragment scaled and split in registers
       f4 fa[TM][2], fb[TN][2];
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
@@ -1385,6 +1452,9 @@ static void launch_bwd2(const Plan& p1, const ConvArgs& a1, const Plan& p2, cons
 }
 
 static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches (A/B experiments)
+// Timing experiment only (filter gradients are NOT computed): what the backward chain costs without the
+// filter-gradient work, i.e. the bound on taking it off the critical path
+static const long g_skip_wgrad = env_long("TDE_SKIP_WGRAD", 0);
 
 
 // Data + filter gradient of one layer.  MODE1 = the data-gradient GEMM of the virtual conv (DGRAD for a
@@ -1413,7 +1483,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
       if (!skip) launch_mode<MODE1>(p1, a1, st);
       if (!skipr) launch_reduce<MODE1>(p1, a1, st);
     }
-    if (!skip) hwg_launch(wp, *d, a2.x, a2.dy, a2.dw, acc2, body + b1, st);
+    if (!skip && !g_skip_wgrad) hwg_launch(wp, *d, a2.x, a2.dy, a2.dw, acc2, body + b1, st);
     return tde_launch_status();
   }
   if (MODE1 == MODE_DGRAD && halo_plan(*d, 1, g_conv_math, hp)) {
@@ -1426,13 +1496,13 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (!skip) {
       halo_launch(hp, *d, a1.dy, a1.w, a1.dx, acc1, body, nullptr, st);
-      launch_mode<MODE_WGRAD>(p2, a2, st);
+      if (!g_skip_wgrad) launch_mode<MODE_WGRAD>(p2, a2, st);
     }
-    if (!skipr) launch_reduce<MODE_WGRAD>(p2, a2, st);
+    if (!skipr && !g_skip_wgrad) launch_reduce<MODE_WGRAD>(p2, a2, st);
     return tde_launch_status();
   }
   const Plan p1 = make_plan(*d, MODE1);
-  const bool fuse = g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0;
+  const bool fuse = g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
   const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : make_plan(*d, MODE_WGRAD);
   if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
@@ -1446,11 +1516,11 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     launch_bwd2<MODE1>(p1, a1, p2, a2, st);
   } else {
     launch_mode<MODE1>(p1, a1, st);
-    launch_mode<MODE_WGRAD>(p2, a2, st);
+    if (!g_skip_wgrad) launch_mode<MODE_WGRAD>(p2, a2, st);
   }
   if (!skipr) {
     launch_reduce<MODE1>(p1, a1, st);
-    launch_reduce<MODE_WGRAD>(p2, a2, st);
+    if (!g_skip_wgrad) launch_reduce<MODE_WGRAD>(p2, a2, st);
   }
   return tde_launch_status();
 }

@@ -68,14 +68,28 @@ __device__ __forceinline__ float f16x3_scale(const float* bound, float dflt) {
   return ldexpf(1.f, 14 - e);
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+// hi = fp16_rne(x*s) by pairs (v_pk_mul_f32 + v_cvt_pk_f16_f32), lo = fp16_rne(fma(x, s, -hi)) read from the
+// packed hi register by v_fma_mix (op_sel picks the f16 half): 2 VALU instructions per element.  hipcc's own
+// lowering of the same arithmetic unpacked hi back to fp32 first (3.25 per element).  Bit-identical: x*s is
+// exact (power-of-two s), x*s - hi is exact in fp32, and both forms round that value once to fp16.
+__device__ __forceinline__ unsigned f16_lo_pair(float x0, float x1, float s, unsigned hi_pair) {
+  unsigned lo;
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %4, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo) : "v"(x0), "v"(s), "v"(hi_pair), "v"(x1));
+  return lo;
+}
+
 __device__ __forceinline__ void split4x2h(f4 v, float s, h4& hi, h4& lo) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float x = v[j] * s;
-    const _Float16 h = (_Float16)x;
-    hi[j] = h;
-    lo[j] = (_Float16)(x - (float)h);
-  }
+  const h2v a = __builtin_convertvector(f2v{v[0], v[1]} * s, h2v);
+  const h2v b = __builtin_convertvector(f2v{v[2], v[3]} * s, h2v);
+  const h2v c = __builtin_bit_cast(h2v, f16_lo_pair(v[0], v[1], s, __builtin_bit_cast(unsigned, a)));
+  const h2v d = __builtin_bit_cast(h2v, f16_lo_pair(v[2], v[3], s, __builtin_bit_cast(unsigned, b)));
+  hi = h4{a[0], a[1], b[0], b[1]};
+  lo = h4{c[0], c[1], d[0], d[1]};
 }
 
 // 8 consecutive-k fp32 values (two f4) -> hi / lo fp16x8 fragments
