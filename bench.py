@@ -249,6 +249,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
     ap.add_argument("--adam-overlap", action="store_true",
                     help="N = 1: run each gradient bucket's Adam on a side stream as soon as backward finalises it")
+    ap.add_argument("--wgrad-overlap", default="on", choices=["on", "off"],
+                    help="filter gradients on a side stream, off backward's data-gradient chain (a parallel graph "
+                         "branch; bit-identical results)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
                          "runs eagerly, RCCL is not captured)")
@@ -281,6 +284,8 @@ def main():
         tr.enable_sync_bn(world)
     if args.adam_overlap and world == 1:
         tr.enable_adam_overlap()
+    if args.wgrad_overlap == "on":
+        tr.enable_wgrad_overlap()
     progs = tr.programs()
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
@@ -355,6 +360,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
+                       "wgrad_overlap": args.wgrad_overlap == "on",
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",

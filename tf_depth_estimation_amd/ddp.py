@@ -71,8 +71,11 @@ class GradSync:
 
     chunks: ParamChunks updated by the step; uses: {id(chunk): backward calls per step} (default 1)."""
 
-    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None):
+    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None):
         self.world, self.group = world, group
+        # called before a bucket launch point: orders the compute stream after side streams that write
+        # gradients (NetProgram.join_wgrad), so the launch event covers them
+        self.pre_launch = pre_launch
         self.chunks = list(chunks)
         self.buckets = []
         self.by_param = {}
@@ -119,6 +122,8 @@ class GradSync:
         return on_grads
 
     def _ready(self, buckets):
+        if self.pre_launch is not None:
+            self.pre_launch()
         for b in buckets:
             b.launched = True
         if self.capturing is not None:
@@ -153,6 +158,8 @@ class GradSync:
     def finish(self):
         """Launch what was never reported, then order the compute stream after the comm stream."""
         rest = self.leftovers()
+        if self.pre_launch is not None:
+            self.pre_launch()
         if rest:
             for b in rest:
                 b.launched = True

@@ -198,6 +198,9 @@ class NetSpec:
         return specs, bn
 
 
+SERIAL = "serial"   # enable_wgrad_overlap(serial=True): the split backward calls on the compute stream
+
+
 class Workspace:
     """Per-(program, batch) scratch shared by all calls on one stream: the split-K / reduction workspace
     and the dense dz buffer of the BN backward."""
@@ -263,6 +266,10 @@ class NetProgram:
         self.bn_sync, self.bn_world = None, 1
         self._bn_sums = {}
         self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
+        # filter-gradient overlap (enable_wgrad_overlap): side stream, its workspace per batch, dz ring
+        self.wgrad_stream = None
+        self._ws2 = {}
+        self._dz2 = {}
 
     def _sums(self, i, K, which):
         key = (i, which)
@@ -307,6 +314,34 @@ class NetProgram:
             folded[op.layer] = (wf, bf, wb)
         self._folded = folded
         return folded
+
+    def enable_wgrad_overlap(self, on=True, serial=False):
+        """Take the filter gradients off backward's critical path: each conv/deconv's data gradient runs on
+        the current stream and its filter gradient (tde_conv2d_bwd_filter / tde_deconv2d_bwd_filter) on a side
+        stream that waits for the layer's dz, with its own workspace; the BN backward alternates between two
+        dz buffers and waits for the filter gradient that last read the one it overwrites.  Nothing on the
+        data-gradient chain waits for a filter gradient (TF's Conv2DBackpropFilter has no consumer but the
+        optimizer), so under capture the side stream is a parallel graph branch joined at the end of
+        backward (and before any gradient-exchange launch point: join_wgrad()).  The two GEMMs are the
+        separate data- and filter-gradient calls (their own tile plans, not the fused launch's shared tile),
+        so results equal serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
+        self.wgrad_stream = (SERIAL if serial else torch.cuda.Stream()) if on else None
+        return self
+
+    def join_wgrad(self):
+        """Order the current stream after every filter gradient launched so far (the dz ring is then free:
+        its events are dropped, so none is waited on across a graph-segment boundary)."""
+        if self.wgrad_stream is not None:
+            if self.wgrad_stream is not SERIAL:
+                torch.cuda.current_stream().wait_stream(self.wgrad_stream)
+            ring = getattr(self, "_ev_ring", None)
+            if ring is not None:
+                ring[0] = ring[1] = None
+
+    def _scratch_side(self, N):
+        ws, dz = self._scratch(N)
+        w = self._ws2.setdefault(N, Workspace())
+        return w.get(ws.numel() * 4, dz.numel(), "cuda")
 
     def _scratch(self, N):
         if N not in self._sizes:
@@ -464,6 +499,15 @@ class NetProgram:
         wsb = ws.numel() * 4
         iv = spec.input_view
         _lib.check(lib.tde_zero_bytes(run.absmax.numel() * 4, ptr(run.absmax), st), "zero dz bounds")
+        side = self.wgrad_stream if (self.timer is None and self.bn_sync is None) else None
+        if side is SERIAL:
+            side = torch.cuda.current_stream()
+        if side is not None:
+            ws2, dz_b = self._scratch_side(N)
+            wsb2 = ws2.numel() * 4
+            dz_ring, nconv = (dz, dz_b), 0
+            ev_ring = self._ev_ring = [None, None]
+            side.wait_stream(torch.cuda.current_stream())   # the side stream's first use of this step's state
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             if self.timer is not None:
@@ -478,6 +522,13 @@ class NetProgram:
                     d.y_absmax = run.absmax_ptr(i)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
+                if side is not None:
+                    # dz ring: wait for the filter gradient that read this buffer two conv layers ago
+                    slot = nconv & 1
+                    nconv += 1
+                    dz = dz_ring[slot]
+                    if ev_ring[slot] is not None:
+                        torch.cuda.current_stream().wait_event(ev_ring[slot])
                 if self.bn_sync is not None:
                     # SyncBN backward: local (sum g, sum g*xhat) -> all-reduced copy -> dz from the global means,
                     # dbeta from the local sum (the gradient all-reduce averages it like every parameter)
@@ -502,7 +553,26 @@ class NetProgram:
                                                   run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
-                if src_needs:
+                if side is not None:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    if src_needs:
+                        acc = mark(op.src)
+                        if op.deconv:
+                            _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
+                                                                 acc, ptr(ws), wsb, st), op.layer + " bwd data")
+                        else:
+                            _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
+                                                               acc, ptr(ws), wsb, st), op.layer + " bwd data")
+                    side.wait_event(ev)
+                    with torch.cuda.stream(side):
+                        wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
+                        a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
+                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws2), wsb2, _lib.stream_ptr()),
+                                   op.layer + " wgrad")
+                        ev_ring[slot] = torch.cuda.Event()
+                        ev_ring[slot].record()
+                elif src_needs:
                     # data + filter gradient: one fused launch (tde_conv2d_bwd / tde_deconv2d_bwd)
                     acc = mark(op.src)
                     with self._span("conv_bwd", 2 * fl, 2 * conv_bytes(op, N)):
@@ -545,6 +615,8 @@ class NetProgram:
                 acc = mark(s)
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
+        if side is not None:
+            self.join_wgrad()
         if need_input_grad:
             return run.view_tensor(iv, grad=True)[..., :spec.cin]
         return None

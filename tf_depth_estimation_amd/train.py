@@ -56,9 +56,10 @@ class AdamOverlap:
     kernel work: under capture the side stream becomes a graph branch (fork at each bucket's event,
     one join before the step ends)."""
 
-    def __init__(self, opts, bucket_mb=16.0, uses=None):
+    def __init__(self, opts, bucket_mb=16.0, uses=None, pre_launch=None):
         from .ddp import make_buckets
         self.opts = list(opts)
+        self.pre_launch = pre_launch
         self.buckets = []
         self.by_param = {}
         for o in self.opts:
@@ -97,6 +98,8 @@ class AdamOverlap:
         return on_grads
 
     def launch(self, buckets):
+        if self.pre_launch is not None:
+            self.pre_launch()
         ev = torch.cuda.Event()
         ev.record()
         self.side.wait_event(ev)
@@ -149,8 +152,20 @@ class Trainer:
         if self.grad_sync is not None:
             raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
-        self.adam_ov = AdamOverlap(opts, bucket_mb, {id(c): self.BACKWARD_USES for c in self.chunks})
+        self.adam_ov = AdamOverlap(opts, bucket_mb, {id(c): self.BACKWARD_USES for c in self.chunks},
+                                   pre_launch=self.join_wgrad)
         return self.adam_ov
+
+    def enable_wgrad_overlap(self, on=True, serial=False):
+        """Filter gradients on a side stream, off the backward chain (NetProgram.enable_wgrad_overlap;
+        serial=True: the same split calls on the compute stream, the bit-exact reference of the overlap)."""
+        for p in self.programs():
+            p.enable_wgrad_overlap(on, serial)
+        return self
+
+    def join_wgrad(self):
+        for p in self.programs():
+            p.join_wgrad()
 
     def _begin(self):
         if self.adam_ov is not None:
@@ -167,7 +182,8 @@ class Trainer:
         if self.adam_ov is not None:
             raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
-        self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group)
+        self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
+                                  pre_launch=self.join_wgrad)
         return self.grad_sync
 
     def enable_sync_bn(self, world, group=None):
