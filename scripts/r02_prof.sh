@@ -10,5 +10,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof_${TA
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 scripts/kstats.py "$(find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' | head -1)" 124 60 > gpurun_out/kstats_${TAG}.txt
 cat gpurun_out/kstats_${TAG}.txt
-timeout -k 10 200 python3 scripts/layer_profile.py --math fp16x3 --top 70 > gpurun_out/layers_${TAG}.txt 2>&1
+timeout -k 10 200 python3 scripts/layer_profile.py --math fp16x3 --top 90 > gpurun_out/layers_${TAG}.txt 2>&1
 rc=$?; echo "layers rc=$rc"; cat gpurun_out/layers_${TAG}.txt
