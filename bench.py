@@ -247,8 +247,10 @@ def main():
                          "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
-    ap.add_argument("--adam-overlap", action="store_true",
-                    help="N = 1: run each gradient bucket's Adam on a side stream as soon as backward finalises it")
+    ap.add_argument("--adam-overlap", default="off", choices=["off", "side", "wgrad"],
+                    help="N = 1: run each gradient bucket's Adam as soon as backward finalises it, on its own side "
+                         "stream or on the filter-gradient stream")
+    ap.add_argument("--adam-bucket-mb", type=float, default=16.0)
     ap.add_argument("--wgrad-overlap", default="on", choices=["on", "off"],
                     help="filter gradients on a side stream, off backward's data-gradient chain (a parallel graph "
                          "branch; bit-identical results)")
@@ -282,10 +284,10 @@ def main():
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     if args.sync_bn:
         tr.enable_sync_bn(world)
-    if args.adam_overlap and world == 1:
-        tr.enable_adam_overlap()
     if args.wgrad_overlap == "on":
         tr.enable_wgrad_overlap()
+    if args.adam_overlap != "off" and world == 1:
+        tr.enable_adam_overlap(args.adam_bucket_mb, on_wgrad_stream=args.adam_overlap == "wgrad")
     progs = tr.programs()
 
     # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
@@ -361,6 +363,7 @@ def main():
                        "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
                        "wgrad_overlap": args.wgrad_overlap == "on",
+                       "adam_overlap": args.adam_overlap if world == 1 else "off",
                        "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",

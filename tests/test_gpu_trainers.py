@@ -256,16 +256,19 @@ def test_warp_fwd_matches_oracle():
     assert (wm.cpu().double() - rw).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("where", ["side", "wgrad"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
 @pytest.mark.parametrize("cfg", ["config2", "config4"])
-def test_adam_overlap_matches_plain(cfg, graph):
+def test_adam_overlap_matches_plain(cfg, graph, where):
     """Bucketed Adam on a side stream during backward (Trainer.enable_adam_overlap; a graph branch under
     capture) updates every element as the single Adam launch after backward: parameters and moments
     bit-identical.  Config 2 after three steps; config 4 (shared-variable nets: a bucket is final only at
     its net's second backward call) after one step with the depth / consistency weight 0, so its
     float-atomic scatter adds only zeros and the step is deterministic (two plain runs are checked to
     agree bit for bit first).  With that term on, run-to-run rounding of the atomics makes Adam's first
-    update flip sign on near-zero gradients, which no tolerance separates from a wrong bucket."""
+    update flip sign on near-zero gradients, which no tolerance separates from a wrong bucket.
+    where="wgrad": the buckets run on the programs' filter-gradient streams (enable_wgrad_overlap), against
+    the same split backward run serially with the single Adam launch after it."""
     from tf_depth_estimation_amd import _api, train, variables
     steps = 3 if cfg == "config2" else 1
 
@@ -284,8 +287,10 @@ def test_adam_overlap_matches_plain(cfg, graph):
             tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
                          torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
                          small_pose(B, 4).cuda())
+        if where == "wgrad":
+            tr.enable_wgrad_overlap(serial=not overlap)
         if overlap:
-            ov = tr.enable_adam_overlap(bucket_mb=0.5)
+            ov = tr.enable_adam_overlap(bucket_mb=0.5, on_wgrad_stream=(where == "wgrad"))
             assert len(ov.buckets) > 4
         if graph:
             tr.capture(warmup=1)

@@ -56,10 +56,13 @@ class AdamOverlap:
     kernel work: under capture the side stream becomes a graph branch (fork at each bucket's event,
     one join before the step ends)."""
 
-    def __init__(self, opts, bucket_mb=16.0, uses=None, pre_launch=None):
+    def __init__(self, opts, bucket_mb=16.0, uses=None, pre_launch=None, streams=None):
         from .ddp import make_buckets
         self.opts = list(opts)
         self.pre_launch = pre_launch
+        # streams: {id(chunk): stream} -- run a chunk's buckets on that stream (its program's filter-gradient
+        # stream, which already holds the chunk's last weight gradients in order: no join with it needed)
+        self.streams = dict(streams or {})
         self.buckets = []
         self.by_param = {}
         for o in self.opts:
@@ -98,21 +101,37 @@ class AdamOverlap:
         return on_grads
 
     def launch(self, buckets):
-        if self.pre_launch is not None:
-            self.pre_launch()
+        # the event orders each update after everything the compute stream has issued so far: the op that
+        # reported the gradients, and the data-gradient GEMM that still READ these parameters
         ev = torch.cuda.Event()
         ev.record()
-        self.side.wait_event(ev)
-        with torch.cuda.stream(self.side):
-            for b in buckets:
+        on_side = [b for b in buckets if id(b.chunk) not in self.streams]
+        if on_side:
+            if self.pre_launch is not None:
+                self.pre_launch()
+                ev = torch.cuda.Event()
+                ev.record()
+            self.side.wait_event(ev)
+            with torch.cuda.stream(self.side):
+                for b in on_side:
+                    b.opt.update(b.lo, b.hi)
+                    self.done.add(id(b))
+        for b in buckets:
+            st = self.streams.get(id(b.chunk))
+            if st is None:
+                continue
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
                 b.opt.update(b.lo, b.hi)
-                self.done.add(id(b))
+            self.done.add(id(b))
 
     def finish(self):
         rest = [b for b in self.buckets if id(b) not in self.done]
         if rest:
             self.launch(rest)
         torch.cuda.current_stream().wait_stream(self.side)
+        for st in set(self.streams.values()):
+            torch.cuda.current_stream().wait_stream(st)
 
 
 class AllReduceGrads:
@@ -146,14 +165,22 @@ class Trainer:
 
     adam_ov = None
 
-    def enable_adam_overlap(self, bucket_mb=16.0):
+    def enable_adam_overlap(self, bucket_mb=16.0, on_wgrad_stream=False):
         """Run each gradient bucket's Adam on a side stream as soon as backward finalises it (single GPU;
-        with a data-parallel exchange the update must wait for the all-reduce)."""
+        with a data-parallel exchange the update must wait for the all-reduce).  on_wgrad_stream: on each
+        program's filter-gradient stream (enable_wgrad_overlap first), behind the filter gradients it holds,
+        so the compute stream never waits for it until the end of the step."""
         if self.grad_sync is not None:
             raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
+        streams = {}
+        if on_wgrad_stream:
+            for p in self.programs():
+                if p.wgrad_stream is None or isinstance(p.wgrad_stream, str):
+                    raise ValueError("on_wgrad_stream needs enable_wgrad_overlap() (a side stream) first")
+                streams[id(p.chunk)] = p.wgrad_stream
         self.adam_ov = AdamOverlap(opts, bucket_mb, {id(c): self.BACKWARD_USES for c in self.chunks},
-                                   pre_launch=self.join_wgrad)
+                                   pre_launch=self.join_wgrad, streams=streams)
         return self.adam_ov
 
     def enable_wgrad_overlap(self, on=True, serial=False):
