@@ -251,6 +251,8 @@ BN_FUSED_CASES = [
     (False, 8, 96, 128, 4, 32, 7, 2),            # cnv1: 768 row tiles, no split
     (False, 8, 2, 2, 512, 512, 3, 1),            # cnv7b-like: split-K 36, last-block reduce
     (False, 4, 24, 32, 256, 128, 3, 1),          # split-K with several row tiles
+    (False, 8, 12, 16, 256, 256, 3, 1),          # icnv5-like, M 1536: split-K reduce fused into the small BN
+    (False, 8, 24, 32, 128, 256, 3, 2),          # cnv4-like, M 1536, stride 2, the same fused launch
     (False, 3, 13, 17, 32, 64, 5, 2),            # ragged tiles
     (True, 2, 6, 8, 32, 16, 3, 2),               # deconv: 4 parity classes
     (True, 8, 1, 1, 512, 512, 3, 2),             # upcnv7-like (1x1 -> 2x2), split-K over classes
