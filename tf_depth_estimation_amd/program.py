@@ -15,11 +15,22 @@ accumulate into the ParamChunk's flat gradient buffer, which the trainer zeroes 
 network called twice with shared variables (train_depth_then_cam_lr.py:130-136) sums both calls like
 TF does.
 """
+import os
+
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import ConvDesc, ptr
+
+
+def _env_pos(name, default):
+    """Positive integer tuning knob from the environment (missing / non-numeric / non-positive: default)."""
+    try:
+        v = int(os.environ.get(name, ""))
+    except ValueError:
+        return default
+    return v if v > 0 else default
 
 
 def same_pad(n, k, s):
@@ -268,8 +279,13 @@ class NetProgram:
         self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
         # filter-gradient overlap (enable_wgrad_overlap): side stream, its workspace per batch, dz ring
         self.wgrad_stream = None
+        self.wgrad_group = _env_pos("TDE_WGRAD_GROUP", 1)
+        # the last `wgrad_tail` conv layers of backward (the first of forward) keep their filter gradient on the
+        # compute stream (fused launch): the side stream's backlog at the end of backward is what the compute
+        # stream waits for
+        self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 0)
         self._ws2 = {}
-        self._dz2 = {}
+        self._dzl = {}
 
     def _sums(self, i, K, which):
         key = (i, which)
@@ -318,13 +334,14 @@ class NetProgram:
     def enable_wgrad_overlap(self, on=True, serial=False):
         """Take the filter gradients off backward's critical path: each conv/deconv's data gradient runs on
         the current stream and its filter gradient (tde_conv2d_bwd_filter / tde_deconv2d_bwd_filter) on a side
-        stream that waits for the layer's dz, with its own workspace; the BN backward alternates between two
-        dz buffers and waits for the filter gradient that last read the one it overwrites.  Nothing on the
-        data-gradient chain waits for a filter gradient (TF's Conv2DBackpropFilter has no consumer but the
-        optimizer), so under capture the side stream is a parallel graph branch joined at the end of
-        backward (and before any gradient-exchange launch point: join_wgrad()).  The two GEMMs are the
-        separate data- and filter-gradient calls (their own tile plans, not the fused launch's shared tile),
-        so results equal serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
+        stream, with its own workspace.  Every layer's BN backward writes its own dz buffer, so nothing on the
+        data-gradient chain ever waits for a filter gradient (TF's Conv2DBackpropFilter has no consumer but
+        the optimizer): the side stream only waits for the compute stream, once per `wgrad_group` conv
+        layers (TDE_WGRAD_GROUP; each cross-stream edge of a captured graph costs the stream that waits
+        ~5 us), and under capture it is a parallel graph branch joined at the end of backward (and before
+        any gradient-exchange launch point: join_wgrad()).  The two GEMMs are the separate data- and
+        filter-gradient calls (their own tile plans, not the fused launch's shared tile), so results equal
+        serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
         self.wgrad_stream = (SERIAL if serial else torch.cuda.Stream()) if on else None
         return self
 
@@ -332,16 +349,41 @@ class NetProgram:
         """Order the current stream after every filter gradient launched so far (the dz ring is then free:
         its events are dropped, so none is waited on across a graph-segment boundary)."""
         if self.wgrad_stream is not None:
+            self._flush_wgrad()
             if self.wgrad_stream is not SERIAL:
                 torch.cuda.current_stream().wait_stream(self.wgrad_stream)
-            ring = getattr(self, "_ev_ring", None)
-            if ring is not None:
-                ring[0] = ring[1] = None
+
+    def _flush_wgrad(self, ev=None):
+        """Issue the deferred filter gradients on the side stream behind ONE wait for the compute stream: on
+        `ev` (recorded on it after the last of their dz was written) or on everything issued so far."""
+        pending = getattr(self, "_wg_pending", None)
+        if not pending:
+            return
+        side = self.wgrad_stream
+        if side is SERIAL:
+            side = torch.cuda.current_stream()
+        elif ev is not None:
+            side.wait_event(ev)
+        else:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for fn, _ in pending:
+                fn()
+        self._wg_issued.extend(n for _, names in pending for n in names)
+        pending.clear()
 
     def _scratch_side(self, N):
-        ws, dz = self._scratch(N)
+        ws, _ = self._scratch(N)
         w = self._ws2.setdefault(N, Workspace())
-        return w.get(ws.numel() * 4, dz.numel(), "cuda")
+        return w.get(ws.numel() * 4, 4, "cuda")
+
+    def _dz_layer(self, N, i, numel):
+        """Layer i's own dz buffer (filter-gradient overlap): never reused within a backward call, so the
+        BN backward never waits for the filter gradient that reads it."""
+        t = self._dzl.get((N, i))
+        if t is None or t.numel() < numel:
+            t = self._dzl[(N, i)] = torch.empty(max(numel, 4), dtype=torch.float32, device="cuda")
+        return t
 
     def _scratch(self, N):
         if N not in self._sizes:
@@ -503,17 +545,20 @@ class NetProgram:
         if side is SERIAL:
             side = torch.cuda.current_stream()
         if side is not None:
-            ws2, dz_b = self._scratch_side(N)
+            ws2, _ = self._scratch_side(N)
             wsb2 = ws2.numel() * 4
-            dz_ring, nconv = (dz, dz_b), 0
-            ev_ring = self._ev_ring = [None, None]
-            side.wait_stream(torch.cuda.current_stream())   # the side stream's first use of this step's state
+            self._wg_pending, self._wg_issued = [], []
+        conv_rank = {}
+        for j, o in enumerate(spec.ops):
+            if isinstance(o, ConvBN):
+                conv_rank[j] = len(conv_rank)
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
             if isinstance(op, ConvBN):
+                use_side = side is not None and conv_rank[i] >= self.wgrad_tail
                 d = op.desc(N)
                 # dz (the conv's output gradient) is the y view of a conv's descriptor, the x view of a deconv's
                 if op.deconv:
@@ -523,12 +568,7 @@ class NetProgram:
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats[i]
                 if side is not None:
-                    # dz ring: wait for the filter gradient that read this buffer two conv layers ago
-                    slot = nconv & 1
-                    nconv += 1
-                    dz = dz_ring[slot]
-                    if ev_ring[slot] is not None:
-                        torch.cuda.current_stream().wait_event(ev_ring[slot])
+                    dz = self._dz_layer(N, i, M * op.K)
                 if self.bn_sync is not None:
                     # SyncBN backward: local (sum g, sum g*xhat) -> all-reduced copy -> dz from the global means,
                     # dbeta from the local sum (the gradient all-reduce averages it like every parameter)
@@ -553,9 +593,23 @@ class NetProgram:
                                                   run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
-                if side is not None:
-                    ev = torch.cuda.Event()
-                    ev.record()
+                if use_side:
+                    # this layer's filter gradient joins the deferred group; the group goes to the side stream
+                    # behind one event recorded after the BN backward that completes it.  The data gradient is
+                    # issued BEFORE the side stream waits on that event: under capture the graph executor keeps
+                    # a node's first-added successor on the node's own HW queue, so the data-gradient chain
+                    # stays on one queue and only the filter-gradient branch forks off it
+                    wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
+                    a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
+
+                    def wgrad_call(wg=wg, d=d, a1=a1, a2=a2, gw=gw, layer=op.layer):
+                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws2), wsb2, _lib.stream_ptr()),
+                                   layer + " wgrad")
+                    self._wg_pending.append((wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
+                    ev = None
+                    if len(self._wg_pending) >= self.wgrad_group:
+                        ev = torch.cuda.Event()
+                        ev.record()
                     if src_needs:
                         acc = mark(op.src)
                         if op.deconv:
@@ -564,14 +618,8 @@ class NetProgram:
                         else:
                             _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
                                                                acc, ptr(ws), wsb, st), op.layer + " bwd data")
-                    side.wait_event(ev)
-                    with torch.cuda.stream(side):
-                        wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
-                        a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
-                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws2), wsb2, _lib.stream_ptr()),
-                                   op.layer + " wgrad")
-                        ev_ring[slot] = torch.cuda.Event()
-                        ev_ring[slot].record()
+                    if ev is not None:
+                        self._flush_wgrad(ev)
                 elif src_needs:
                     # data + filter gradient: one fused launch (tde_conv2d_bwd / tde_deconv2d_bwd)
                     acc = mark(op.src)
@@ -590,7 +638,15 @@ class NetProgram:
                     a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
                     with self._span("conv_wgrad", fl, conv_bytes(op, N)):
                         _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
-                if on_grads is not None:
+                if side is not None:
+                    # report the parameters of the filter gradients issued so far (a deferred one is reported
+                    # once its group is on the side stream)
+                    names, self._wg_issued = self._wg_issued, []
+                    if not use_side:
+                        names += [f"{self.prefix}/{n}" for n, _, _ in op.params]
+                    if on_grads is not None and names:
+                        on_grads(names)
+                elif on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Head):
                 d = op.desc(N)
@@ -616,6 +672,10 @@ class NetProgram:
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
         if side is not None:
+            self._flush_wgrad()
+            names, self._wg_issued = self._wg_issued, []
+            if on_grads is not None and names:
+                on_grads(names)
             self.join_wgrad()
         if need_input_grad:
             return run.view_tensor(iv, grad=True)[..., :spec.cin]
