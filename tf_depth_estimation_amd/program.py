@@ -283,7 +283,7 @@ class NetProgram:
         # the last `wgrad_tail` conv layers of backward (the first of forward) keep their filter gradient on the
         # compute stream (fused launch): the side stream's backlog at the end of backward is what the compute
         # stream waits for
-        self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 0)
+        self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 1)
         self._ws2 = {}
         self._dzl = {}
 
