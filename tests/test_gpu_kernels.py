@@ -391,6 +391,11 @@ HEAD_CASES = [
     (4, 96, 128, 16, 1, 3, 1, 4.0, 0.0, 20, 4),      # many wgrad chunks, offset view
     (2, 48, 64, 32, 2, 5, 0, 1.0, 0.0, 32, 0),       # exp/mask2 shape: 25 taps = 5 tap groups
     (2, 48, 64, 16, 2, 7, 0, 1.0, 0.0, 16, 0),       # exp/mask1 shape: 49 taps = 10 tap groups
+    # >= 32768 pixels: the LDS-tiled head kernels (head_t*_kernel), 16 x 64 output tiles
+    (3, 96, 128, 16, 2, 7, 1, 4.0, 0.0, 16, 0),      # mask1-like, sigmoid
+    (2, 150, 130, 32, 2, 5, 0, 1.0, 0.0, 32, 0),     # ragged rows and columns, 2 channel groups (dgrad)
+    (1, 190, 200, 64, 1, 3, 1, 10.0, 0.001, 68, 4),  # 4 channel groups, offset view, ragged
+    (2, 130, 160, 32, 1, 3, 0, 1.0, 0.0, 32, 0),     # disp2-like
 ]
 
 

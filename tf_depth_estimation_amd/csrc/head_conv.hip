@@ -240,6 +240,312 @@ __global__ void __launch_bounds__(256) head_dgrad_kernel(const HeadArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ tiled heads (high resolution, C <= 64)
+// The direct kernels above re-read every activation once per tap from L1/L2 (49x for the 7x7 mask1 head of
+// depth_net: 1.2 GB of cache traffic per config-4 call).  These stage an output tile's input halo in LDS once
+// per 4-channel chunk and slide a register window along each thread's row segment, so each staged value
+// feeds KS x PX x KC FMAs.  Weights are wave-uniform (scalar loads).  Stride 1, KS x KS, K <= 2.
+//   tfwd  : thread = 4 consecutive output pixels of one row, all K outputs; halo chunks double-buffered.
+//   tdgrad: thread = 4 consecutive input pixels x 16 channels; the dz halo (computed from y, dy at staging).
+//   twgrad: thread = (kernel row, row lane); a KS x 4 x K register tile per chunk, lane sums by xor shuffles,
+//           one partial row per tile (head_wgrad_reduce_kernel sums the tiles in a fixed order).
+constexpr int HT_TW = 64, HT_TH = 16, HT_PX = 4, HT_SEG = HT_TW / HT_PX;
+
+template <int KS, int TH = HT_TH>
+struct HaloGeom {
+  static constexpr int HW = HT_TW + KS - 1;        // halo width (pixels)
+  static constexpr int PITCH = HW | 1;             // odd f4 row pitch: rows of a lane group hit distinct banks
+  static constexpr int HH = TH + KS - 1;
+  static constexpr int NSLOT = HH * PITCH;
+  static constexpr int LPT = (HH * HW + 255) / 256;   // staging loads per thread
+};
+
+struct TileIdx {
+  int n, oh0, ow0;
+};
+__device__ __forceinline__ TileIdx tile_of(int b, int tiles_w, int tiles_h, int th) {
+  TileIdx t;
+  const int tw = b % tiles_w;
+  const int r = b / tiles_w;
+  t.oh0 = (r % tiles_h) * th;
+  t.n = r / tiles_h;
+  t.ow0 = tw * HT_TW;
+  return t;
+}
+
+// halo element i of channel chunk cq: byte offset into x (or OOB)
+template <int KS, int TH = HT_TH>
+__device__ __forceinline__ int halo_off(const HeadArgs& p, const TileIdx& t, int i, int cq) {
+  using G = HaloGeom<KS, TH>;
+  const int hr = i / G::HW, hc = i - hr * G::HW;
+  const int ih = t.oh0 - p.PT + hr, iw = t.ow0 - p.PL + hc;
+  const bool ok = i < G::HH * G::HW && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && 4 * cq < p.wcin;
+  return ok ? 4 * (((t.n * p.H + ih) * p.W + iw) * p.xcs + p.xco + 4 * cq) : OOB;
+}
+
+template <int KS, int TH = HT_TH>
+__device__ __forceinline__ void halo_fetch(const HeadArgs& p, __amdgpu_buffer_rsrc_t rx, const TileIdx& t, int cq,
+                                           f4 (&r)[HaloGeom<KS, TH>::LPT]) {
+#pragma unroll
+  for (int u = 0; u < HaloGeom<KS, TH>::LPT; ++u) r[u] = bload(rx, halo_off<KS, TH>(p, t, threadIdx.x + 256 * u, cq));
+}
+
+template <int KS, int TH = HT_TH>
+__device__ __forceinline__ void halo_store(f4* sx, const f4 (&r)[HaloGeom<KS, TH>::LPT]) {
+  using G = HaloGeom<KS, TH>;
+#pragma unroll
+  for (int u = 0; u < G::LPT; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < G::HH * G::HW) {
+      const int hr = i / G::HW, hc = i - hr * G::HW;
+      sx[hr * G::PITCH + hc] = r[u];
+    }
+  }
+}
+
+// Weights staged in LDS as [tap][k][c] over the channel count padded to 4 (zeros past w_cin), so the quad
+// of 4 channels a thread multiplies is one wave-uniform (broadcast) ds_read_b128.  Capacity: KS^2 * C * K
+// <= 3200 floats (head_tiled: C <= 32 at KS 7, C <= 64 at KS <= 5).
+constexpr int HT_WMAX = 3200;
+
+template <int KC, int KS>
+__device__ __forceinline__ void stage_wt(const HeadArgs& p, float* sw) {
+  const int cp = (p.wcin + 3) & ~3;
+  const int n = KS * KS * KC * cp;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int c = i % cp, r = i / cp, k = r % KC, tap = r / KC;
+    sw[i] = c < p.wcin ? p.w[((long)tap * p.wcin + c) * KC + k] : 0.f;
+  }
+}
+
+__device__ __forceinline__ f4 wquad(const float* sw, int tap, int c, int cp, int KC, int k) {
+  return *reinterpret_cast<const f4*>(sw + (tap * KC + k) * cp + c);
+}
+
+template <int KC, int KS>
+__global__ void __launch_bounds__(256) head_tfwd_kernel(const HeadArgs p, int tiles_w, int tiles_h) {
+  using G = HaloGeom<KS>;
+  __shared__ f4 sx[2][G::NSLOT];
+  __shared__ __attribute__((aligned(16))) float sw[HT_WMAX];
+  const TileIdx t = tile_of(blockIdx.x, tiles_w, tiles_h, HT_TH);
+  const int row = threadIdx.x % HT_TH, x0 = (threadIdx.x / HT_TH) * HT_PX;
+  const int cp = (p.wcin + 3) & ~3;
+  stage_wt<KC, KS>(p, sw);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const int CQ = (p.wcin + 3) / 4;
+  float acc[HT_PX][KC];
+#pragma unroll
+  for (int i = 0; i < HT_PX; ++i)
+#pragma unroll
+    for (int k = 0; k < KC; ++k) acc[i][k] = 0.f;
+  f4 r[G::LPT];
+  halo_fetch<KS>(p, rx, t, 0, r);
+  halo_store<KS>(sx[0], r);
+  __syncthreads();
+  for (int cq = 0; cq < CQ; ++cq) {
+    if (cq + 1 < CQ) halo_fetch<KS>(p, rx, t, cq + 1, r);
+    const f4* s = sx[cq & 1];
+#pragma unroll 1
+    for (int kh = 0; kh < KS; ++kh) {
+      f4 win[HT_PX + KS - 1];
+#pragma unroll
+      for (int j = 0; j < HT_PX + KS - 1; ++j) win[j] = s[(row + kh) * G::PITCH + x0 + j];
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const f4 wv = wquad(sw, kh * KS + kw, 4 * cq, cp, KC, k);
+#pragma unroll
+          for (int i = 0; i < HT_PX; ++i) {
+            const f4 xv = win[i + kw];
+            acc[i][k] = fmaf(xv[0], wv[0], fmaf(xv[1], wv[1], fmaf(xv[2], wv[2], fmaf(xv[3], wv[3], acc[i][k]))));
+          }
+        }
+        // keep each tap's weight reads next to their FMAs (hoisting all taps' reads costs occupancy)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (cq + 1 < CQ) halo_store<KS>(sx[(cq + 1) & 1], r);
+    __syncthreads();
+  }
+  const int oh = t.oh0 + row;
+  if (oh >= p.OH) return;
+#pragma unroll
+  for (int i = 0; i < HT_PX; ++i) {
+    const int ow = t.ow0 + x0 + i;
+    if (ow < p.OW) {
+      float* yp = p.y + ((long)(t.n * p.OH + oh) * p.OW + ow) * p.ycs + p.yco;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[i][k] + p.b[k], p.act, p.scale, p.offset);
+    }
+  }
+}
+
+// dz = dL/d(pre-activation) of output pixel (oh, ow), zero outside the image
+template <int KC>
+__device__ __forceinline__ void dz_at(const HeadArgs& p, int n, int oh, int ow, float (&d)[KC]) {
+  const bool ok = (unsigned)oh < (unsigned)p.OH && (unsigned)ow < (unsigned)p.OW;
+  const long o = ((long)(n * p.OH + (ok ? oh : 0)) * p.OW + (ok ? ow : 0)) * p.ycs + p.yco;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) d[k] = ok ? head_dz(p.yin[o + k], p.dy[o + k], p.act, p.scale, p.offset) : 0.f;
+}
+
+// NG channel groups of 16 (C = 16 * NG); rows per tile 16 / NG
+template <int KC, int KS, int NG>
+__global__ void __launch_bounds__(256) head_tdgrad_kernel(const HeadArgs p, int tiles_w, int tiles_h) {
+  constexpr int TH = HT_TH / NG, HW = HT_TW + KS - 1, PITCH = HW | 1, HH = TH + KS - 1;
+  constexpr int CG = 16;
+  __shared__ float sdz[HH * PITCH * KC];
+  __shared__ __attribute__((aligned(16))) float sw[HT_WMAX];
+  const TileIdx t = tile_of(blockIdx.x, tiles_w, tiles_h, TH);
+  const int cp = (p.wcin + 3) & ~3;
+  stage_wt<KC, KS>(p, sw);
+  // dz halo: output pixels (ih0 + PT - (KS-1) + hr, iw0 + PL - (KS-1) + hc)
+  for (int i = threadIdx.x; i < HH * HW; i += 256) {
+    const int hr = i / HW, hc = i - hr * HW;
+    float d[KC];
+    dz_at<KC>(p, t.n, t.oh0 + p.PT - (KS - 1) + hr, t.ow0 + p.PL - (KS - 1) + hc, d);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) sdz[(hr * PITCH + hc) * KC + k] = d[k];
+  }
+  __syncthreads();
+  const int row = threadIdx.x % TH, seg = (threadIdx.x / TH) % HT_SEG, g = threadIdx.x / (TH * HT_SEG);
+  const int x0 = seg * HT_PX, c0 = g * CG;
+  f4 acc[HT_PX][CG / 4];
+#pragma unroll
+  for (int i = 0; i < HT_PX; ++i)
+#pragma unroll
+    for (int q = 0; q < CG / 4; ++q) acc[i][q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll 1
+    for (int kw = 0; kw < KS; ++kw) {
+      // dz of the 4 output pixels this tap maps the thread's input pixels to, and the tap's weight quads
+      const float* dzp = sdz + ((row + KS - 1 - kh) * PITCH + x0 + KS - 1 - kw) * KC;
+      float dv[HT_PX][KC];
+#pragma unroll
+      for (int i = 0; i < HT_PX; ++i)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) dv[i][k] = dzp[i * KC + k];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+#pragma unroll
+        for (int q = 0; q < CG / 4; ++q) {
+          const f4 wv = c0 + 4 * q < cp ? wquad(sw, kh * KS + kw, c0 + 4 * q, cp, KC, k) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < HT_PX; ++i) acc[i][q] += dv[i][k] * wv;
+        }
+      }
+    }
+  }
+  const int ih = t.oh0 + row;
+  if (ih >= p.H) return;
+#pragma unroll
+  for (int i = 0; i < HT_PX; ++i) {
+    const int iw = t.ow0 + x0 + i;
+    if (iw < p.W) {
+      float* dst = p.dx + ((long)(t.n * p.H + ih) * p.W + iw) * p.xcs + p.xco + c0;
+#pragma unroll
+      for (int q = 0; q < CG / 4; ++q) {
+        f4 o = acc[i][q];
+        if (p.acc_dx) o += *reinterpret_cast<const f4*>(dst + 4 * q);
+        *reinterpret_cast<f4*>(dst + 4 * q) = o;
+      }
+    }
+  }
+}
+
+// lanes per tap: L consecutive lanes share one tap's outputs and split the tile's pixels (xor-shuffle sum
+// within L <= 16 lanes); KS 3 / 5 / 7 -> 144 / 200 / 196 active threads
+template <int KS>
+struct TwLanes { static constexpr int L = KS == 3 ? 16 : (KS == 5 ? 8 : 4); };
+constexpr int HT_TWG_TH = 8;   // filter-gradient tile rows (more tiles than the forward's 16: fills the chip)
+
+template <int KC, int KS>
+__global__ void __launch_bounds__(256) head_twgrad_kernel(const HeadArgs p, int tiles_w, int tiles_h, float* part) {
+  constexpr int TH = HT_TWG_TH;
+  using G = HaloGeom<KS, TH>;
+  constexpr int L = TwLanes<KS>::L, NPX = TH * HT_TW;
+  __shared__ f4 sx[2][G::NSLOT];
+  __shared__ float sdz[NPX * KC];
+  __shared__ float sb[4][KC];
+  const TileIdx t = tile_of(blockIdx.x, tiles_w, tiles_h, TH);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const int E = KS * KS * p.wcin;
+  // partials transposed, part[output][tile]: head_wgrad_reduce_t_kernel reads each output's row contiguously
+  const long R = gridDim.x;
+  float* out = part + blockIdx.x;
+  f4 r[G::LPT];
+  halo_fetch<KS, TH>(p, rx, t, 0, r);
+  // dz of the tile's own output pixels, and their sums (the bias gradient)
+  float bs[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) bs[k] = 0.f;
+  for (int i = threadIdx.x; i < NPX; i += 256) {
+    float d[KC];
+    dz_at<KC>(p, t.n, t.oh0 + i / HT_TW, t.ow0 + i % HT_TW, d);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) { sdz[i * KC + k] = d[k]; bs[k] += d[k]; }
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bs[k] += __shfl_xor(bs[k], o, 64);
+    if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6][k] = bs[k];
+  }
+  halo_store<KS, TH>(sx[0], r);
+  __syncthreads();
+  if (threadIdx.x < KC)
+    out[(E * KC + threadIdx.x) * R] = ((sb[0][threadIdx.x] + sb[1][threadIdx.x]) + sb[2][threadIdx.x]) + sb[3][threadIdx.x];
+  const int tap = threadIdx.x / L, l = threadIdx.x % L;
+  const int kh = tap / KS, kw = tap - kh * KS;
+  const bool active = tap < KS * KS;
+  const int CQ = (p.wcin + 3) / 4;
+  for (int cq = 0; cq < CQ; ++cq) {
+    if (cq + 1 < CQ) halo_fetch<KS, TH>(p, rx, t, cq + 1, r);
+    float acc[4][KC];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) acc[j][k] = 0.f;
+    if (active) {
+      const f4* s = sx[cq & 1] + kh * G::PITCH + kw;
+#pragma unroll 8
+      for (int px = l; px < NPX; px += L) {
+        const int row = px / HT_TW, col = px - row * HT_TW;
+        const f4 xv = s[row * G::PITCH + col];
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const float d = sdz[px * KC + k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j][k] = fmaf(xv[j], d, acc[j][k]);
+        }
+      }
+    }
+    // sum over the L lanes of this tap (fixed xor order), lane 0 writes the tile's partial
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        float v = acc[j][k];
+#pragma unroll
+        for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[j][k] = v;
+      }
+    if (active && l == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * cq + j;
+        if (c < p.wcin)
+#pragma unroll
+          for (int k = 0; k < KC; ++k) out[((tap * p.wcin + c) * KC + k) * R] = acc[j][k];
+      }
+    }
+    if (cq + 1 < CQ) halo_store<KS, TH>(sx[(cq + 1) & 1], r);
+    __syncthreads();
+  }
+}
+
 // taps per wgrad block: TT * 4 * KC accumulators per thread
 template <int KC>
 struct WgTaps { static constexpr int TT = KC == 1 ? 9 : (KC == 2 ? 5 : 2); };
@@ -372,6 +678,28 @@ __global__ void __launch_bounds__(1024) head_wgrad_reduce_kernel(const float* pa
   *dst = accumulate ? *dst + (float)s : (float)s;
 }
 
+// Sum of the transposed tiled partials part[output][rows]: one wave per output, lanes over rows in a fixed
+// order (fp64), xor-tree combine.
+__global__ void __launch_bounds__(64) head_wgrad_reduce_t_kernel(const float* part, int rows, int nw, float* dw,
+                                                                  float* db, int accumulate) {
+  const float* src = part + (long)blockIdx.x * rows;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  int r = threadIdx.x;
+  for (; r + 192 < rows; r += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += src[r + 64 * u];
+  }
+  for (int u = 0; r < rows; r += 64, ++u) a[u & 3] += src[r];
+  double s = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (threadIdx.x == 0) {
+    const int i = blockIdx.x;
+    float* dst = (i < nw) ? dw + i : db + (i - nw);
+    *dst = accumulate ? *dst + (float)s : (float)s;
+  }
+}
+
 struct WgPlan {
   int chunks, ppc, tgroups;
 };
@@ -396,6 +724,25 @@ WgPlan wg_plan(const tde_conv_desc_t* d) {
   w.ppc = (int)((M + chunks - 1) / chunks);
   w.chunks = (int)((M + w.ppc - 1) / w.ppc);
   return w;
+}
+
+// tiled path (head_t*_kernel): stride-1 square KS in {3,5,7}, K <= 2, C = 16 * {1,2,4}, at least
+// TDE_HEAD_TILE_MIN output pixels (default 32768; below it the direct kernels' parallelism wins); TDE_HEAD_TILE=0
+// turns it off
+static const long g_head_tile_min = tde_env_pos("TDE_HEAD_TILE_MIN", 32768);
+static const bool g_head_tile_on = !(std::getenv("TDE_HEAD_TILE") && std::atol(std::getenv("TDE_HEAD_TILE")) == 0);
+
+bool head_tiled(const tde_conv_desc_t* d) {
+  return g_head_tile_on && d->stride == 1 && d->KH == d->KW && (d->KH == 3 || d->KH == 5 || d->KH == 7) &&
+         (d->K == 1 || d->K == 2) && (d->C == 16 || d->C == 32 || d->C == 64) && d->OH == d->H && d->OW == d->W &&
+         d->KH * d->KH * d->C * d->K <= HT_WMAX &&
+         d->W >= 32 && (long)d->N * d->H * d->W >= g_head_tile_min;
+}
+
+int head_ng(const tde_conv_desc_t* d) { return d->C / 16; }
+
+long head_tiles(const tde_conv_desc_t* d, int th) {
+  return (long)d->N * ((d->OH + th - 1) / th) * ((d->OW + HT_TW - 1) / HT_TW);
 }
 
 bool head_desc_ok(const tde_conv_desc_t* d) {
@@ -476,6 +823,38 @@ int launch_fwd(const HeadArgs& a, long M, hipStream_t st) {
   return TDE_OK;
 }
 
+template <int KC, int KS>
+void launch_tiled_ks(const tde_conv_desc_t* d, const HeadArgs& a, int which, float* part, hipStream_t st) {
+  const int tw = (d->OW + HT_TW - 1) / HT_TW;
+  if (which == 0) {
+    hipLaunchKernelGGL((head_tfwd_kernel<KC, KS>), dim3(head_tiles(d, HT_TH)), dim3(256), 0, st, a, tw,
+                       (d->OH + HT_TH - 1) / HT_TH);
+  } else if (which == 1) {
+    const int ng = head_ng(d), th = HT_TH / ng;
+    const dim3 g(head_tiles(d, th));
+    const int thn = (d->H + th - 1) / th;
+    if (ng == 1) hipLaunchKernelGGL((head_tdgrad_kernel<KC, KS, 1>), g, dim3(256), 0, st, a, tw, thn);
+    else if (ng == 2) hipLaunchKernelGGL((head_tdgrad_kernel<KC, KS, 2>), g, dim3(256), 0, st, a, tw, thn);
+    else hipLaunchKernelGGL((head_tdgrad_kernel<KC, KS, 4>), g, dim3(256), 0, st, a, tw, thn);
+  } else {
+    hipLaunchKernelGGL((head_twgrad_kernel<KC, KS>), dim3(head_tiles(d, HT_TWG_TH)), dim3(256), 0, st, a, tw,
+                       (d->OH + HT_TWG_TH - 1) / HT_TWG_TH, part);
+  }
+}
+
+// which: 0 forward, 1 data gradient, 2 filter-gradient partials (one row per HT_TH x HT_TW tile)
+void launch_tiled(const tde_conv_desc_t* d, const HeadArgs& a, int which, float* part, hipStream_t st) {
+  const int key = d->K * 10 + d->KH;
+  switch (key) {
+    case 13: launch_tiled_ks<1, 3>(d, a, which, part, st); break;
+    case 15: launch_tiled_ks<1, 5>(d, a, which, part, st); break;
+    case 17: launch_tiled_ks<1, 7>(d, a, which, part, st); break;
+    case 23: launch_tiled_ks<2, 3>(d, a, which, part, st); break;
+    case 25: launch_tiled_ks<2, 5>(d, a, which, part, st); break;
+    default: launch_tiled_ks<2, 7>(d, a, which, part, st); break;
+  }
+}
+
 template <int KC>
 int launch_dgrad(const HeadArgs& a, hipStream_t st) {
   const long n = (long)a.N * a.H * a.W * (a.C / 4);
@@ -509,7 +888,8 @@ extern "C" {
 size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
   const WgPlan w = wg_plan(d);
-  const size_t part = (size_t)w.chunks * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
+  const long rows = head_tiled(d) ? head_tiles(d, HT_TWG_TH) : w.chunks;
+  const size_t part = (size_t)rows * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
   return dz_bytes(d) + part;
 }
 
@@ -520,6 +900,10 @@ int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   a.x = x; a.w = w; a.b = bias; a.y = y; a.act = act; a.scale = scale; a.offset = offset;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const long M = (long)d->N * d->OH * d->OW;
+  if (head_tiled(d)) {
+    launch_tiled(d, a, 0, nullptr, st);
+    return tde_launch_status();
+  }
   switch (d->K) {
     case 1: launch_fwd<1>(a, M, st); break;
     case 2: launch_fwd<2>(a, M, st); break;
@@ -547,6 +931,18 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   a.dzw = dz;
   TDE_CHECK_ARG(!dx || tde_aligned16(dx));
   TDE_CHECK_ARG(!dw || dbias != nullptr);
+  if (head_tiled(d)) {
+    // dz recomputed from (y, dy) at each kernel's staging: no dz pass
+    const int E = d->KH * d->KW * d->w_cin;
+    const int total = E * d->K + d->K;
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
+    if (dw) launch_tiled(d, a, 2, part, st);
+    if (dx) launch_tiled(d, a, 1, nullptr, st);
+    if (dw)
+      hipLaunchKernelGGL(head_wgrad_reduce_t_kernel, dim3(total), dim3(64), 0, st, part, (int)head_tiles(d, HT_TWG_TH),
+                         E * d->K, dw, dbias, accumulate_dw);
+    return tde_launch_status();
+  }
   // the wgrad pass computes dz on the fly and stores it; without a weight gradient a dz pass does that
   if (dw) {
     float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
