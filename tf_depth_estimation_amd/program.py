@@ -343,6 +343,11 @@ class NetProgram:
         filter-gradient calls (their own tile plans, not the fused launch's shared tile), so results equal
         serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
         self.wgrad_stream = (SERIAL if serial else torch.cuda.Stream()) if on else None
+        # TDE_WGRAD_STREAMS > 1: the filter-gradient groups alternate over that many side streams (each with its
+        # own workspace), so independent filter gradients may run concurrently with each other
+        n = 1 if (serial or not on) else _env_pos("TDE_WGRAD_STREAMS", 1)
+        self.wgrad_streams = [self.wgrad_stream] + [torch.cuda.Stream() for _ in range(n - 1)] if on else []
+        self._wg_rr = 0
         return self
 
     def join_wgrad(self):
@@ -351,7 +356,8 @@ class NetProgram:
         if self.wgrad_stream is not None:
             self._flush_wgrad()
             if self.wgrad_stream is not SERIAL:
-                torch.cuda.current_stream().wait_stream(self.wgrad_stream)
+                for sd in self.wgrad_streams:
+                    torch.cuda.current_stream().wait_stream(sd)
 
     def _flush_wgrad(self, ev=None):
         """Issue the deferred filter gradients on the side stream behind ONE wait for the compute stream: on
@@ -360,22 +366,28 @@ class NetProgram:
         if not pending:
             return
         side = self.wgrad_stream
+        sidx = 0
         if side is SERIAL:
             side = torch.cuda.current_stream()
-        elif ev is not None:
-            side.wait_event(ev)
         else:
-            side.wait_stream(torch.cuda.current_stream())
+            sidx = self._wg_rr % len(self.wgrad_streams)
+            self._wg_rr += 1
+            side = self.wgrad_streams[sidx]
+            if ev is not None:
+                side.wait_event(ev)
+            else:
+                side.wait_stream(torch.cuda.current_stream())
+        ws2 = self._scratch_side(self._wg_N, sidx)
         with torch.cuda.stream(side):
             for fn, _ in pending:
-                fn()
+                fn(ptr(ws2), ws2.numel() * 4)
         self._wg_issued.extend(n for _, names in pending for n in names)
         pending.clear()
 
-    def _scratch_side(self, N):
+    def _scratch_side(self, N, sidx=0):
         ws, _ = self._scratch(N)
-        w = self._ws2.setdefault(N, Workspace())
-        return w.get(ws.numel() * 4, 4, "cuda")
+        w = self._ws2.setdefault((N, sidx), Workspace())
+        return w.get(ws.numel() * 4, 4, "cuda")[0]
 
     def _dz_layer(self, N, i, numel):
         """Layer i's own dz buffer (filter-gradient overlap): never reused within a backward call, so the
@@ -545,8 +557,7 @@ class NetProgram:
         if side is SERIAL:
             side = torch.cuda.current_stream()
         if side is not None:
-            ws2, _ = self._scratch_side(N)
-            wsb2 = ws2.numel() * 4
+            self._wg_N = N
             self._wg_pending, self._wg_issued = [], []
         conv_rank = {}
         for j, o in enumerate(spec.ops):
@@ -602,8 +613,8 @@ class NetProgram:
                     wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
                     a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
 
-                    def wgrad_call(wg=wg, d=d, a1=a1, a2=a2, gw=gw, layer=op.layer):
-                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws2), wsb2, _lib.stream_ptr()),
+                    def wgrad_call(wsp, wsb2, wg=wg, d=d, a1=a1, a2=a2, gw=gw, layer=op.layer):
+                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, wsp, wsb2, _lib.stream_ptr()),
                                    layer + " wgrad")
                     self._wg_pending.append((wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
                     ev = None

@@ -178,6 +178,8 @@ class Trainer:
             for p in self.programs():
                 if p.wgrad_stream is None or isinstance(p.wgrad_stream, str):
                     raise ValueError("on_wgrad_stream needs enable_wgrad_overlap() (a side stream) first")
+                if len(p.wgrad_streams) > 1:
+                    raise ValueError("on_wgrad_stream needs ONE filter-gradient stream (TDE_WGRAD_STREAMS=1)")
                 streams[id(p.chunk)] = p.wgrad_stream
         self.adam_ov = AdamOverlap(opts, bucket_mb, {id(c): self.BACKWARD_USES for c in self.chunks},
                                    pre_launch=self.join_wgrad, streams=streams)
