@@ -1,0 +1,14 @@
+#!/bin/bash
+# Re-entry check of the restored tree: full GPU suite, smoke, default bench, kernel-trace profile.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r02t}
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${TAG}_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/${TAG}_smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
+cat gpurun_out/${TAG}_bench.json

@@ -12,6 +12,8 @@
 // d(loss)/d(projection matrix) is reduced per block in fp64 and added with 12 atomics per block.
 #include "tde_common.h"
 
+#include <algorithm>
+
 namespace {
 
 struct Tap4 {
@@ -44,13 +46,14 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
   __shared__ double sh[16][4];
   const int b = blockIdx.y;
   const int HW = a.H * a.W;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  // per-thread fp64 accumulators over a grid-stride loop: a capped grid (tde_warp_loss) keeps the
+  // block-end fp64 atomics on the shared loss / dL/dP words few
   double l_photo = 0, l_exp = 0, l_cons = 0;
   double gp[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) gp[i] = 0.0;
   const double inv_n3 = 1.0 / (3.0 * a.B * HW), inv_n = 1.0 / ((double)a.B * HW);
-  if (idx < HW) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < HW; idx += gridDim.x * blockDim.x) {
     const int y = idx / a.W, x = idx - y * a.W;
     const long pix = (long)b * HW + idx;
     // ---- coordinates (cam2pixel of pixel2cam) or grid + flow
@@ -101,11 +104,11 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
       p1 = e1 / (e0 + e1);
       wpix = p1;
       // softmax_cross_entropy_with_logits, label [0,1] (get_reference_explain_mask, :76-85)
-      l_exp = (double)(-(l1 - m) + logf(e0 + e1)) * a.exp_w * inv_n;
+      l_exp += (double)(-(l1 - m) + logf(e0 + e1)) * a.exp_w * inv_n;
     } else if (a.wmask) {
       wpix = a.wmask[pix];
     }
-    l_photo = (double)esum * wpix * a.photo_w * inv_n3;
+    l_photo += (double)esum * wpix * a.photo_w * inv_n3;
     // ---- left-right consistency: |z - bilinear(1/disp_other)(u,v)| * p1 (utils_lr.py:369-458)
     float g_z = 0.f, g_o = 0.f, cons = 0.f, o = 0.f;
     const float* Do = a.disp_other ? a.disp_other + (long)b * HW * a.other_cs + a.other_co : nullptr;
@@ -118,7 +121,7 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
       o = w00 * o00 + w01 * o01 + w10 * o10 + w11 * o11;
       const float dzo = z - o;
       cons = fabsf(dzo);
-      l_cons = (double)cons * p1 * a.consist_w * inv_n;
+      l_cons += (double)cons * p1 * a.consist_w * inv_n;
       const float gc = (float)(a.consist_w * inv_n) * p1 * tde_sign(dzo);
       g_z = gc;
       g_o = -gc;
@@ -171,10 +174,10 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
         const float gps[3] = {gp0, gp1, gp2};
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-          gp[4 * i + 0] = gps[i] * cam[0];
-          gp[4 * i + 1] = gps[i] * cam[1];
-          gp[4 * i + 2] = gps[i] * cam[2];
-          gp[4 * i + 3] = gps[i];
+          gp[4 * i + 0] += gps[i] * cam[0];
+          gp[4 * i + 1] += gps[i] * cam[1];
+          gp[4 * i + 2] += gps[i] * cam[2];
+          gp[4 * i + 3] += gps[i];
         }
       }
       // cam = dep * Kinv [x y 1]  ->  d dep = gcam . (cam / dep);  disp = 1/dep -> d disp = -d dep / disp^2
@@ -647,7 +650,13 @@ int tde_warp_loss(const tde_warp_loss_t* a, void* stream) {
   TDE_CHECK_ARG((a->disp != nullptr) != (a->flow != nullptr));
   TDE_CHECK_ARG(!a->disp || (a->P && a->Kinv));
   TDE_CHECK_ARG(!a->disp_other || a->disp);
-  dim3 grid((a->H * a->W + 255) / 256, a->B);
+  // <= ~512 blocks in all (each ends in up to 15 fp64 atomics on words shared by the whole grid / by its
+  // batch element); threads loop over the rest
+  static const long maxb = tde_env_pos("TDE_WARP_MAXB", 512);
+  int gx = (a->H * a->W + 255) / 256;
+  const int cap = (int)std::max(1L, maxb / a->B);
+  if (gx > cap) gx = cap;
+  dim3 grid(gx, a->B);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (a->g_P && a->disp) hipLaunchKernelGGL(warp_loss_kernel<true>, grid, dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(warp_loss_kernel<false>, grid, dim3(256), 0, st, *a);

@@ -34,6 +34,64 @@ def zero(*ts):
         _lib.check(lib.tde_zero_bytes(t.numel() * t.element_size(), ptr(t), st), "zero")
 
 
+class Arena:
+    """Per-step scratch tensors (loss accumulators, output gradients, pose gradients) carved out of ONE
+    device buffer, so a trainer clears them all with one launch (zero()) instead of one per tensor."""
+
+    def __init__(self):
+        self._specs = []
+        self.buf = None
+
+    def new(self, shape, dtype=torch.float32):
+        """Reserve a tensor; returns a callable-free placeholder index resolved by finalize()."""
+        self._specs.append((tuple(shape), dtype))
+        return len(self._specs) - 1
+
+    def finalize(self):
+        offs, off = [], 0
+        for shape, dtype in self._specs:
+            n = 1
+            for d in shape:
+                n *= d
+            nbytes = n * torch.empty((), dtype=dtype).element_size()
+            offs.append((off, n))
+            off += (nbytes + 255) // 256 * 256
+        self.buf = torch.zeros(max(off, 256), dtype=torch.uint8, device="cuda")
+        out = []
+        for (shape, dtype), (o, n) in zip(self._specs, offs):
+            esz = torch.empty((), dtype=dtype).element_size()
+            out.append(self.buf[o:o + n * esz].view(dtype).view(shape))
+        return out
+
+    def zero(self):
+        lib, st = _lib.load(), _lib.stream_ptr()
+        _lib.check(lib.tde_zero_bytes(self.buf.numel(), ptr(self.buf), st), "zero arena")
+
+
+def pyramid(preds, grads, acc, smooth_w, slot_smooth, recip=False, coff=0, label=None, l1_w=None, slot_l1=None,
+            nonfinite=False, accumulate=True):
+    """All scales of compute_smooth_loss (of channel `coff` of each preds[s], or of 1/pred) and, with a
+    label, mean|nf(resize_area(label, s) - pred_s)| in ONE launch (tde_loss_depth_pyramid): the same
+    fp32 expressions as smooth() + area() + l1() per scale.  preds[s] / grads[s]: NHWC [N,H>>s,W>>s,C]
+    dense tensors (same C); label: full-resolution [N,H,W] / [N,H,W,1]; smooth_w / l1_w: per-scale weights."""
+    n = len(preds)
+    N, H, W, C = preds[0].shape
+    a = _lib.DepthLoss()
+    a.N, a.H, a.W, a.nscales = N, H, W, n
+    for s in range(n):
+        a.pred[s] = ptr(preds[s]).value + 4 * coff
+        a.pred_cs[s], a.pred_co[s] = C, 0
+        a.grad[s] = ptr(grads[s]).value + 4 * coff
+        a.g_cs[s], a.g_co[s] = grads[s].shape[-1], 0
+        a.smooth_w[s] = float(smooth_w[s])
+        a.l1_w[s] = float(l1_w[s]) if l1_w is not None else 0.0
+    a.recip, a.nonfinite, a.grad_accumulate = int(recip), int(nonfinite), int(accumulate)
+    a.label = ptr(label) if label is not None else None
+    a.loss_smooth = dptr(acc, slot_smooth)
+    a.loss_l1 = dptr(acc, slot_l1) if slot_l1 is not None else None
+    _lib.call("tde_loss_depth_pyramid", ctypes.byref(a), _lib.stream_ptr())
+
+
 def smooth(pred, g, weight, acc, slot, recip=False, coff=0):
     """compute_smooth_loss of channel `coff` of pred (or of 1/pred) (train_depth_then_cam_lr.py:59-68)."""
     N, H, W, C = pred.shape

@@ -210,6 +210,10 @@ class NetSpec:
 
 
 SERIAL = "serial"   # enable_wgrad_overlap(serial=True): the split backward calls on the compute stream
+# forward(run, IN_PLACE): the input is already in run.input_tensor(); backward(run, [IN_PLACE, ...]): that
+# output's gradient was already written into run.grad_tensor(view) (e.g. by a loss kernel), so the step skips
+# the copy launches
+IN_PLACE = "in_place"
 
 
 class Workspace:
@@ -261,6 +265,34 @@ class NetRun:
     def view_tensor(self, v, grad=False):
         t = (self.grad if grad else self.act)[v.buf.name]
         return t[..., v.coff:v.coff + v.C]
+
+    def ensure_grad(self):
+        if self.grad is None:
+            self.grad = {b.name: torch.empty((self.N, b.H, b.W, b.cs), device=self.device, dtype=torch.float32)
+                         for b in self.prog.spec.bufs}
+        return self.grad
+
+    def bind_output_grads(self, tensors):
+        """Use the given dense [N,H,W,cs] tensors as the gradient buffers of the program's output buffers
+        (e.g. views of one per-step arena that a trainer zeroes with one launch and its loss kernels write);
+        backward(run, [IN_PLACE, ...]) then reads them where they are."""
+        self.ensure_grad()
+        for v, t in zip(self.prog.spec.outputs, tensors):
+            b = v.buf
+            if v.coff != 0 or v.C != b.cs or tuple(t.shape) != (self.N, b.H, b.W, b.cs) or not t.is_contiguous():
+                raise ValueError(f"output {b.name}: needs a dense [N,H,W,{b.cs}] tensor")
+            self.grad[b.name] = t
+
+    def input_tensor(self):
+        """The input view [N,H,W,cin] of the program's input buffer (write the batch here and call
+        forward(run, IN_PLACE) to skip the input copy)."""
+        iv = self.prog.spec.input_view
+        return self.act[iv.buf.name][..., iv.coff:iv.coff + self.prog.spec.cin]
+
+    def grad_tensor(self, v):
+        """Gradient view of output view v (a loss kernel may write it; then pass IN_PLACE to backward)."""
+        self.ensure_grad()
+        return self.view_tensor(v, True)
 
 
 class NetProgram:
@@ -431,10 +463,11 @@ class NetProgram:
         st = _lib.stream_ptr()
         spec = self.spec
         iv = spec.input_view
-        assert tuple(x.shape) == (N, spec.H, spec.W, spec.cin), (x.shape, spec.H, spec.W, spec.cin)
-        x = x.contiguous()
-        _lib.check(lib.tde_copy_view(N * spec.H * spec.W, spec.cin, ptr(x), spec.cin, 0, run.vptr(iv), iv.buf.cs, 0,
-                                     0, st), "copy input")
+        if not (isinstance(x, str) and x == IN_PLACE):
+            assert tuple(x.shape) == (N, spec.H, spec.W, spec.cin), (x.shape, spec.H, spec.W, spec.cin)
+            x = x.contiguous()
+            _lib.check(lib.tde_copy_view(N * spec.H * spec.W, spec.cin, ptr(x), spec.cin, 0, run.vptr(iv), iv.buf.cs,
+                                         0, 0, st), "copy input")
         ws, _ = self._scratch(N)
         wsb = ws.numel() * 4
         for i, op in enumerate(spec.ops):
@@ -526,8 +559,7 @@ class NetProgram:
         lib = _lib.load()
         st = _lib.stream_ptr()
         spec = self.spec
-        if run.grad is None:
-            run.grad = {b.name: torch.empty((N, b.H, b.W, b.cs), device=run.device, dtype=torch.float32) for b in spec.bufs}
+        run.ensure_grad()
         written = {b.name: [] for b in spec.bufs}
 
         def mark(v):
@@ -543,6 +575,9 @@ class NetProgram:
 
         for v, g in zip(spec.outputs, grad_outputs):
             acc = mark(v)
+            if isinstance(g, str) and g == IN_PLACE:
+                assert acc == 0, "an in-place output gradient must be the view's only gradient"
+                continue
             if g is None:
                 g = torch.empty((N, v.H, v.W, v.C), device=run.device, dtype=torch.float32)
                 _lib.check(lib.tde_fill(g.numel(), ptr(g), 0.0, st), "zero grad_out")

@@ -10,7 +10,7 @@ import torch
 
 from . import _api, _lib, _netlib, variables
 from ._lib import ptr
-from .program import NetRun
+from .program import IN_PLACE, NetRun
 
 W_CONFIG2 = dict(smooth=1.0, depth=1.0)     # train_depth_only.py:33-37
 
@@ -347,10 +347,13 @@ class DepthOnlyTrainer(Trainer):
         self.run = NetRun(self.prog, batch)
         self.opt = Adam(self.chunk, lr, beta1)
         dev = "cuda"
-        self.images = torch.zeros(batch, H, W, 3, device=dev, dtype=torch.float32)
+        # the batch lives in the program's own input buffer (forward(run, IN_PLACE): no input copy), and the
+        # loss head writes the output gradients straight into the program's gradient views (IN_PLACE)
+        self.images = self.run.input_tensor()
+        self.images.zero_()
         self.label = torch.ones(batch, H, W, 1, device=dev, dtype=torch.float32)
         outs = self.prog.spec.outputs
-        self.d_out = [torch.empty(batch, v.H, v.W, v.C, device=dev, dtype=torch.float32) for v in outs]
+        self.d_out = [IN_PLACE] * len(outs)
         self.loss = torch.zeros(1, dtype=torch.float64, device=dev)
         self.parts = torch.zeros(2, dtype=torch.float64, device=dev)   # [depth, smooth]
         a = _lib.DepthLoss()
@@ -358,8 +361,8 @@ class DepthOnlyTrainer(Trainer):
         for s, v in enumerate(outs):
             a.pred[s] = self.run.vptr(v).value + 4 * v.coff   # 1-channel view of the net output
             a.pred_cs[s], a.pred_co[s] = v.buf.cs, 0
-            a.grad[s] = self.d_out[s].data_ptr()
-            a.g_cs[s], a.g_co[s] = 1, 0
+            a.grad[s] = self.run.grad_tensor(v).data_ptr()
+            a.g_cs[s], a.g_co[s] = v.buf.cs, 0
             a.smooth_w[s] = self.w["smooth"] / 2 ** s        # train_depth_only.py:167-168
             a.l1_w[s] = self.w["depth"] / 2 ** s             # :183-184
         a.recip, a.nonfinite, a.grad_accumulate = 0, 0, 0
@@ -378,7 +381,7 @@ class DepthOnlyTrainer(Trainer):
     def phase_compute(self):
         lib, st = _lib.load(), _lib.stream_ptr()
         _lib.check(lib.tde_zero_bytes(16, ptr(self.parts), st), "zero loss")
-        outs = self.prog.forward(self.run, self.images, True)
+        outs = self.prog.forward(self.run, IN_PLACE, True)
         # the whole loss head (4 scales x (smooth + L1 to the area-downsampled label)) in one launch that
         # WRITES the output gradients (no zeroed gradient buffers)
         _lib.check(lib.tde_loss_depth_pyramid(ctypes_ref(self.loss_args), st), "depth loss head")
@@ -438,7 +441,7 @@ class DepthThenCamTrainer(Trainer):
     BACKWARD_USES = 2        # each net runs on both images (shared variables)
 
     def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
-        from .losses import W_CONFIG4, new, zero
+        from .losses import W_CONFIG4, Arena, new
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG4
         with variables.variable_scope("model_singledepth"):
@@ -457,19 +460,29 @@ class DepthThenCamTrainer(Trainer):
         self.gt_cam = new((B, 6))
         self.pair_in = {"lr": new((B, H, W, 6)), "rl": new((B, H, W, 6))}
         self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
-        self.label_pyr = [self.label] + [new(s) for s in _scale_shapes(B, H, W, 1)[1:]]
         self.Ks = [new((B, 9)) for _ in range(4)]
         so, po = self.single.spec.outputs, self.pair.spec.outputs
-        self.d_out = {k: [new((B, v.H, v.W, v.C)) for v in (so if k[0] == "s" else po)] for k in self.runs}
         self.pose = {"lr": new((B, 6)), "rl": new((B, 6))}
         self.g_pose = {"lr": new((B, 6)), "rl": new((B, 6))}
         self.T = {"lr": new((B, 16)), "rl": new((B, 16))}
-        self.gT = {"lr": new((B, 16)), "rl": new((B, 16))}
         self.P = {d: [new((B, 12)) for _ in range(4)] for d in ("lr", "rl")}
         self.Kinv = [new((B, 9)) for _ in range(4)]
-        self.gP = {d: new((4, B, 12), torch.float64) for d in ("lr", "rl")}
-        self.acc = new((8,), torch.float64)
-        self._zero = zero
+        # everything the loss head accumulates into (loss parts, dL/dP, dL/dT, the four runs' output
+        # gradients) lives in one arena: one zeroing launch per step; the output gradients are the runs'
+        # own gradient buffers (backward reads them in place)
+        ar = Arena()
+        ia = ar.new((8,), torch.float64)
+        igp = {d: ar.new((4, B, 12), torch.float64) for d in ("lr", "rl")}
+        igt = {d: ar.new((B, 16)) for d in ("lr", "rl")}
+        ido = {k: [ar.new((B, v.H, v.W, v.C)) for v in (so if k[0] == "s" else po)] for k in self.runs}
+        t = ar.finalize()
+        self.arena = ar
+        self.acc = t[ia]
+        self.gP = {d: t[i] for d, i in igp.items()}
+        self.gT = {d: t[i] for d, i in igt.items()}
+        self.d_out = {k: [t[i] for i in idx] for k, idx in ido.items()}
+        for k, run in self.runs.items():
+            run.bind_output_grads(self.d_out[k])
 
     def set_batch(self, img_l, img_r, label, K, gt_cam):
         """img_* [B,H,W,3] in [-0.5,0.5]; label = inverse depth [B,H,W,1] (NaN holes allowed);
@@ -490,8 +503,7 @@ class DepthThenCamTrainer(Trainer):
         lib, st = _lib.load(), _lib.stream_ptr()
         B, H, W, w = self.N, self.H, self.W, self.w
         M = B * H * W
-        self._zero(self.acc, self.gP["lr"], self.gP["rl"], self.gT["lr"], self.gT["rl"],
-                   *[g for v in self.d_out.values() for g in v])
+        self.arena.zero()
         # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
         for key, (a, b) in (("lr", ("l", "r")), ("rl", ("r", "l"))):
             dst = self.pair_in[key]
@@ -509,7 +521,6 @@ class DepthThenCamTrainer(Trainer):
         for s in range(1, 4):
             Ls.area(self.img["l"], self.pyr["l"][s])
             Ls.area(self.img["r"], self.pyr["r"][s])
-            Ls.area(self.label, self.label_pyr[s])
         for s in range(4):
             for d in ("lr", "rl"):
                 Ls.pose_prep(self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
@@ -517,11 +528,14 @@ class DepthThenCamTrainer(Trainer):
         S = self.SLOTS
         _lib.check(lib.tde_cam_loss(B, ptr(self.gt_cam), ptr(self.T["lr"]), ptr(self.T["rl"]), w["cam"],
                                     Ls.dptr(self.acc, S["cam"]), ptr(self.gT["lr"]), ptr(self.gT["rl"]), st), "cam")
+        # smoothness of 1/disp on the 4 maps at every scale (:216-225) and, on the single left net, the depth L1
+        # to the area-downsampled label with replace_nonfinite (:227-232,241-243): one multi-scale launch per map
+        sw = [w["smooth"] / 2 ** s for s in range(4)]
+        for k in ("pl", "pr", "sr"):
+            Ls.pyramid(out[k][:4], self.d_out[k][:4], self.acc, sw, S["smooth"], recip=True)
+        Ls.pyramid(out["sl"][:4], self.d_out["sl"][:4], self.acc, sw, S["smooth"], recip=True, label=self.label,
+                   l1_w=[w["depth"]] * 4, slot_l1=S["depth"], nonfinite=True)
         for s in range(4):
-            for k in ("pl", "pr", "sl", "sr"):     # :216-225
-                Ls.smooth(out[k][s], self.d_out[k][s], w["smooth"] / 2 ** s, self.acc, S["smooth"], recip=True)
-            Ls.l1(out["sl"][s], self.label_pyr[s], self.d_out["sl"][s], w["depth"], self.acc, S["depth"],
-                  nonfinite=True)                 # :241-243
             for tgt, src, run, oth, d in (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl")):
                 Ls.warp_loss(self.acc, S["photo"], self.pyr[src][s], self.pyr[tgt][s], P=self.P[d][s],
                              Kinv=self.Kinv[s], disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s],
@@ -538,7 +552,8 @@ class DepthThenCamTrainer(Trainer):
         # the second accumulates -- no zeroed gradient buffer needed
         for k, prog, first in (("pr", self.pair, True), ("pl", self.pair, False), ("sr", self.single, True),
                                ("sl", self.single, False)):
-            prog.backward(self.runs[k], self.d_out[k], on_grads=self.hook(prog.chunk), grad_accumulate=not first)
+            prog.backward(self.runs[k], [IN_PLACE] * len(self.d_out[k]), on_grads=self.hook(prog.chunk),
+                          grad_accumulate=not first)
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
@@ -558,7 +573,7 @@ class OptflowCombineTrainer(Trainer):
     SLOTS = dict(smooth=0, depth=1, photo=2, optflow=5)
 
     def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
-        from .losses import W_CONFIG3, new, zero
+        from .losses import W_CONFIG3, Arena, new
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG3
         with variables.variable_scope("model"):
@@ -579,9 +594,13 @@ class OptflowCombineTrainer(Trainer):
         self.Kinv = [new((B, 9)) for _ in range(4)]
         self.wmask = [new((B, H >> s, W >> s)) for s in range(4)]
         self.gflow = [(new((B, H >> s, W >> s)), new((B, H >> s, W >> s))) for s in range(4)]
-        self.d_out = [new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
-        self.acc = new((8,), torch.float64)
-        self._zero = zero
+        # loss accumulators + the output gradients (the run's own gradient buffers): one arena, one zeroing
+        ar = Arena()
+        ia = ar.new((8,), torch.float64)
+        ido = [ar.new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
+        t = ar.finalize()
+        self.arena, self.acc, self.d_out = ar, t[ia], [t[i] for i in ido]
+        self.run.bind_output_grads(self.d_out)
 
     def set_batch(self, img_l, img_r, label, K, tgt2src):
         self.img["l"].copy_(img_l)
@@ -600,7 +619,7 @@ class OptflowCombineTrainer(Trainer):
         lib, st = _lib.load(), _lib.stream_ptr()
         B, H, W, w = self.N, self.H, self.W, self.w
         M = B * H * W
-        self._zero(self.acc, *self.d_out)
+        self.arena.zero()
         _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["l"]), 3, 0, ptr(self.pair_in), 6, 0, 0, st), "concat")
         _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["r"]), 3, 0, ptr(self.pair_in), 6, 3, 0, st), "concat")
         out = self.prog.forward(self.run, self.pair_in)
@@ -609,14 +628,17 @@ class OptflowCombineTrainer(Trainer):
             Ls.area(self.img["r"], self.pyr["r"][s])
             Ls.area(self.label, self.label_pyr[s])
         S = self.SLOTS
+        # every scale's smoothness of disp (:143-144) with its depth L1 to the area-downsampled label
+        # (:163-164), and of flow-x / flow-y (:147-150): one multi-scale launch each
+        sw = [w["smooth"] / 2 ** s for s in range(4)]
+        Ls.pyramid(out[:4], self.d_out[:4], self.acc, sw, S["smooth"], label=self.label,
+                   l1_w=[w["depth"] / 2 ** s for s in range(4)], slot_l1=S["depth"])
+        Ls.pyramid(out[4:8], self.d_out[4:8], self.acc, sw, S["smooth"], coff=0)
+        Ls.pyramid(out[4:8], self.d_out[4:8], self.acc, sw, S["smooth"], coff=1)
         for s in range(4):
             disp, flow = out[s], out[4 + s]
             gd, gf = self.d_out[s], self.d_out[4 + s]
             ws = 1.0 / 2 ** s
-            Ls.smooth(disp, gd, w["smooth"] * ws, self.acc, S["smooth"])                  # :143-144
-            Ls.smooth(flow, gf, w["smooth"] * ws, self.acc, S["smooth"], coff=0)          # :147-148
-            Ls.smooth(flow, gf, w["smooth"] * ws, self.acc, S["smooth"], coff=1)          # :149-150
-            Ls.l1(disp, self.label_pyr[s], gd, w["depth"] * ws, self.acc, S["depth"])    # :163-164
             Ls.pose_prep(self.Ks[s], P=self.P[s], Kinv=self.Kinv[s], mat=self.tgt2src)
             h, wd = H >> s, W >> s
             _lib.check(lib.tde_warp_fwd(B, h, wd, 3, ptr(self.label_pyr[s]), 1, ptr(self.P[s]), ptr(self.Kinv[s]),
@@ -629,7 +651,8 @@ class OptflowCombineTrainer(Trainer):
             Ls.l1(flow, self.gflow[s][0], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=0)   # :205-207
             Ls.l1(flow, self.gflow[s][1], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=1)   # :209-210
         # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
-        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
+        self.prog.backward(self.run, [IN_PLACE] * len(self.d_out), on_grads=self.hook(self.prog.chunk),
+                           grad_accumulate=False)
 
     def total_loss(self):
         return float(self.acc.sum().item())
@@ -643,7 +666,7 @@ class RefineTrainer(Trainer):
     SLOTS = dict(smooth=0, depth=1, photo=2)
 
     def __init__(self, batch, H=480, W=640, lr=2e-5, beta1=0.9, weights=None):
-        from .losses import W_CONFIG5, new, zero
+        from .losses import W_CONFIG5, Arena, new
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG5
         with variables.variable_scope("model"):
@@ -659,13 +682,15 @@ class RefineTrainer(Trainer):
         self.pose = new((B, 4, 4))
         self.pyr1 = [self.x1] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]]
         self.pyr2 = [self.x2] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]]
-        self.gt_pyr = [self.gt] + [new(s) for s in _scale_shapes(B, H, W, 1)[1:]]
         self.Ks = [new((B, 9)) for _ in range(4)]
         self.P = [new((B, 12)) for _ in range(4)]
         self.Kinv = [new((B, 9)) for _ in range(4)]
-        self.d_out = [new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
-        self.acc = new((4,), torch.float64)
-        self._zero = zero
+        ar = Arena()
+        ia = ar.new((4,), torch.float64)
+        ido = [ar.new((B, v.H, v.W, v.C)) for v in self.prog.spec.outputs]
+        t = ar.finalize()
+        self.arena, self.acc, self.d_out = ar, t[ia], [t[i] for i in ido]
+        self.run.bind_output_grads(self.d_out)
 
     def set_batch(self, x1, x2, gt_disp, K, pose4):
         self.x1.copy_(x1)
@@ -682,22 +707,24 @@ class RefineTrainer(Trainer):
     def phase_compute(self):
         from . import losses as Ls
         lib, st = _lib.load(), _lib.stream_ptr()
-        self._zero(self.acc, *self.d_out)
+        self.arena.zero()
         out = self.prog.forward(self.run, self.x1)
         for s in range(1, 4):
             Ls.area(self.x1, self.pyr1[s])
             Ls.area(self.x2, self.pyr2[s])
-            Ls.area(self.gt, self.gt_pyr[s])
         S, w = self.SLOTS, self.w
+        # every scale's smoothness (:186-187) and depth L1 to the area-downsampled ground truth (:210-213):
+        # one multi-scale launch
+        Ls.pyramid(out[:4], self.d_out[:4], self.acc, [w["smooth"] / 2 ** s for s in range(4)], S["smooth"],
+                   label=self.gt, l1_w=[w["data"] / 2 ** s for s in range(4)], slot_l1=S["depth"])
         for s in range(4):
             disp, g = out[s], self.d_out[s]
-            Ls.smooth(disp, g, w["smooth"] / 2 ** s, self.acc, S["smooth"])                # :186-187
             Ls.pose_prep(self.Ks[s], P=self.P[s], Kinv=self.Kinv[s], mat=self.pose)
             Ls.warp_loss(self.acc, S["photo"], self.pyr2[s], self.pyr1[s], P=self.P[s], Kinv=self.Kinv[s],
                          disp=disp, photo_w=1.0, g_disp=g)                                  # :200-212
-            Ls.l1(disp, self.gt_pyr[s], g, w["data"] / 2 ** s, self.acc, S["depth"])         # :210-213
         # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
-        self.prog.backward(self.run, self.d_out, on_grads=self.hook(self.prog.chunk), grad_accumulate=False)
+        self.prog.backward(self.run, [IN_PLACE] * len(self.d_out), on_grads=self.hook(self.prog.chunk),
+                           grad_accumulate=False)
 
     def total_loss(self):
         return float(self.acc.sum().item())
