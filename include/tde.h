@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 4
+#define TDE_ABI_VERSION 5
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
@@ -66,6 +66,11 @@ typedef struct {
   const float* x_absmax;
   const float* y_absmax;
   const float* w_absmax;
+  /* Optional pre-split weights: w_split[0] for the forward conv (tde_conv2d_fwd / _fwd_bn / _fwd_bias_act),
+   * w_split[1] for its data gradient (tde_conv2d_bwd_data / tde_conv2d_bwd), each written by
+   * tde_conv2d_split_weights for THESE weights under the current conv math.  NULL: a call that needs a
+   * split makes it itself (one extra launch per call). */
+  const void* w_split[2];
 } tde_conv_desc_t;
 
 int tde_abi_version(void);
@@ -97,6 +102,14 @@ uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
+/* Weight pre-split (the halo-tiled stride-1 path keeps the layer's weights as split fp16 / bf16 tiles):
+ * bytes of the split image op (0 forward, 1 data gradient) of layer d needs under the current conv math;
+ * 0 = that call takes no split weights (then leave d->w_split[op] NULL).  tde_conv2d_split_weights writes
+ * n such images (outs[i], 256-byte aligned, >= the size) in ONE launch -- e.g. every layer of a network
+ * once per step, then each conv call skips its own split launch. */
+size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op);
+int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const int* ops,
+                             const float* const* weights, void* const* outs, void* stream);
 int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y,
                    int accumulate, void* ws, size_t ws_bytes, void* stream);
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx,
@@ -246,6 +259,26 @@ int tde_resize_bilinear_bwd(int N, int H, int W, int C, float* dx, int dx_cstrid
                             int dy_coff, void* stream);
 int tde_resize_area_fwd(int N, int H, int W, int C, const float* x, int OH, int OW, float* y,
                         void* stream);
+
+/* ---------------------------------------------------------------- input pipeline (device half)
+ * imageselect_Dataloader_optflow.py:104-133,216-233 (read_images_from_disk + unpack_image_sequence):
+ * to_float(tf.image.resize_images(decode_jpeg(file), [out_h, out_w * nframes])) -- BILINEAR,
+ * align_corners=False, TF-1 legacy coordinates -- cut into nframes frames of [out_h, out_w] (frame 0 =
+ * tgt_image, 1 = src_image_1), each written into an NHWC float view (3 channels at out_coff[f] of
+ * out_cstride[f]).  Input: the batch's decoded uint8 HWC RGB images packed in device memory, image b at byte
+ * src_off[b] with size src_hw[2b] x src_hw[2b+1] (both arrays in device memory).  Results are bit-identical
+ * to the float32 restatement (no FMA contraction). */
+#define TDE_MAX_FRAMES 4
+typedef struct {
+  int B, out_h, out_w, nframes;
+  const unsigned char* src;
+  const long long* src_off;
+  const int* src_hw;
+  float* out[TDE_MAX_FRAMES];
+  int out_cstride[TDE_MAX_FRAMES];
+  int out_coff[TDE_MAX_FRAMES];
+} tde_image_batch_t;
+int tde_image_resize_unpack(const tde_image_batch_t* args, void* stream);
 
 /* ---------------------------------------------------------------- loss head
  * Fused forward+backward of the scalar loss terms: each call ADDS weight*term to loss[0] (a

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
@@ -26,7 +26,7 @@ class ConvDesc(ctypes.Structure):
     """Mirror of tde_conv_desc_t (include/tde.h)."""
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "OH", "OW", "K", "KH", "KW", "stride", "pad_top",
                                      "pad_left", "w_cin", "x_cstride", "x_coff", "y_cstride", "y_coff")] + \
-               [("x_absmax", c_void_p), ("y_absmax", c_void_p), ("w_absmax", c_void_p)]
+               [("x_absmax", c_void_p), ("y_absmax", c_void_p), ("w_absmax", c_void_p), ("w_split", c_void_p * 2)]
 
 
 P = c_void_p
@@ -60,7 +60,17 @@ class DepthLoss(ctypes.Structure):
                 ("l1_w", c_float * 4), ("loss_smooth", P), ("loss_l1", P), ("grad_accumulate", c_int)]
 
 
+class ImageBatch(ctypes.Structure):
+    """Mirror of tde_image_batch_t (include/tde.h): the input pipeline's resize + unpack launch."""
+    _fields_ = [("B", c_int), ("out_h", c_int), ("out_w", c_int), ("nframes", c_int),
+                ("src", P), ("src_off", P), ("src_hw", P),
+                ("out", P * 4), ("out_cstride", c_int * 4), ("out_coff", c_int * 4)]
+
+
 _SIGS = {
+    "tde_conv2d_split_weights_size": (c_size_t, [P, c_int]),
+    "tde_conv2d_split_weights": (c_int, [c_int, P, P, P, P, P]),
+    "tde_image_resize_unpack": (c_int, [P, P]),
     "tde_loss_depth_pyramid": (c_int, [P, P]),
     "tde_warp_loss": (c_int, [P, P]),
     "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),

@@ -19,6 +19,8 @@
 // Split-K partials go to a caller workspace and are reduced by a second kernel (deterministic; no
 // float atomics).
 #include "tde_common.h"
+
+#include <vector>
 #include "bn_internal.h"
 #include "split_math.h"
 #include "halo_conv.h"
@@ -1567,6 +1569,25 @@ int tde_set_conv_math(int mode) {
 }
 
 int tde_get_conv_math(void) { return g_conv_math; }
+
+size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op) {
+  HaloPlan hp;
+  if (!desc_ok(d) || (op != 0 && op != 1) || !halo_plan(*d, op, g_conv_math, hp)) return 0;
+  return hp.wbytes;
+}
+
+int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const int* ops, const float* const* weights,
+                             void* const* outs, void* stream) {
+  TDE_CHECK_ARG(n >= 0 && (n == 0 || (descs && ops && weights && outs)));
+  std::vector<HaloPlan> hps(n);
+  for (int i = 0; i < n; ++i) {
+    TDE_CHECK_ARG(desc_ok(descs[i]) && (ops[i] == 0 || ops[i] == 1) && weights[i] && outs[i] && tde_aligned16(outs[i]));
+    // a layer / op that takes no split (tde_conv2d_split_weights_size == 0) is the caller's error
+    TDE_CHECK_ARG(halo_plan(*descs[i], ops[i], g_conv_math, hps[i]));
+  }
+  if (n > 0) halo_wprep_batch(n, hps.data(), descs, weights, outs, static_cast<hipStream_t>(stream));
+  return tde_launch_status();
+}
 
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op) {
   // op 3 = forward + batch norm + ReLU (tde_conv2d_fwd_bn)

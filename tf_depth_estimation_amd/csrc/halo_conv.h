@@ -27,12 +27,16 @@ struct HaloPlan {
 // call should take the implicit-GEMM path.
 bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp);
 
-// Weight split (one launch) + conv (one launch).  ws: >= hp.wbytes of 16-byte aligned workspace;
+// Weight split (one launch; skipped when d.w_split[hp.mode] holds the pre-split weights) + conv (one launch).  ws: >= hp.wbytes of 16-byte aligned workspace;
 // bnp: fp64 BN partials [hp.nparts][2][Ncols] or null.  bias / relu: folded-BN inference epilogue
 // (out = relu?(conv + bias[col]); accumulate 0), null / 0 for a plain conv.
 void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
                  int accumulate, void* ws, double* bnp, hipStream_t st, const float* bias = nullptr,
                  int relu = 0);
+
+// The weight splits of n (plan, layer) pairs in one launch (tde_conv2d_split_weights): outs[i] >= hps[i].wbytes.
+void halo_wprep_batch(int n, const HaloPlan* hps, const tde_conv_desc_t* const* ds, const float* const* ws,
+                      void* const* outs, hipStream_t st);
 
 // Halo-tiled filter gradient (halo_wgrad.hip) of a stride-1 conv with K <= 32 output channels at high
 // resolution: partial dW per (pixel chunk, kernel row) in fp32 MFMA, then a fixed-order chunk reduce.

@@ -60,12 +60,26 @@ struct HaloArgs {
 //   DGRAD: B[(tap, k)][col] = w[ntap - 1 - tap][col][k]          (col = dx channel < wcin, k < K)
 // The tile is copied byte-for-byte into its LDS ring slot by LDS-DMA, so this IS the LDS image.
 //   planes 3: bf16x6 hi / mid / lo (split3); planes 2: fp16x3 hi / lo of w * f16x3_scale(wmax) (split4x2h)
-__global__ void __launch_bounds__(256) halo_wprep_kernel(const float* __restrict__ w, u16* __restrict__ wp, int mode,
-                                                         long total, int steps, int CC, int ntap, int Cred,
-                                                         int Ncols, int NCP, int ncolt, int wcin, int K, int planes,
-                                                         const float* wmax) {
-  const float ws = planes == 2 ? f16x3_scale(wmax, F16X3_WSCALE) : 1.f;
-  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+struct WprepJob {
+  const float* w;
+  u16* wp;
+  const float* wmax;
+  long total;
+  int block0, nblocks;    // the job's blocks in a batched launch
+  int mode, steps, CC, ntap, Cred, Ncols, NCP, ncolt, wcin, K, planes;
+};
+constexpr int WPREP_MAXJ = 16;
+struct WprepBatch {
+  int njobs;
+  WprepJob j[WPREP_MAXJ];
+};
+
+__device__ __forceinline__ void wprep_elem(const WprepJob& J, float ws, long idx) {
+  const float* __restrict__ w = J.w;
+  u16* __restrict__ wp = J.wp;
+  const int mode = J.mode, steps = J.steps, CC = J.CC, ntap = J.ntap, Cred = J.Cred, Ncols = J.Ncols;
+  const int NCP = J.NCP, ncolt = J.ncolt, wcin = J.wcin, K = J.K, planes = J.planes;
+  {
     const int rl = (int)(idx % LDB);
     long t = idx / LDB;
     const int cl = (int)(t % NCP);
@@ -94,6 +108,22 @@ __global__ void __launch_bounds__(256) halo_wprep_kernel(const float* __restrict
       wp[base + 2l * NCP * LDB] = (u16)(l >> 16);
     }
   }
+}
+
+__global__ void __launch_bounds__(256) halo_wprep_kernel(const WprepJob J) {
+  const float ws = J.planes == 2 ? f16x3_scale(J.wmax, F16X3_WSCALE) : 1.f;
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < J.total; idx += (long)gridDim.x * 256)
+    wprep_elem(J, ws, idx);
+}
+
+// Several layers' splits in one launch (tde_conv2d_split_weights): a block works on ONE job (block ranges).
+__global__ void __launch_bounds__(256) halo_wprep_batch_kernel(const WprepBatch B) {
+  int k = 0;
+  while (k + 1 < B.njobs && (int)blockIdx.x >= B.j[k + 1].block0) ++k;
+  const WprepJob& J = B.j[k];
+  const float ws = J.planes == 2 ? f16x3_scale(J.wmax, F16X3_WSCALE) : 1.f;
+  for (long idx = (long)(blockIdx.x - J.block0) * 256 + threadIdx.x; idx < J.total; idx += (long)J.nblocks * 256)
+    wprep_elem(J, ws, idx);
 }
 
 // Workgroup barrier that waits only for this wave's LDS operations.  __syncthreads() is a release/acquire
@@ -480,14 +510,41 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
   return true;
 }
 
+static WprepJob wprep_job(const HaloPlan& hp, const tde_conv_desc_t& d, const float* w, void* out) {
+  WprepJob J{};
+  J.w = w; J.wp = static_cast<u16*>(out); J.wmax = d.w_absmax;
+  J.total = (long)hp.nch * hp.steps * hp.NcolsP * LDB;
+  long blocks = (J.total + 255) / 256;
+  J.nblocks = (int)(blocks > 2048 ? 2048 : blocks);
+  J.mode = hp.mode; J.steps = hp.steps; J.CC = hp.CC; J.ntap = hp.ntap; J.Cred = hp.Cred; J.Ncols = hp.Ncols;
+  J.NCP = 16 * hp.TN; J.ncolt = hp.ncolt; J.wcin = d.w_cin; J.K = d.K; J.planes = hp.planes;
+  return J;
+}
+
+void halo_wprep_batch(int n, const HaloPlan* hps, const tde_conv_desc_t* const* ds, const float* const* ws,
+                      void* const* outs, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += WPREP_MAXJ) {
+    WprepBatch B{};
+    int blocks = 0;
+    for (int i = i0; i < n && B.njobs < WPREP_MAXJ; ++i) {
+      WprepJob J = wprep_job(hps[i], *ds[i], ws[i], outs[i]);
+      J.block0 = blocks;
+      blocks += J.nblocks;
+      B.j[B.njobs++] = J;
+    }
+    hipLaunchKernelGGL(halo_wprep_batch_kernel, dim3(blocks), dim3(256), 0, st, B);
+  }
+}
+
 void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, const float* w, float* out,
                  int accumulate, void* ws, double* bnp, hipStream_t st, const float* bias, int relu) {
-  u16* wp = static_cast<u16*>(ws);
-  const long total = (long)hp.nch * hp.steps * hp.NcolsP * LDB;
-  long blocks = (total + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(halo_wprep_kernel, dim3((int)blocks), dim3(256), 0, st, w, wp, hp.mode, total, hp.steps, hp.CC,
-                     hp.ntap, hp.Cred, hp.Ncols, 16 * hp.TN, hp.ncolt, d.w_cin, d.K, hp.planes, d.w_absmax);
+  // weights split beforehand (tde_conv2d_split_weights, d.w_split[mode]) or here, into the workspace
+  const u16* wp = static_cast<const u16*>(d.w_split[hp.mode]);
+  if (wp == nullptr) {
+    const WprepJob J = wprep_job(hp, d, w, ws);
+    hipLaunchKernelGGL(halo_wprep_kernel, dim3(J.nblocks), dim3(256), 0, st, J);
+    wp = static_cast<const u16*>(ws);
+  }
   HaloArgs a{};
   a.N = d.N; a.H = d.H; a.W = d.W;
   a.HWd = hp.HWd; a.HP = hp.HP; a.CC = hp.CC; a.nch = hp.nch; a.SA = hp.SA; a.steps = hp.steps; a.ntap = hp.ntap;

@@ -90,6 +90,67 @@ __global__ void __launch_bounds__(256) bilinear_fwd_kernel(int N, int H, int W, 
   }
 }
 
+// Exact x2 upsample (the disparity heads, nets_optflow_depth.py:124,131,138) with 32-bit indices: one thread
+// per output pixel, the source offsets from shifts (in = o * 0.5: lower = o >> 1, lerp 0 or 0.5) -- the same
+// float expressions as bilinear_fwd_kernel, so the same values.
+__global__ void __launch_bounds__(256) bilinear_up2_fwd_kernel(int N, int H, int W, int C, const float* x, int xcs,
+                                                               int xco, float* y, int ycs, int yco) {
+  const int OH = 2 * H, OW = 2 * W;
+  const int total = N * OH * OW;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < total; p += gridDim.x * 256) {
+    const int ow = p % OW, t = p / OW;
+    const int oh = t % OH, n = t / OH;
+    const int y0 = oh >> 1, x0 = ow >> 1;
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const float ly = (oh & 1) ? 0.5f : 0.f, lx = (ow & 1) ? 0.5f : 0.f;
+    const float* b = x + n * H * W * xcs + xco;
+    for (int c = 0; c < C; ++c) {
+      const float tl = b[(y0 * W + x0) * xcs + c], tr = b[(y0 * W + x1) * xcs + c];
+      const float bl = b[(y1 * W + x0) * xcs + c], br = b[(y1 * W + x1) * xcs + c];
+      const float top = tl + (tr - tl) * lx;
+      const float bot = bl + (br - bl) * lx;
+      y[p * ycs + yco + c] = top + (bot - top) * ly;
+    }
+  }
+}
+
+// Its gradient: an input row i receives from output rows 2i-1 (weight 0.5), 2i (1) and 2i+1 (0.5, plus the
+// clamped upper tap 0.5 on the last row); columns alike.  Summed in the generic kernel's order (ascending
+// output row, then column, zero weights skipped) with the same weight products: the same values.
+__global__ void __launch_bounds__(256) bilinear_up2_bwd_kernel(int N, int H, int W, int C, float* dx, int dxcs,
+                                                               int dxco, int acc, const float* dy, int dycs,
+                                                               int dyco) {
+  const int OH = 2 * H, OW = 2 * W;
+  const int total = N * H * W;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < total; p += gridDim.x * 256) {
+    const int iw = p % W, t = p / W;
+    const int ih = t % H, n = t / H;
+    float wys[3], wxs[3];
+    wys[0] = ih > 0 ? 0.5f : 0.f;
+    wys[1] = 1.f;
+    wys[2] = ih == H - 1 ? 1.f : 0.5f;     // row 2i+1: lower tap 0.5, and on the last row its clamped upper too
+    wxs[0] = iw > 0 ? 0.5f : 0.f;
+    wxs[1] = 1.f;
+    wxs[2] = iw == W - 1 ? 1.f : 0.5f;
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (wys[a] == 0.f) continue;
+        const int oh = 2 * ih - 1 + a;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          if (wxs[b] == 0.f) continue;
+          const int ow = 2 * iw - 1 + b;
+          s += dy[((n * OH + oh) * OW + ow) * dycs + dyco + c] * (wys[a] * wxs[b]);
+        }
+      }
+      float* d = dx + p * dxcs + dxco + c;
+      *d = acc ? *d + s : s;
+    }
+  }
+}
+
 // ResizeBilinearGrad as a gather: dx[i] = sum over outputs o of dy[o] * weight(o -> i).
 __global__ void __launch_bounds__(256) bilinear_bwd_kernel(int N, int H, int W, int C, float* dx, int dxcs,
                                                            int dxco, int acc, int OH, int OW, const float* dy,
@@ -174,6 +235,11 @@ int tde_resize_nearest_bwd(int N, int H, int W, int C, float* dx, int dx_cstride
 int tde_resize_bilinear_fwd(int N, int H, int W, int C, const float* x, int x_cstride, int x_coff, int OH, int OW,
                             float* y, int y_cstride, int y_coff, void* stream) {
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && x && y);
+  if (OH == 2 * H && OW == 2 * W && (long)N * OH * OW * (y_cstride > x_cstride ? y_cstride : x_cstride) < (1L << 31)) {
+    hipLaunchKernelGGL(bilinear_up2_fwd_kernel, dim3(ew_grid((long)N * OH * OW)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), N, H, W, C, x, x_cstride, x_coff, y, y_cstride, y_coff);
+    return tde_launch_status();
+  }
   hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(ew_grid((long)N * OH * OW * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, H, W, C, x, x_cstride, x_coff, OH, OW, y, y_cstride, y_coff);
   return tde_launch_status();
@@ -182,6 +248,12 @@ int tde_resize_bilinear_fwd(int N, int H, int W, int C, const float* x, int x_cs
 int tde_resize_bilinear_bwd(int N, int H, int W, int C, float* dx, int dx_cstride, int dx_coff, int accumulate, int OH,
                             int OW, const float* dy, int dy_cstride, int dy_coff, void* stream) {
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && dx && dy);
+  if (OH == 2 * H && OW == 2 * W && (long)N * OH * OW * (dy_cstride > dx_cstride ? dy_cstride : dx_cstride) < (1L << 31)) {
+    hipLaunchKernelGGL(bilinear_up2_bwd_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), N, H, W, C, dx, dx_cstride, dx_coff, accumulate, dy,
+                       dy_cstride, dy_coff);
+    return tde_launch_status();
+  }
   hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(ew_grid((long)N * H * W * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, H, W, C, dx, dx_cstride, dx_coff, accumulate, OH, OW, dy,
                      dy_cstride, dy_coff);

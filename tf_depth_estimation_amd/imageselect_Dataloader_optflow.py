@@ -1,0 +1,335 @@
+"""Input pipeline of the training scripts: `imageselect_Dataloader_optflow.DataLoader`,
+the loader of train_depth_only.py:77-84 (config 2) and train_optflow_combine.py (config 3).
+
+Same constructor, file layout and outputs as the reference (imageselect_Dataloader_optflow.py:8-262):
+
+  loader = DataLoader(dataset_dir, batch_size, image_height, image_width, num_source, num_scales, 'train')
+  tgt_image, src_image_stack, label, intrinsics, tgt2src_projs, m_scale = loader.load_train_batch()
+
+except that each load_train_batch() call returns the NEXT batch as device tensors (the reference returns
+graph tensors that yield a new batch per sess.run):
+  tgt_image, src_image_stack  [B, resizedheight, resizedwidth, 3] float32 (0..255: the /255 is commented out
+                              in the reference, :129)
+  label                       [B, image_height, image_width, 1] float32 (raw *_z.bin)
+  intrinsics                  [B, num_scales, 3, 3] (get_multi_scale_intrinsics, :248-262)
+  tgt2src_projs, m_scale      [B, 2, 4, 4], [B] (*_tgt2src_proj.txt, :168-181)
+
+Pipeline (MI355X-first): a producer thread keeps `prefetch` batches in flight.  A thread pool decodes the
+JPEGs (PIL / libjpeg, the GIL is released while decoding) straight into a pinned staging buffer together
+with the raw labels; one async H2D copy per batch on a copy stream; then ONE launch of
+tde_image_resize_unpack (csrc/image_io.hip) resizes every image of the batch to [resizedheight,
+2 * resizedwidth] with TF-1's bilinear resize_images and cuts it into tgt / src frames.  The consumer's
+stream waits on the batch's event; a batch's device buffers are reused only after the consumer's stream
+has passed the point where it asked for the next batch (release event), so nothing is overwritten while
+a step still reads it.  Epochs: a fresh permutation per epoch (slice_input_producer(shuffle=True,
+num_epochs)), batches run across epoch boundaries, the last partial batch is dropped (tf.train.batch);
+StopIteration when the epochs are exhausted (TF's OutOfRangeError).
+"""
+import os
+import queue
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ImageBatch, ptr
+
+
+def _hdr_bytes(B):
+    """Staging header: per-image byte offsets int64[B], then sizes int32[2B], padded to 256 bytes."""
+    return (16 * B + 255) // 256 * 256
+
+
+def _csv_record(text, n, delim):
+    """tf.decode_csv of one record of n float fields with record_defaults [[1.]] * n (empty field -> 1.0);
+    the record is the file's content without its line terminator."""
+    fields = text.rstrip("\r\n").split(delim)
+    if len(fields) != n:
+        raise ValueError(f"expected {n} '{delim}'-separated fields, got {len(fields)}")
+    return np.array([float(v) if v.strip() else 1.0 for v in fields], dtype=np.float32)
+
+
+class _Slot:
+    """One batch in flight: pinned staging + device buffers + events."""
+
+    def __init__(self, B, img_bytes, ih, iw, rh, rw, ns):
+        self.B, self.cap, self.hdr, self.stride = B, img_bytes, _hdr_bytes(B), 0
+        self.stage = torch.empty(self.hdr + img_bytes, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(self.hdr + img_bytes, dtype=torch.uint8, device="cuda")
+        self.label_h = torch.empty((B, ih, iw, 1), dtype=torch.float32, pin_memory=True)
+        self.small_h = torch.empty(B * (ns * 9 + 32 + 1), dtype=torch.float32, pin_memory=True)
+        self.tgt = torch.empty((B, rh, rw, 3), dtype=torch.float32, device="cuda")
+        self.src = torch.empty((B, rh, rw, 3), dtype=torch.float32, device="cuda")
+        self.label = torch.empty((B, ih, iw, 1), dtype=torch.float32, device="cuda")
+        self.small = torch.empty(B * (ns * 9 + 32 + 1), dtype=torch.float32, device="cuda")
+        n1, n2 = B * ns * 9, B * 32
+        self.intr = self.small[:n1].view(B, ns, 3, 3)
+        self.projs = self.small[n1:n1 + n2].view(B, 2, 4, 4)
+        self.m_scale = self.small[n1 + n2:]
+        self.ready = None      # event: batch resident on the device
+        self.release = None    # event on the consumer's stream: device buffers free again
+
+    def grow(self, img_bytes):
+        if img_bytes > self.cap:
+            self.cap = img_bytes
+            self.stage = torch.empty(self.hdr + img_bytes, dtype=torch.uint8, pin_memory=True)
+            self.dev = torch.empty(self.hdr + img_bytes, dtype=torch.uint8, device="cuda")
+
+
+class DataLoader(object):
+    def __init__(self, dataset_dir, batch_size, image_height, image_width, num_source, num_scales, split,
+                 resizedheight=240, resizedwidth=720, shuffle=True, num_epochs=1500, seed=None, workers=8,
+                 prefetch=2):
+        self.dataset_dir = dataset_dir
+        self.batch_size = batch_size
+        self.image_height = image_height
+        self.image_width = image_width
+        self.split = split
+        self.num_source = num_source
+        self.num_scales = num_scales
+        self.resizedheight = resizedheight      # imageselect_Dataloader_optflow.py:24-25
+        self.resizedwidth = resizedwidth
+        self.shuffle, self.num_epochs = shuffle, num_epochs
+        self._rng = np.random.default_rng(seed)
+        self._workers, self._prefetch = max(1, int(workers)), max(1, int(prefetch))
+        self._started = False
+        self._held = None
+        self.last_indices = None
+        self._lib = _lib.load()
+
+    # ------------------------------------------------------------------ reference API
+    def read_labeled_image_list(self):
+        """imageselect_Dataloader_optflow.py:66-101 (same paths, same frame-id parsing)."""
+        with open(self.dataset_dir + "/%s.txt" % self.split, "r") as f:
+            frames = f.readlines()
+        subfolders = [x.split(" ")[0] for x in frames]
+        frame_ids = [x.split(" ")[1] + "_" + x.split(" ")[2][:-1] for x in frames]
+        j = os.path.join
+        n = len(frames)
+        return {
+            "image_file_list": [j(self.dataset_dir, subfolders[i], frame_ids[i] + ".jpg") for i in range(n)],
+            "cam_file_list": [j(self.dataset_dir, subfolders[i], frame_ids[i] + "_cam.txt") for i in range(n)],
+            "gt_depth_file_list": [j(self.dataset_dir, subfolders[i], "frame" + frame_ids[i] + ".jpg" + "_z.bin")
+                                   for i in range(n)],
+            "tgt2src_proj_list": [j(self.dataset_dir, subfolders[i], frame_ids[i] + "_tgt2src_proj.txt")
+                                  for i in range(n)],
+        }
+
+    def load_train_batch(self):
+        """The next batch: (tgt_image, src_image_stack, label_batch, intrinsics, tgt2src_projs, m_scale) on the
+        current device stream (imageselect_Dataloader_optflow.py:28-63)."""
+        if not self._started:
+            self._start()
+        cur = torch.cuda.current_stream()
+        if self._held is not None:       # the previous batch's buffers are free once cur passes this point
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._held.release = ev
+            self._free.put(self._held)
+            self._held = None
+        item = self._q.get()
+        if isinstance(item, BaseException):
+            self._q.put(item)
+            raise item
+        cur.wait_event(item.ready)
+        self._held = item
+        self.last_indices = list(item.indices)     # sample indices (file-list order) of the batch returned
+        return item.tgt, item.src, item.label, item.intr, item.projs, item.m_scale
+
+    def make_intrinsics_matrix(self, fx, fy, cx, cy):
+        """:236-246 ([B] float32 arrays -> [B,3,3])."""
+        B = fx.shape[0]
+        z = np.zeros(B, np.float32)
+        r3 = np.tile(np.array([[0.0, 0.0, 1.0]], np.float32), (B, 1))
+        return np.stack([np.stack([fx, z, cx], 1), np.stack([z, fy, cy], 1), r3], axis=1).astype(np.float32)
+
+    def get_multi_scale_intrinsics(self, intrinsics, num_scales, x_resize_ratio, y_resize_ratio):
+        """:248-262 in float32: f / 2**s * ratio, c / 2**s * ratio -> [B, num_scales, 3, 3]."""
+        f = np.float32
+        out = []
+        for s in range(num_scales):
+            d = f(2 ** s)
+            fx = ((intrinsics[:, 0, 0] / d).astype(f) * f(x_resize_ratio)).astype(f)
+            fy = ((intrinsics[:, 1, 1] / d).astype(f) * f(y_resize_ratio)).astype(f)
+            cx = ((intrinsics[:, 0, 2] / d).astype(f) * f(x_resize_ratio)).astype(f)
+            cy = ((intrinsics[:, 1, 2] / d).astype(f) * f(y_resize_ratio)).astype(f)
+            out.append(self.make_intrinsics_matrix(fx, fy, cx, cy))
+        return np.stack(out, axis=1)
+
+    def close(self):
+        if self._started:
+            import time
+            self._stop.set()
+            t0 = time.monotonic()
+            while self._thread.is_alive() and time.monotonic() - t0 < 30:
+                while True:      # unblock a producer waiting to queue a batch or for a free slot
+                    try:
+                        self._q.get_nowait()
+                    except queue.Empty:
+                        break
+                for sl in self._slots:
+                    self._free.put(sl)
+                self._thread.join(timeout=0.05)
+            self._pool.shutdown(wait=True)
+            self._started = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ pipeline
+    def _order(self):
+        n = len(self._files["image_file_list"])
+        for _ in range(self.num_epochs):
+            yield from (self._rng.permutation(n) if self.shuffle else np.arange(n))
+
+    def _start(self):
+        self._files = self.read_labeled_image_list()
+        if len(self._files["image_file_list"]) == 0:
+            raise ValueError(f"{self.dataset_dir}/{self.split}.txt lists no samples")
+        B = self.batch_size
+        first = self._decode(self._files["image_file_list"][0])
+        stride = (first.nbytes + 15) // 16 * 16          # staging bytes per image (a slot grows if it must)
+        # slots: `prefetch` batches decoding + `prefetch` queued + the consumer's + one being released
+        nslots = 2 * self._prefetch + 2
+        self._slots = [_Slot(B, B * stride, self.image_height, self.image_width, self.resizedheight,
+                             self.resizedwidth, self.num_scales) for _ in range(nslots)]
+        for sl in self._slots:
+            sl.stride = stride
+        self._free = queue.Queue()
+        for sl in self._slots:
+            self._free.put(sl)
+        self._q = queue.Queue(maxsize=self._prefetch)
+        self._stop = threading.Event()
+        self._pool = ThreadPoolExecutor(self._workers)
+        self._copy = torch.cuda.Stream()
+        self._dev = torch.cuda.current_device()
+        self._thread = threading.Thread(target=self._produce, daemon=True)
+        self._started = True
+        self._thread.start()
+
+    @staticmethod
+    def _decode(path):
+        from PIL import Image      # host JPEG decoder (libjpeg); decode_jpeg, imageselect_Dataloader_optflow.py:124
+        with Image.open(path) as im:
+            if im.mode != "RGB":
+                im = im.convert("RGB")       # decode_jpeg(channels=3) of a grey / CMYK file
+            return np.asarray(im, dtype=np.uint8)
+
+    def _produce(self):
+        """Producer thread: up to `prefetch` batches decode at once in the pool (one task per sample: JPEG
+        decode into the slot's pinned staging, raw label, cam / proj files); the oldest is finished
+        (header, intrinsics, H2D, resize launch) and queued in order."""
+        import collections
+        try:
+            torch.cuda.set_device(self._dev)
+            order = self._order()
+            B = self.batch_size
+            pending = collections.deque()
+            while not self._stop.is_set():
+                idx = []
+                for i in order:
+                    idx.append(int(i))
+                    if len(idx) == B:
+                        break
+                if len(idx) < B:          # epochs exhausted (the last partial batch is dropped)
+                    while pending and not self._stop.is_set():
+                        self._finish(*pending.popleft())
+                    self._q.put(StopIteration("DataLoader: num_epochs exhausted"))
+                    return
+                while True:               # a free slot; finish pending batches rather than wait on the consumer
+                    try:
+                        slot = self._free.get_nowait()
+                        break
+                    except queue.Empty:
+                        if pending:
+                            self._finish(*pending.popleft())
+                        else:
+                            slot = self._free.get()
+                            break
+                if self._stop.is_set():
+                    return
+                if slot.ready is not None:
+                    slot.ready.synchronize()      # the previous H2D out of this slot's staging has finished
+                slot.indices = idx
+                futs = [self._pool.submit(self._sample, slot, b, i) for b, i in enumerate(idx)]
+                pending.append((slot, futs))
+                if len(pending) >= self._prefetch:
+                    self._finish(*pending.popleft())
+        except BaseException as e:       # surfaced by load_train_batch
+            self._q.put(e)
+
+    def _sample(self, slot, b, i):
+        """One sample into slot row b: image bytes at hdr + b * stride (None back if it does not fit), label,
+        intrinsics and projections (imageselect_Dataloader_optflow.py:104-183)."""
+        f = self._files
+        img = self._decode(f["image_file_list"][i])
+        fits = img.nbytes <= slot.stride
+        if fits:
+            st = slot.stage.numpy()
+            o = slot.hdr + b * slot.stride
+            st[o:o + img.nbytes] = img.reshape(-1)
+        H, W = self.image_height, self.image_width
+        v = np.fromfile(f["gt_depth_file_list"][i], dtype="<f4")
+        if v.size != H * W:
+            raise ValueError(f"{f['gt_depth_file_list'][i]}: {v.size} floats, expected {H}x{W}")
+        slot.label_h.numpy()[b] = v.reshape(H, W, 1)
+        with open(f["cam_file_list"][i]) as fh:
+            cam = _csv_record(fh.read(), 9, ",").reshape(3, 3)
+        with open(f["tgt2src_proj_list"][i]) as fh:
+            pv = _csv_record(fh.read(), 34, " ")[:-1]       # :176-180
+        return img.shape[0], img.shape[1], cam, pv[:-1].reshape(2, 4, 4), pv[-1], (None if fits else img)
+
+    def _finish(self, slot, futs):
+        B = self.batch_size
+        res = [fu.result() for fu in futs]
+        if any(r[5] is not None for r in res):      # an image larger than the slot's stride: grow, re-stage
+            stride = max((r[0] * r[1] * 3 + 15) // 16 * 16 for r in res)
+            old = slot.stage.numpy().copy()
+            slot.grow(B * stride)
+            st = slot.stage.numpy()
+            for b, r in enumerate(res):
+                n = r[0] * r[1] * 3
+                src = r[5].reshape(-1) if r[5] is not None else old[slot.hdr + b * slot.stride:][:n]
+                st[slot.hdr + b * stride:slot.hdr + b * stride + n] = src
+            slot.stride = stride
+        st = slot.stage.numpy()
+        offs = slot.hdr + np.arange(B, dtype=np.int64) * slot.stride
+        st[:8 * B] = offs.view(np.uint8)
+        st[8 * B:16 * B] = np.array([[r[0], r[1]] for r in res], np.int32).reshape(-1).view(np.uint8)
+        xr = np.float32(np.float32(self.resizedwidth) / np.float32(self.image_width))      # :59-60
+        yr = np.float32(np.float32(self.resizedheight) / np.float32(self.image_height))
+        intr = self.get_multi_scale_intrinsics(np.stack([r[2] for r in res]), self.num_scales, xr, yr)
+        sm = slot.small_h.numpy()
+        n1, n2 = intr.size, B * 32
+        sm[:n1] = intr.reshape(-1)
+        sm[n1:n1 + n2] = np.stack([r[3] for r in res]).reshape(-1)
+        sm[n1 + n2:] = np.array([r[4] for r in res], np.float32)
+        end = int(slot.hdr + B * slot.stride)
+        with torch.cuda.stream(self._copy):
+            if slot.release is not None:
+                self._copy.wait_event(slot.release)      # the consumer is done with this slot's device buffers
+            slot.dev[:end].copy_(slot.stage[:end], non_blocking=True)
+            slot.label.copy_(slot.label_h, non_blocking=True)
+            slot.small.copy_(slot.small_h, non_blocking=True)
+            a = ImageBatch()
+            a.B, a.out_h, a.out_w, a.nframes = B, self.resizedheight, self.resizedwidth, 2
+            base = slot.dev.data_ptr()
+            a.src, a.src_off, a.src_hw = base, base, base + 8 * B
+            a.out[0], a.out[1] = slot.tgt.data_ptr(), slot.src.data_ptr()
+            a.out_cstride[0] = a.out_cstride[1] = 3
+            a.out_coff[0] = a.out_coff[1] = 0
+            _lib.check(self._lib.tde_image_resize_unpack(ctypes_ref(a), _lib.stream_ptr()), "image resize")
+            ev = torch.cuda.Event()
+            ev.record(self._copy)
+        slot.ready = ev
+        self._q.put(slot)
+
+
+def ctypes_ref(x):
+    import ctypes
+    return ctypes.byref(x)
