@@ -352,3 +352,52 @@ def test_wgrad_overlap_matches_serial(cfg, graph):
             assert torch.equal(ga, gb) and torch.equal(pa, pb), "serial config-4 step not deterministic"
     for (pa, ga, _), (pb, gb, _) in zip(ref, run("overlap")):
         assert torch.equal(ga, gb) and torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+@pytest.mark.parametrize("cfg", ["config2", "config4"])
+def test_deferred_adam_matches_plain(cfg, graph):
+    """Trainer.enable_deferred_adam: each step's Adam runs at the start of the next step on a side stream,
+    overlapped with that forward (per-bucket waits, the weight splits issued once their bucket is final).
+    After flush() the parameters and Adam moments equal the plain trainer's bit for bit (config 4 with the
+    consistency weight 0: its float-atomic scatter is the only non-deterministic term, see above); the loss
+    of every step matches too (the forward sees the same parameters; up to the fp64 atomics' summation order)."""
+    from tf_depth_estimation_amd import _api, train, variables
+    steps = 3
+
+    def run(deferred):
+        variables.get_store().reset(seed=1)
+        _api.clear_programs()
+        B, H, W = 2, 64, 96
+        if cfg == "config2":
+            tr = train.DepthOnlyTrainer(B, H, W)
+            g = np.random.default_rng(9)
+            tr.set_batch(torch.tensor(g.uniform(-0.5, 0.5, (B, H, W, 3)), dtype=torch.float32).cuda(),
+                         torch.tensor(g.uniform(0.25, 4.0, (B, H, W, 1)), dtype=torch.float32).cuda())
+        else:
+            tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+            lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
+            tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
+                         torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
+                         small_pose(B, 4).cuda())
+        tr.enable_wgrad_overlap()
+        if deferred:
+            tr.enable_deferred_adam(first_mb=0.25)
+        losses = []
+        if graph:
+            tr.capture(warmup=1)
+            losses.append(tr.total_loss())
+        for _ in range(steps):
+            tr.step()
+            torch.cuda.synchronize()
+            losses.append(tr.total_loss())
+        tr.flush()
+        torch.cuda.synchronize()
+        return losses, [(c.flat.clone(), c.adam_m.clone(), c.adam_v.clone()) for c in tr.chunks]
+
+    l0, ref = run(False)
+    l1, got = run(True)
+    # loss values: fp64 sums of block partials added with atomics (last-bit order noise only)
+    np.testing.assert_allclose(l1, l0, rtol=1e-12)
+    for (a, b, c), (x, y, z) in zip(ref, got):
+        assert torch.equal(a, x) and torch.equal(b, y) and torch.equal(c, z)

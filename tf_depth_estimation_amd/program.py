@@ -15,6 +15,7 @@ accumulate into the ParamChunk's flat gradient buffer, which the trainer zeroes 
 network called twice with shared variables (train_depth_then_cam_lr.py:130-136) sums both calls like
 TF does.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -318,6 +319,68 @@ class NetProgram:
         self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 1)
         self._ws2 = {}
         self._dzl = {}
+        self._wsplit = {}       # (N, conv math) -> pre-split weight images (_split_plan)
+        self._cur_split = None
+        self._spans = {}
+        # forward hooks (Trainer.enable_deferred_adam): pre_op(prog, i) orders the current stream after
+        # whatever updates op i's parameters; params_ready(prog, i) tells whether that has been done
+        self.pre_op = None
+        self.params_ready = None
+        self.pre_backward = None    # called first thing in backward (before any gradient is written)
+
+    def _split_plan(self, N):
+        """The convs whose forward or data-gradient call takes the halo-tiled path (their weights are kept as
+        split MFMA tiles, tde_conv2d_split_weights): [(op index, op, desc, buffer)], cached per (N, conv math)."""
+        lib = _lib.load()
+        key = (N, lib.tde_get_conv_math())
+        plan = self._wsplit.get(key)
+        if plan is None:
+            plan = []
+            for i, op in enumerate(self.spec.ops):
+                if not isinstance(op, ConvBN):
+                    continue
+                d = op.desc(N)
+                for o in (0, 1):
+                    nb = lib.tde_conv2d_split_weights_size(ctypes_ref(d), o)
+                    if nb:
+                        plan.append((i, o, d, torch.empty((nb + 255) // 256 * 64, dtype=torch.float32, device="cuda")))
+            self._wsplit[key] = plan
+        return key, plan
+
+    def _issue_split(self, jobs):
+        """Split the weights of `jobs` (entries of _split_plan) in ONE launch; valid until the weights change
+        (the optimizer step): the forward makes them, and the backward of that forward uses them."""
+        if not jobs:
+            return
+        lib = _lib.load()
+        n = len(jobs)
+        descs = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for _, _, d, _ in jobs])
+        ops = (ctypes.c_int * n)(*[o for _, o, _, _ in jobs])
+        ws = (ctypes.c_void_p * n)(*[self.P(f"{self.spec.ops[i].layer}/weights").data_ptr() for i, _, _, _ in jobs])
+        outs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, _, _, t in jobs])
+        _lib.check(lib.tde_conv2d_split_weights(n, descs, ops, ws, outs, _lib.stream_ptr()), "split weights")
+        for i, o, _, t in jobs:
+            self._cur_split[1].setdefault(i, [None, None])[o] = t.data_ptr()
+
+    def op_param_span(self, i):
+        """[lo, hi) flat-buffer span of op i's parameters (None without parameters)."""
+        span = self._spans.get(i)
+        if span is None and i not in self._spans:
+            op = self.spec.ops[i]
+            names = [f"{self.prefix}/{n}" for n, _, _ in getattr(op, "params", [])]
+            if names:
+                lo = min(self.chunk.offsets[n] for n in names)
+                hi = max(self.chunk.offsets[n] + int(np.prod(self.chunk.shapes[n])) for n in names)
+                span = (lo, hi)
+            self._spans[i] = span
+        return span
+
+    def _use_split(self, d, i, N):
+        cur = getattr(self, "_cur_split", None)
+        if cur is not None and cur[0] == (N, _lib.load().tde_get_conv_math()):
+            sp = cur[1].get(i)
+            if sp is not None:
+                d.w_split[0], d.w_split[1] = sp[0], sp[1]
 
     def _sums(self, i, K, which):
         key = (i, which)
@@ -470,11 +533,28 @@ class NetProgram:
                                          0, 0, st), "copy input")
         ws, _ = self._scratch(N)
         wsb = ws.numel() * 4
+        split_todo = {}
+        if fold_bn:
+            self._cur_split = None
+        else:
+            key, plan = self._split_plan(N)
+            self._cur_split = (key, {})
+            for job in plan:
+                split_todo.setdefault(job[0], []).append(job)
         for i, op in enumerate(spec.ops):
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
+            if self.pre_op is not None and isinstance(op, (ConvBN, Head)):
+                self.pre_op(self, i)
             if isinstance(op, ConvBN):
+                if i in split_todo:
+                    # one split launch for every pending layer whose weights are final by now (all of them
+                    # unless an optimizer step is still running on a side stream)
+                    ready = [j for j in split_todo if self.params_ready is None or self.params_ready(self, j)]
+                    self._issue_split([job for j in ready for job in split_todo.pop(j)])
                 d = op.desc(N)
+                if not fold_bn:
+                    self._use_split(d, i, N)
                 w = self.P(f"{op.layer}/weights")
                 z = run.z[i] if op.bn else None
                 if not op.bn:
@@ -556,6 +636,8 @@ class NetProgram:
         wrote (the data-parallel exchange launches a bucket once all its parameters are final, ddp.py)."""
         pacc = 1 if grad_accumulate else 0
         N = run.N
+        if self.pre_backward is not None:
+            self.pre_backward()
         lib = _lib.load()
         st = _lib.stream_ptr()
         spec = self.spec
@@ -606,6 +688,7 @@ class NetProgram:
             if isinstance(op, ConvBN):
                 use_side = side is not None and conv_rank[i] >= self.wgrad_tail
                 d = op.desc(N)
+                self._use_split(d, i, N)
                 # dz (the conv's output gradient) is the y view of a conv's descriptor, the x view of a deconv's
                 if op.deconv:
                     d.x_absmax = run.absmax_ptr(i)

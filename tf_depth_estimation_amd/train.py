@@ -134,6 +134,77 @@ class AdamOverlap:
             torch.cuda.current_stream().wait_stream(st)
 
 
+class DeferredAdam:
+    """Single-GPU: the optimizer step of step k runs at the START of step k+1 on a side stream, overlapped
+    with that step's forward, which waits (per parameter bucket, in forward order) only for the buckets of
+    the layers it is about to run.  Each chunk's flat buffer is cut into two buckets in forward order: the
+    first layers (`first_mb`, updated in a few microseconds) and the rest, which the forward needs only when
+    it reaches the deeper layers -- the high-resolution encoder layers run meanwhile.  The sequence of
+    updates and their arithmetic are those of Adam after backward (bit-identical parameters and moments once
+    flush() has applied the last step's update); the backward of step k+1 overwrites the gradients only after
+    its forward has waited for every bucket, i.e. after Adam read them."""
+
+    def __init__(self, opts, first_mb=2.0):
+        self.opts = list(opts)
+        self.side = torch.cuda.Stream()
+        self.buckets = {}
+        for o in self.opts:
+            c = o.chunk
+            cap = int(first_mb * 2 ** 20) // 4
+            offs = sorted(c.offsets.values())
+            cut = max([v for v in offs if v <= cap] or [0])
+            cuts = [0] + ([cut] if 0 < cut < c.numel else []) + [c.numel]
+            self.buckets[id(c)] = [[lo, hi, None] for lo, hi in zip(cuts[:-1], cuts[1:])]
+        self.pending = False     # an update (of the last step's gradients) is owed
+        self.active = False      # this step's forward must wait for the side stream's buckets
+        self.waited = set()
+
+    def launch(self):
+        """Start of a step: the owed update on the side stream, one event per bucket."""
+        self.active, self.waited = False, set()
+        if not self.pending:
+            return
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            for o in self.opts:
+                o.begin()
+                for b in self.buckets[id(o.chunk)]:
+                    o.update(b[0], b[1])
+                    b[2] = torch.cuda.Event()
+                    b[2].record()
+        self.active, self.pending = True, False
+
+    def _needed(self, prog, i):
+        span = prog.op_param_span(i)
+        if span is None:
+            return []
+        return [b for b in self.buckets.get(id(prog.chunk), []) if b[0] < span[1] and span[0] < b[1]]
+
+    def pre_op(self, prog, i):
+        if not self.active:
+            return
+        for b in self._needed(prog, i):
+            if id(b) not in self.waited:
+                torch.cuda.current_stream().wait_event(b[2])
+                self.waited.add(id(b))
+
+    def params_ready(self, prog, i):
+        return not self.active or all(id(b) in self.waited for b in self._needed(prog, i))
+
+    def end_forward(self):
+        """After the forward: every bucket waited for (the join of the side branch under capture)."""
+        if self.active:
+            cur = torch.cuda.current_stream()
+            for bs in self.buckets.values():
+                for b in bs:
+                    if id(b) not in self.waited:
+                        cur.wait_event(b[2])
+                        self.waited.add(id(b))
+            cur.wait_stream(self.side)
+            self.active = False
+
+
 class AllReduceGrads:
     """Data-parallel gradient exchange: ONE RCCL all-reduce (sum) of the chunk's flat fp32 gradient
     buffer, then a scale by 1/world inside the next Adam launch's input (the loss terms are batch
@@ -164,6 +235,25 @@ class Trainer:
     BACKWARD_USES = 1        # backward calls per chunk per step (shared-variable nets call it twice)
 
     adam_ov = None
+    dadam = None
+
+    def enable_deferred_adam(self, first_mb=2.0):
+        """Run each step's Adam at the start of the next step, overlapped with its forward (DeferredAdam).
+        The parameters then lag the gradients by one update until flush()."""
+        if self.grad_sync is not None or self.adam_ov is not None:
+            raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap")
+        opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
+        self.dadam = DeferredAdam(opts, first_mb)
+        for p in self.programs():
+            # the backward overwrites the gradients the update reads: it starts after every bucket is done
+            p.pre_op, p.params_ready, p.pre_backward = self.dadam.pre_op, self.dadam.params_ready, self.dadam.end_forward
+        return self.dadam
+
+    def flush(self):
+        """Apply the update a deferred-Adam step still owes (before reading or saving the parameters)."""
+        if self.dadam is not None and self.dadam.pending:
+            self.phase_update()
+            self.dadam.pending = False
 
     def enable_adam_overlap(self, bucket_mb=16.0, on_wgrad_stream=False):
         """Run each gradient bucket's Adam on a side stream as soon as backward finalises it (single GPU;
@@ -199,10 +289,15 @@ class Trainer:
     def _begin(self):
         if self.adam_ov is not None:
             self.adam_ov.begin_step()
+        if self.dadam is not None:
+            self.dadam.launch()
 
     def _update(self):
         if self.adam_ov is not None:
             self.adam_ov.finish()
+        elif self.dadam is not None:
+            self.dadam.end_forward()      # (normally already joined: the forward waited for every bucket)
+            self.dadam.pending = True
         else:
             self.phase_update()
 
