@@ -29,21 +29,22 @@ from tf_depth_estimation_amd.imageselect_Dataloader_optflow import DataLoader  #
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batches", type=int, default=40)
+    ap.add_argument("--batches", type=int, default=60)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--samples", type=int, default=64)
     ap.add_argument("--shape", default="config2", choices=["ref", "config2"])
+    ap.add_argument("--procs", type=int, default=16, help="JPEG decode worker processes (0: threads)")
     args = ap.parse_args()
     rh, rw = (240, 720) if args.shape == "ref" else (192, 256)
     B = args.batch
     tmp = tempfile.mkdtemp(prefix="tde_ds_")
-    out = {"shape": args.shape, "frames": [rh, rw], "batch": B, "workers": args.workers}
+    out = {"shape": args.shape, "frames": [rh, rw], "batch": B, "workers": args.workers, "decode_procs": args.procs}
     try:
         make_dataset(tmp, args.samples, strip_hw=(rh, 2 * rw), image_hw=(rh, rw), quality=90)
         # 1. loader alone: the consumer only waits for each batch to be resident
         dl = DataLoader(tmp, B, rh, rw, 2, 4, "train", resizedheight=rh, resizedwidth=rw, seed=0,
-                        workers=args.workers, prefetch=3)
+                        workers=args.workers, prefetch=3, decode_procs=args.procs)
         for _ in range(5):
             dl.load_train_batch()
         torch.cuda.synchronize()
@@ -97,7 +98,7 @@ def main():
             tr = train.DepthOnlyTrainer(B, rh, rw)
             tr.enable_wgrad_overlap()
             dl = DataLoader(tmp, B, rh, rw, 2, 4, "train", resizedheight=rh, resizedwidth=rw, seed=1,
-                            workers=args.workers, prefetch=3)
+                            workers=args.workers, prefetch=3, decode_procs=args.procs)
             tgt, src, label, *_ = dl.load_train_batch()
             tr.set_batch(tgt, label)
             tr.capture(warmup=2)
@@ -111,12 +112,21 @@ def main():
                     tr.step()
             run(10, True)
             torch.cuda.synchronize()
-            for feed in (False, True):
+            for feed, key in ((False, "train_synthetic"), (True, "train_fed")):
                 t0 = time.perf_counter()
                 run(args.batches, feed)
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
-                out["train_fed" if feed else "train_synthetic"] = round(B * args.batches / dt, 1)
+                out[key] = round(B * args.batches / dt, 1)
+            # the same with a 0.2 ms GIL switch interval (the consumer thread launches each step sooner while
+            # the loader's threads hold the GIL; a process-wide setting, so only measured here)
+            sw = sys.getswitchinterval()
+            sys.setswitchinterval(2e-4)
+            t0 = time.perf_counter()
+            run(args.batches, True)
+            torch.cuda.synchronize()
+            out["train_fed_switch_0.2ms"] = round(B * args.batches / (time.perf_counter() - t0), 1)
+            sys.setswitchinterval(sw)
             dl.close()
         out["host_cpus"] = os.cpu_count()
     finally:

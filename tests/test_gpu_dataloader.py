@@ -75,12 +75,17 @@ def _check_batch(got, fl, idx, ih, iw, ns, rh, rw):
         np.testing.assert_array_equal(g.cpu().numpy(), r)
 
 
-def test_loader_matches_oracle_in_order(tmp_path):
+@pytest.mark.parametrize("procs", [0, 2], ids=["threads", "procs"])
+def test_loader_matches_oracle_in_order(tmp_path, procs):
+    """procs=2: JPEG decode in two worker processes into shared memory (the 7th image is larger than the
+    first: the slot's staging grows, in the shared segment too)."""
+    import os
     from tf_depth_estimation_amd.imageselect_Dataloader_optflow import DataLoader
     root = make_dataset(str(tmp_path), 7, sizes=[(60, 180)] * 6 + [(64, 200)])
     fl = OD.read_labeled_image_list(root, "train")
+    shm_before = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
     dl = DataLoader(root, 3, 30, 90, 2, 4, "train", resizedheight=30, resizedwidth=90, shuffle=False,
-                    num_epochs=2, workers=4, prefetch=2)
+                    num_epochs=2, workers=4, prefetch=2, decode_procs=procs)
     seen = []
     try:
         while True:
@@ -94,6 +99,8 @@ def test_loader_matches_oracle_in_order(tmp_path):
         dl.close()
     # 2 epochs x 7 samples in file order, batches of 3 across the epoch boundary, last partial batch dropped
     assert seen == ([0, 1, 2, 3, 4, 5, 6] * 2)[:12]
+    if os.path.isdir("/dev/shm"):        # every shared staging segment unlinked by close()
+        assert set(os.listdir("/dev/shm")) - shm_before == set()
 
 
 def test_loader_shuffles_per_epoch(tmp_path):

@@ -33,7 +33,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
-from . import _lib
+from . import _decode_worker, _lib
 from ._lib import ImageBatch, ptr
 
 
@@ -43,12 +43,8 @@ def _hdr_bytes(B):
 
 
 def _csv_record(text, n, delim):
-    """tf.decode_csv of one record of n float fields with record_defaults [[1.]] * n (empty field -> 1.0);
-    the record is the file's content without its line terminator."""
-    fields = text.rstrip("\r\n").split(delim)
-    if len(fields) != n:
-        raise ValueError(f"expected {n} '{delim}'-separated fields, got {len(fields)}")
-    return np.array([float(v) if v.strip() else 1.0 for v in fields], dtype=np.float32)
+    """tf.decode_csv of one record of n float fields, record_defaults [[1.]] * n (_decode_worker.csv_record)."""
+    return _decode_worker.csv_record(text, n, delim)
 
 
 class _Slot:
@@ -81,7 +77,7 @@ class _Slot:
 class DataLoader(object):
     def __init__(self, dataset_dir, batch_size, image_height, image_width, num_source, num_scales, split,
                  resizedheight=240, resizedwidth=720, shuffle=True, num_epochs=1500, seed=None, workers=8,
-                 prefetch=2):
+                 prefetch=2, decode_procs=0):
         self.dataset_dir = dataset_dir
         self.batch_size = batch_size
         self.image_height = image_height
@@ -94,8 +90,12 @@ class DataLoader(object):
         self.shuffle, self.num_epochs = shuffle, num_epochs
         self._rng = np.random.default_rng(seed)
         self._workers, self._prefetch = max(1, int(workers)), max(1, int(prefetch))
+        # decode_procs > 0: JPEG decode in that many worker processes into shared memory (PIL holds the GIL
+        # for most of a decode, so threads stop scaling at ~2); 0: in the thread pool
+        self._procs = max(0, int(decode_procs))
         self._started = False
         self._held = None
+        self._retired = []
         self.last_indices = None
         self._lib = _lib.load()
 
@@ -173,6 +173,19 @@ class DataLoader(object):
                     self._free.put(sl)
                 self._thread.join(timeout=0.05)
             self._pool.shutdown(wait=True)
+            if self._ppool is not None:
+                self._ppool.terminate()
+                self._ppool.join()
+                self._ppool = None
+            for sh in [sl.shm for sl in self._slots if sl.shm is not None] + self._retired:
+                sh.close()
+                try:
+                    sh.unlink()
+                except FileNotFoundError:
+                    pass
+            self._retired = []
+            for sl in self._slots:
+                sl.shm = None
             self._started = False
 
     def __del__(self):
@@ -200,12 +213,23 @@ class DataLoader(object):
                              self.resizedwidth, self.num_scales) for _ in range(nslots)]
         for sl in self._slots:
             sl.stride = stride
+            sl.shm = None
+        self._ppool = None
+        if self._procs > 0:
+            import multiprocessing as mp
+            from multiprocessing import shared_memory
+            lab = B * self.image_height * self.image_width * 4
+            for sl in self._slots:
+                sl.shm = shared_memory.SharedMemory(create=True, size=B * stride + lab)
+            self._ppool = mp.get_context("spawn").Pool(self._procs)
         self._free = queue.Queue()
         for sl in self._slots:
             self._free.put(sl)
         self._q = queue.Queue(maxsize=self._prefetch)
         self._stop = threading.Event()
-        self._pool = ThreadPoolExecutor(self._workers)
+        # (with worker processes the thread pool only serves the rare re-stage: keep it small, fewer threads
+        # competing for the GIL with the consumer)
+        self._pool = ThreadPoolExecutor(self._workers if self._procs == 0 else 1)
         self._copy = torch.cuda.Stream()
         self._dev = torch.cuda.current_device()
         self._thread = threading.Thread(target=self._produce, daemon=True)
@@ -256,18 +280,29 @@ class DataLoader(object):
                 if slot.ready is not None:
                     slot.ready.synchronize()      # the previous H2D out of this slot's staging has finished
                 slot.indices = idx
-                futs = [self._pool.submit(self._sample, slot, b, i) for b, i in enumerate(idx)]
-                pending.append((slot, futs))
+                if self._ppool is not None:
+                    # whole samples in the worker processes (image + label into shared memory, cam / proj parsed)
+                    f, HW = self._files, self.image_height * self.image_width
+                    futs = [self._ppool.apply_async(
+                        _decode_worker.load_sample,
+                        (slot.shm.name, b * slot.stride, slot.stride, f["image_file_list"][i],
+                         B * slot.stride + b * HW * 4, HW, f["gt_depth_file_list"][i], f["cam_file_list"][i],
+                         f["tgt2src_proj_list"][i])) for b, i in enumerate(idx)]
+                    pending.append((slot, futs, True))
+                else:
+                    futs = [self._pool.submit(self._sample, slot, b, i) for b, i in enumerate(idx)]
+                    pending.append((slot, futs, False))
                 if len(pending) >= self._prefetch:
                     self._finish(*pending.popleft())
         except BaseException as e:       # surfaced by load_train_batch
             self._q.put(e)
 
     def _sample(self, slot, b, i):
-        """One sample into slot row b: image bytes at hdr + b * stride (None back if it does not fit), label,
-        intrinsics and projections (imageselect_Dataloader_optflow.py:104-183)."""
+        """One sample into slot row b: image bytes at hdr + b * stride (the image back if it does not fit),
+        label, intrinsics and projections (imageselect_Dataloader_optflow.py:104-183)."""
         f = self._files
         img = self._decode(f["image_file_list"][i])
+        h, w = img.shape[0], img.shape[1]
         fits = img.nbytes <= slot.stride
         if fits:
             st = slot.stage.numpy()
@@ -278,15 +313,23 @@ class DataLoader(object):
         if v.size != H * W:
             raise ValueError(f"{f['gt_depth_file_list'][i]}: {v.size} floats, expected {H}x{W}")
         slot.label_h.numpy()[b] = v.reshape(H, W, 1)
-        with open(f["cam_file_list"][i]) as fh:
-            cam = _csv_record(fh.read(), 9, ",").reshape(3, 3)
-        with open(f["tgt2src_proj_list"][i]) as fh:
-            pv = _csv_record(fh.read(), 34, " ")[:-1]       # :176-180
-        return img.shape[0], img.shape[1], cam, pv[:-1].reshape(2, 4, 4), pv[-1], (None if fits else img)
+        cam, projs, m = _decode_worker.read_cam_proj(f["cam_file_list"][i], f["tgt2src_proj_list"][i])
+        return h, w, cam, projs, m, (None if fits else img)
 
-    def _finish(self, slot, futs):
+    def _finish(self, slot, futs, procs=False):
         B = self.batch_size
-        res = [fu.result() for fu in futs]
+        if procs:
+            # worker-loaded samples: (h, w, image if it did not fit, cam, projs, m); shared staging -> pinned
+            res = []
+            for fu in futs:
+                h, w, big, cam, projs, m = fu.get()
+                res.append([h, w, cam, projs, m, big])
+            n = B * slot.stride
+            seg = slot.shm.buf
+            slot.stage.numpy()[slot.hdr:slot.hdr + n] = np.ndarray((n,), np.uint8, seg, 0)
+            slot.label_h.numpy().reshape(-1)[:] = np.ndarray((slot.label_h.numel(),), np.float32, seg, n)
+        else:
+            res = [list(fu.result()) for fu in futs]
         if any(r[5] is not None for r in res):      # an image larger than the slot's stride: grow, re-stage
             stride = max((r[0] * r[1] * 3 + 15) // 16 * 16 for r in res)
             old = slot.stage.numpy().copy()
@@ -297,6 +340,11 @@ class DataLoader(object):
                 src = r[5].reshape(-1) if r[5] is not None else old[slot.hdr + b * slot.stride:][:n]
                 st[slot.hdr + b * stride:slot.hdr + b * stride + n] = src
             slot.stride = stride
+            if slot.shm is not None:        # a larger shared staging area for the next batches of this slot
+                from multiprocessing import shared_memory
+                old_shm = slot.shm
+                slot.shm = shared_memory.SharedMemory(create=True, size=B * stride + slot.label_h.numel() * 4)
+                self._retired.append(old_shm)
         st = slot.stage.numpy()
         offs = slot.hdr + np.arange(B, dtype=np.int64) * slot.stride
         st[:8 * B] = offs.view(np.uint8)
