@@ -87,24 +87,28 @@ __global__ void __launch_bounds__(256) bn_part_kernel(int M, int C, const float*
   }
 }
 
-// Reduce `nparts` partials per channel.  Block = one channel quad x 256 stripes (1024 lanes; four
+// Reduce `nparts` partials per channel.  Block = one channel quad x 64 stripes (256 lanes; four
 // neighbouring lanes read 32 contiguous bytes), so a C-channel layer runs C/4 blocks; 8 loads in flight
-// per lane, fixed-order combine.  MODE 0 publishes mean / invstd and updates the moving averages;
-// MODE 1 writes coef = (mean g, mean g*xhat) and dbeta.
-constexpr int FIN_ST = 256;
-template <int MODE>
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(int M, int C, int nparts, const double* part, float eps,
-                                                           float decay, int bessel, float* mm, float* mv,
-                                                           float* save_mean, float* save_invstd, float* dbeta,
-                                                           int acc, float* coef, double* sums = nullptr) {
-  __shared__ double sh[2][1024];
+// per lane, then a fixed-order combine: an xor-shuffle tree over a wave's 16 stripes of a channel and the 4
+// waves through LDS (one barrier; the round-1 version walked 1024 lanes down 9 LDS levels with a barrier
+// each).  MODE 0 publishes mean / invstd and updates the moving averages; MODE 1 writes
+// coef = (mean g, mean g*xhat) and dbeta; MODE 2 the raw sums.
+// NT = 256 lanes for up to 512 partial rows, 1024 above (more loads in flight for the long reductions).
+template <int MODE, int NT>
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int nparts, const double* part, float eps,
+                                                         float decay, int bessel, float* mm, float* mv,
+                                                         float* save_mean, float* save_invstd, float* dbeta,
+                                                         int acc, float* coef, double* sums = nullptr) {
+  constexpr int FIN_ST = NT / 4, NWV = NT / 64;
+  __shared__ double sh[2][NWV][4];
   const int cl = threadIdx.x & 3, st = threadIdx.x >> 2;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 4 + cl;
-  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   int k = st;
-  for (; k + 7 * FIN_ST < nparts; k += 8 * FIN_ST) {
+  for (; k + 3 * FIN_ST < nparts; k += 4 * FIN_ST) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       a[u] += part[(long)(k + u * FIN_ST) * 2 * C + c];
       b[u] += part[(long)(k + u * FIN_ST) * 2 * C + C + c];
     }
@@ -113,19 +117,18 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(int M, int C, int npa
     a[u] += part[(long)k * 2 * C + c];
     b[u] += part[(long)k * 2 * C + C + c];
   }
-  sh[0][threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  sh[1][threadIdx.x] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
-  __syncthreads();
-  // 1024 -> 4 in fixed halving steps
-  for (int h = 512; h >= 4; h >>= 1) {
-    if (threadIdx.x < h) {
-      sh[0][threadIdx.x] += sh[0][threadIdx.x + h];
-      sh[1][threadIdx.x] += sh[1][threadIdx.x + h];
-    }
-    __syncthreads();
+  double ra = (a[0] + a[1]) + (a[2] + a[3]), rb = (b[0] + b[1]) + (b[2] + b[3]);
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {   // the 16 lanes of this wave with the same channel (lane bits 2..5)
+    ra += __shfl_xor(ra, o, 64);
+    rb += __shfl_xor(rb, o, 64);
   }
+  if (lane < 4) { sh[0][wv][lane] = ra; sh[1][wv][lane] = rb; }
+  __syncthreads();
   if (threadIdx.x >= 4) return;
-  const double s = sh[0][cl], s2 = sh[1][cl];
+  double s = 0, s2 = 0;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) { s += sh[0][w][cl]; s2 += sh[1][w][cl]; }
   if (MODE == 2) {   // raw per-channel sums (SyncBN: all-reduced by the caller, then *_from_sums)
     sums[c] = s;
     sums[C + c] = s2;
@@ -432,6 +435,18 @@ int apply_rows_per_block(int M, int C) {
 
 int finalize_blocks(int C) { return C / 4; }
 
+template <int MODE>
+void finalize_launch(int nparts, int C, hipStream_t st, int M, const double* part, float eps, float decay, int bessel,
+                     float* mm, float* mv, float* save_mean, float* save_invstd, float* dbeta, int acc, float* coef,
+                     double* sums) {
+  if (nparts <= 512)
+    hipLaunchKernelGGL((bn_finalize_kernel<MODE, 256>), dim3(finalize_blocks(C)), dim3(256), 0, st, M, C, nparts, part,
+                       eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums);
+  else
+    hipLaunchKernelGGL((bn_finalize_kernel<MODE, 1024>), dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, nparts,
+                       part, eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ internal launchers (bn_internal.h)
@@ -467,8 +482,8 @@ void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream
 
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
                                  hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, nparts, part, o.eps,
-                     o.decay, o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, nullptr, 0, nullptr);
+  finalize_launch<0>(nparts, C, st, M, part, o.eps, o.decay, o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, nullptr,
+                     0, nullptr, nullptr);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, o.save_mean,
                      o.save_invstd, o.beta, o.relu, o.y, o.ycs, o.yco, rpb);
@@ -540,8 +555,8 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
   float* coef = reinterpret_cast<float*>(part + (size_t)pp.chunks * 2 * C);
   hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride, dy_coff,
                      save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, pp.chunks, part, 0.f,
-                     0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
+  finalize_launch<1>(pp.chunks, C, st, M, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta,
+                     coef, nullptr);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                      dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
@@ -565,8 +580,8 @@ int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, i
   else
     hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                        dy_coff, save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
-  hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, pp.chunks, part, 0.f,
-                     0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, sums);
+  finalize_launch<2>(pp.chunks, C, st, M, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                     sums);
   return tde_launch_status();
 }
 
