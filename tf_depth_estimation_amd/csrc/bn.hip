@@ -72,15 +72,8 @@ __global__ void __launch_bounds__(256) bn_part_kernel(int M, int C, const float*
       for (int j = 0; j < 4; ++j) { s0[j] += f0[j]; s1[j] += f1[j]; }
     }
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { sh[0][threadIdx.x * 4 + j] = s0[j]; sh[1][threadIdx.x * 4 + j] = s1[j]; }
-  __syncthreads();
+  rowlane_combine(s0, s1, nq, ty_n, &sh[0][0]);
   if (ty == 0) {
-    for (int t = 1; t < ty_n; ++t) {
-      const int s = (t * nq + tx) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { s0[j] += sh[0][s + j]; s1[j] += sh[1][s + j]; }
-    }
     double* o = part + (long)blockIdx.x * 2 * C;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o[c + j] = s0[j]; o[C + c + j] = s1[j]; }

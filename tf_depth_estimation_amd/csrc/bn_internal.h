@@ -29,3 +29,45 @@ void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream
 // From `nparts` fp64 partials [part][2][C] of z: finalize (one small launch) + apply (one launch).
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
                                  hipStream_t st);
+
+// Row-lane combine of the partial-sum kernels (bn_part_kernel, splitk_reduce_bn_kernel): thread = ty * nq + tx
+// (256 threads, nq channel quads), s0 / s1 its 4-channel sums.  Leaves the block's sums for quad tx in the
+// threads with ty == 0 (tid < nq), combined in a fixed order: an xor-shuffle tree over a wave's row lanes and
+// one LDS level over the 4 waves when nq is a power of two (64 % nq == 0), else the serial LDS loop.
+__device__ __forceinline__ void rowlane_combine(double (&s0)[4], double (&s1)[4], int nq, int ty_n,
+                                                double* sh /* [2][256*4] */) {
+  const int tid = threadIdx.x;
+  if ((nq & (nq - 1)) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      for (int o = nq; o < 64; o <<= 1) {
+        s0[j] += __shfl_xor(s0[j], o, 64);
+        s1[j] += __shfl_xor(s1[j], o, 64);
+      }
+    const int lane = tid & 63, wv = tid >> 6;
+    if (lane < nq) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { sh[(wv * 16 + lane) * 4 + j] = s0[j]; sh[1024 + (wv * 16 + lane) * 4 + j] = s1[j]; }
+    }
+    __syncthreads();
+    if (tid < nq) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s0[j] = sh[tid * 4 + j]; s1[j] = sh[1024 + tid * 4 + j];
+        for (int w = 1; w < 4; ++w) { s0[j] += sh[(w * 16 + tid) * 4 + j]; s1[j] += sh[1024 + (w * 16 + tid) * 4 + j]; }
+      }
+    }
+    return;
+  }
+  const int tx = tid % nq;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { sh[tid * 4 + j] = s0[j]; sh[1024 + tid * 4 + j] = s1[j]; }
+  __syncthreads();
+  if (tid < nq) {
+    for (int t = 1; t < ty_n; ++t) {
+      const int o = (t * nq + tx) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s0[j] += sh[o + j]; s1[j] += sh[1024 + o + j]; }
+    }
+  }
+}

@@ -1021,15 +1021,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) { s0[j] = f0[j]; s1[j] = f1[j]; }
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { sh[0][threadIdx.x * 4 + j] = s0[j]; sh[1][threadIdx.x * 4 + j] = s1[j]; }
-  __syncthreads();
+  rowlane_combine(s0, s1, nq, ty_n, &sh[0][0]);
   if (ty == 0) {
-    for (int t = 1; t < ty_n; ++t) {
-      const int o = (t * nq + tx) * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { s0[j] += sh[0][o + j]; s1[j] += sh[1][o + j]; }
-    }
     double* o = part + (long)blockIdx.x * 2 * cols;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o[c + j] = s0[j]; o[cols + c + j] = s1[j]; }
