@@ -16,7 +16,7 @@ ok_or_stop() {  # rc 0 (pass) and 1 (test failures) keep going; anything else is
 }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 700 python -m pytest tests -q -m gpu ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
   ok_or_stop $? "pytest -m gpu"
   grep -E "passed|failed|FAILED|ERROR" gpurun_out/gpu_tests.log | tail -20
 fi

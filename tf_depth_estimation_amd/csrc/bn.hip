@@ -97,6 +97,13 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int npart
   const int cl = threadIdx.x & 3, st = threadIdx.x >> 2;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 4 + cl;
+  // the read-modify-write operands of the 4 publishing lanes, loaded before the reduction so their
+  // latency overlaps the partial-sum loads (after the barrier they would add one dependent round trip)
+  float mm0 = 0.f, mv0 = 0.f, db0 = 0.f;
+  if (threadIdx.x < 4) {
+    if (MODE == 0 && mm) { mm0 = mm[c]; mv0 = mv[c]; }
+    if (MODE == 1 && dbeta && acc) db0 = dbeta[c];
+  }
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   int k = st;
   for (; k + 3 * FIN_ST < nparts; k += 4 * FIN_ST) {
@@ -133,11 +140,11 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int npart
     save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
     if (mm) {
       const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
-      mm[c] -= (mm[c] - (float)mean) * (1.f - decay);
-      mv[c] -= (mv[c] - (float)vu) * (1.f - decay);
+      mm[c] = mm0 - (mm0 - (float)mean) * (1.f - decay);
+      mv[c] = mv0 - (mv0 - (float)vu) * (1.f - decay);
     }
   } else {
-    if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)s : (float)s;
+    if (dbeta) dbeta[c] = acc ? db0 + (float)s : (float)s;
     coef[c] = (float)(s / M);
     coef[C + c] = (float)(s2 / M);
   }
@@ -267,6 +274,10 @@ __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const f
   __shared__ float s_mu[4], s_is[4];
   const int c = blockIdx.x * 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // beta and the moving averages loaded up front (off the reduce -> publish -> apply chain)
+  const f4 bt = *reinterpret_cast<const f4*>(beta + c);
+  float mm0 = 0.f, mv0 = 0.f;
+  if (threadIdx.x < 4 && mm) { mm0 = mm[c + threadIdx.x]; mv0 = mv[c + threadIdx.x]; }
   f4 v[SMALL_R];
   float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -295,12 +306,11 @@ __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const f
     save_invstd[cc] = is;
     if (mm) {
       const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
-      mm[cc] -= (mm[cc] - mu) * (1.f - decay);
-      mv[cc] -= (mv[cc] - (float)vu) * (1.f - decay);
+      mm[cc] = mm0 - (mm0 - mu) * (1.f - decay);
+      mv[cc] = mv0 - (mv0 - (float)vu) * (1.f - decay);
     }
   }
   __syncthreads();
-  const f4 bt = *reinterpret_cast<const f4*>(beta + c);
 #pragma unroll
   for (int i = 0; i < SMALL_R; ++i) {
     const int r = threadIdx.x + 256 * i;
@@ -327,6 +337,7 @@ __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const f
   const f4 mu = *reinterpret_cast<const f4*>(mean + c);
   const f4 is = *reinterpret_cast<const f4*>(invstd + c);
   const f4 bt = *reinterpret_cast<const f4*>(beta + c);
+  const float db0 = (threadIdx.x < 4 && dbeta && acc) ? dbeta[c + threadIdx.x] : 0.f;
   f4 xr[SMALL_R], gr[SMALL_R];
   float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -357,7 +368,7 @@ __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const f
     const double sx = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
     s_mg[j] = (float)(s / M);
     s_mgx[j] = (float)(sx / M);
-    if (dbeta) dbeta[c + j] = acc ? dbeta[c + j] + (float)s : (float)s;
+    if (dbeta) dbeta[c + j] = acc ? db0 + (float)s : (float)s;
   }
   __syncthreads();
   float mx = 0.f;

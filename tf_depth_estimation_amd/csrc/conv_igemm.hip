@@ -943,11 +943,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
   const int zlane = threadIdx.x % zl, ql = threadIdx.x / zl, qpb = 256 / zl;
   for (long i0 = (long)blockIdx.x * qpb; i0 < total4; i0 += (long)gridDim.x * qpb) {
     const long i = i0 + ql;
-    f4 s = {0.f, 0.f, 0.f, 0.f};
+    f4 s = {0.f, 0.f, 0.f, 0.f}, prev = {0.f, 0.f, 0.f, 0.f};
     int row = 0, col = 0;
+    float* dst = nullptr;
     if (i < total4) {
       row = (int)(i / (cols / 4));
       col = 4 * (int)(i - (long)row * (cols / 4));
+      if constexpr (MODE == MODE_FWD) {
+        dst = p.y + (long)row * p.ycs + p.yco + col;
+      } else if constexpr (MODE == MODE_DGRAD) {
+        dst = p.dx + (long)row * p.xcs + p.xco + col;
+      } else {
+        const int tap = row / p.C, c = row - tap * p.C;
+        dst = c < p.wcin ? p.dw + (long)(tap * p.wcin + c) * p.K + col : nullptr;
+      }
+      // the accumulated-into value is loaded with the slabs (not after the sum: one round trip less)
+      if (p.accumulate && zlane == 0 && dst) prev = ld4(dst);
       const float* src = p.ws + (long)row * cols + col;
       f4 s4[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       int z = zlane;
@@ -966,18 +977,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
       }
       __syncthreads();
     }
-    if (zlane != 0 || i >= total4) continue;
-    float* dst;
-    if constexpr (MODE == MODE_FWD) {
-      dst = p.y + (long)row * p.ycs + p.yco + col;
-    } else if constexpr (MODE == MODE_DGRAD) {
-      dst = p.dx + (long)row * p.xcs + p.xco + col;
-    } else {
-      const int tap = row / p.C, c = row - tap * p.C;
-      if (c >= p.wcin) continue;
-      dst = p.dw + (long)(tap * p.wcin + c) * p.K + col;
-    }
-    if (p.accumulate) s += ld4(dst);
+    if (zlane != 0 || i >= total4 || !dst) continue;
+    if (p.accumulate) s += prev;
     if constexpr (MODE != MODE_WGRAD) {
       if (p.bias || p.relu) {
 #pragma unroll
