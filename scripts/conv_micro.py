@@ -32,6 +32,14 @@ SHAPES = [
     ("cnv7b", 8, 2, 2, 512, 512, 3, 1),
     ("icnv7", 8, 2, 2, 1024, 512, 3, 1),
     ("cnv6b", 8, 3, 4, 512, 512, 3, 1),
+    # deconvs as their virtual convs (x = deconv output, y = deconv input): "dgrad" = the deconv forward,
+    # "fwd" = its data gradient
+    ("upcnv1", 8, 192, 256, 16, 32, 3, 2),
+    ("upcnv2", 8, 96, 128, 32, 64, 3, 2),
+    ("upcnv3", 8, 48, 64, 64, 128, 3, 2),
+    ("upcnv4", 8, 24, 32, 128, 256, 3, 2),
+    ("upcnv5", 8, 12, 16, 256, 512, 3, 2),
+    ("upcnv6", 8, 6, 8, 512, 512, 3, 2),
 ]
 
 

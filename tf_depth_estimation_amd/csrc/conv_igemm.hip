@@ -1073,6 +1073,8 @@ static const long g_split_slab = tde_env_pos("TDE_SPLIT_SLAB_MB", 128) << 20;
 static const long g_force_bn = env_long("TDE_FORCE_BN", 0);
 static const long g_force_bm = env_long("TDE_FORCE_BM", 0);
 static const long g_force_splits = env_long("TDE_FORCE_SPLITS", 0);
+// column tile cap of the 64-row (deep-level) tiles: narrower tiles = more tiles = fewer K splits (tuning)
+static const long g_deep_bn = env_long("TDE_DEEP_BN", 0);
 
 static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to which FWD / DGRAD go skinny
 
@@ -1123,6 +1125,10 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
   // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.
   if ((mode != MODE_WGRAD && tiles < 256 && M <= 4096) || g_force_bm == 64 || fix_bm == 64) {
     pl.bm = 64;
+    tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
+  }
+  if (g_deep_bn && pl.bm == 64 && !fix_bn && !g_force_bn && pl.bn > g_deep_bn) {
+    pl.bn = (int)g_deep_bn;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
   if (fix_bm == 128 && pl.bm != 128) {
@@ -1227,8 +1233,10 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   return b;
 }
 
-// prefetch depth (tiles in flight) of the fp32 kernels: 1 for 128-row tiles, 2 for the 64-row tiles of
-// the deep layers (TDE_CONV_PF: 1 / 2 forces one depth for all, tuning experiments)
+// prefetch depth (tiles in flight): 1 for 128-row tiles; for the 64-row tiles of the deep layers 2 in the
+// register-split maths, 1 in fp16x3 (depth 2 costs 187 VGPR+AGPR = 2 waves/SIMD, depth 1 136 = 3; measured
+// (scripts/r02zm.sh) icnv5 DGRAD 43.6 -> 36.6 us, config 2 2.82 -> 2.80 ms, config 4 13.30 -> 13.18 ms).
+// TDE_CONV_PF: 1 / 2 forces one depth for all (tuning experiments).
 static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
 // wave layout of a tile: 2 x 2 waves when BN is a multiple of TDE_WN_DIV, else 4 x 1 (all rows split)
 #ifndef TDE_WN_DIV
@@ -1253,8 +1261,8 @@ template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
-  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? 2 : 1);
   const int math = tile_math(BN, MODE);
+  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 && math != 4 ? 2 : 1);
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 4 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
