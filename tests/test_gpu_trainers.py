@@ -401,3 +401,50 @@ def test_deferred_adam_matches_plain(cfg, graph):
     np.testing.assert_allclose(l1, l0, rtol=1e-12)
     for (a, b, c), (x, y, z) in zip(ref, got):
         assert torch.equal(a, x) and torch.equal(b, y) and torch.equal(c, z)
+
+
+@pytest.mark.parametrize("wgrad", [False, True], ids=["wgrad_inline", "wgrad_side"])
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_net_overlap_matches_serial(graph, wgrad):
+    """Trainer.enable_net_overlap (config 4): depth_net's forward and backward calls on a second stream beside
+    disp_net's (a parallel graph branch under capture) give the serial step's parameters, gradients and Adam
+    moments bit for bit after two steps -- the programs share nothing, and each program's calls keep their
+    order.  Consistency weight 0: its float-atomic scatter is the only non-deterministic term (see above)."""
+    from tf_depth_estimation_amd import _api, train, variables
+
+    def run(overlap):
+        variables.get_store().reset(seed=1)
+        _api.clear_programs()
+        B, H, W = 2, 64, 96
+        tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+        lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
+        tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
+                     torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
+                     small_pose(B, 4).cuda())
+        if wgrad:
+            tr.enable_wgrad_overlap()
+        if overlap:
+            tr.enable_net_overlap()
+        if graph:
+            tr.capture(warmup=1)
+        for _ in range(2):
+            tr.step()
+        torch.cuda.synchronize()
+        return tr.total_loss(), [(c.flat.clone(), c.grad.clone(), c.adam_m.clone(), c.adam_v.clone())
+                                 for c in tr.chunks]
+
+    l0, ref = run(False)
+    l1, got = run(True)
+    np.testing.assert_allclose(l1, l0, rtol=1e-12)
+    for a, b in zip(ref, got):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+def test_net_overlap_rejects_exchange_hooks():
+    from tf_depth_estimation_amd import _api, train, variables
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    tr = train.DepthThenCamTrainer(2, 64, 96)
+    tr.enable_adam_overlap(bucket_mb=0.5)
+    with pytest.raises(ValueError):
+        tr.enable_net_overlap()

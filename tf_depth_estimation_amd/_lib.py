@@ -183,6 +183,26 @@ def stream_ptr():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+_hip = None
+_own_streams = []
+
+
+def dedicated_stream():
+    """A HIP stream of its own (hipStreamCreateWithFlags, non-blocking) wrapped as a torch ExternalStream, kept for
+    the life of the process.  torch.cuda.Stream() hands out streams from a fixed round-robin pool, so after enough
+    of them a "new" stream can be the very HIP stream a graph is being captured on or another side stream: a
+    cross-stream wait between the two is then a self-wait, and one such capture crashed in capture_end."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    rc = _hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
+    if rc != 0 or not s.value:
+        raise TdeError(f"hipStreamCreateWithFlags failed ({rc})")
+    _own_streams.append(s)
+    return torch.cuda.ExternalStream(s.value)
+
+
 def call(name, *args):
     """Call an int-returning ABI function and raise on a non-zero status."""
     lib = load()

@@ -236,6 +236,27 @@ class Trainer:
 
     adam_ov = None
     dadam = None
+    net_stream = None        # enable_net_overlap: the second program's calls on their own stream
+
+    def enable_net_overlap(self, on=True):
+        """Single GPU: run the calls of one network program concurrently with those of the other on a second
+        stream (config 4: `depth_net` on both pairs beside `disp_net` on both images, forward and backward;
+        a parallel graph branch under capture).  The two programs share no buffer, parameter, gradient or
+        moving statistic, and each program's calls keep their order, so the step is bit-identical to the
+        serial one.  Not combinable with the bucketed exchange, Adam overlaps or SyncBN (their hooks and
+        collectives order against the one compute stream)."""
+        if on and (self.grad_sync is not None or self.adam_ov is not None or self.dadam is not None or
+                   getattr(self, "sync_bn", False)):
+            raise ValueError("net overlap is for the single-GPU step without exchange / Adam overlap / SyncBN")
+        self.net_stream = _lib.dedicated_stream() if on else None
+        return self
+
+    def _overlap_stream(self):
+        """The second stream when the overlap applies to this call (not under the instrumented eager step,
+        whose per-family HIP-event timer records on one stream)."""
+        if self.net_stream is None or any(getattr(p, "timer", None) is not None for p in self.programs()):
+            return None
+        return self.net_stream
 
     def enable_deferred_adam(self, first_mb=2.0):
         """Run each step's Adam at the start of the next step, overlapped with its forward (DeferredAdam).
@@ -593,21 +614,112 @@ class DepthThenCamTrainer(Trainer):
     def phase_update(self):
         self.opt.step()
 
-    def phase_compute(self):
-        from . import losses as Ls
+    # phase_compute in pieces: "main" pieces on the compute stream, "ov" pieces (depth_net's calls) on the
+    # second stream under enable_net_overlap.  Under capture each piece is its own graph (a whole program
+    # forked onto a captured side branch made capture_end crash in a long-lived process -- ROCm 7 graph
+    # instantiation, not reproducible alone), and replay interleaves them with stream waits.
+    def _pieces(self):
+        return [("main", self._p_inputs), ("ov", self._p_fwd_pair), ("main", self._p_fwd_single), ("join", None),
+                ("main", self._p_loss), ("ov", self._p_bwd_pair), ("main", self._p_bwd_single), ("join", None)]
+
+    def _p_inputs(self):
         lib, st = _lib.load(), _lib.stream_ptr()
-        B, H, W, w = self.N, self.H, self.W, self.w
-        M = B * H * W
+        M = self.N * self.H * self.W
         self.arena.zero()
         # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
         for key, (a, b) in (("lr", ("l", "r")), ("rl", ("r", "l"))):
             dst = self.pair_in[key]
             _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[a]), 3, 0, ptr(dst), 6, 0, 0, st), "concat")
             _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[b]), 3, 0, ptr(dst), 6, 3, 0, st), "concat")
-        out = {"sl": self.single.forward(self.runs["sl"], self.img["l"]),
-               "sr": self.single.forward(self.runs["sr"], self.img["r"]),
-               "pl": self.pair.forward(self.runs["pl"], self.pair_in["lr"]),
-               "pr": self.pair.forward(self.runs["pr"], self.pair_in["rl"])}
+
+    def _p_fwd_pair(self):
+        self._out["pl"] = self.pair.forward(self.runs["pl"], self.pair_in["lr"])
+        self._out["pr"] = self.pair.forward(self.runs["pr"], self.pair_in["rl"])
+
+    def _p_fwd_single(self):
+        self._out["sl"] = self.single.forward(self.runs["sl"], self.img["l"])
+        self._out["sr"] = self.single.forward(self.runs["sr"], self.img["r"])
+
+    # each net runs twice (shared variables): the first backward call overwrites its gradients, the second
+    # accumulates -- no zeroed gradient buffer needed
+    def _bwd(self, k, prog, first):
+        prog.backward(self.runs[k], [IN_PLACE] * len(self.d_out[k]), on_grads=self.hook(prog.chunk),
+                      grad_accumulate=not first)
+
+    def _p_bwd_pair(self):
+        self._bwd("pr", self.pair, True)
+        self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
+
+    def _p_bwd_single(self):
+        self._bwd("sr", self.single, True)
+        self._bwd("sl", self.single, False)
+
+    def phase_compute(self):
+        self._out = {}
+        ov = self._overlap_stream()
+        cur = torch.cuda.current_stream()
+        for where, fn in self._pieces():
+            if where == "join":
+                if ov is not None:
+                    cur.wait_stream(ov)
+            elif where == "ov" and ov is not None:
+                # depth_net on both pairs on the second stream, beside disp_net on both images
+                ov.wait_stream(cur)
+                with torch.cuda.stream(ov):
+                    fn()
+            else:
+                fn()
+
+    def capture(self, warmup=2):
+        """With the net overlap: one graph per piece, captured on the piece's stream; step() replays them
+        with the same stream waits as the eager overlapped step."""
+        if self._overlap_stream() is None:
+            return super().capture(warmup)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_eager()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        main, ov = _lib.dedicated_stream(), self.net_stream
+        pieces = self._pieces() + [("main", self._update)]
+        seq = []
+        self._out = {}
+        for where, fn in pieces:
+            if where == "join":
+                seq.append((where, None))
+                continue
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(ov if where == "ov" else main):
+                g.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+                fn()
+                g.capture_end()
+            seq.append((where, g))
+        torch.cuda.synchronize()
+        self.ov_seq = seq
+        self.graphs = [g for _, g in seq if g is not None]
+        return self.graphs
+
+    def step(self):
+        if self.graphs is None or getattr(self, "ov_seq", None) is None:
+            return super().step()
+        cur, ov = torch.cuda.current_stream(), self.net_stream
+        for where, g in self.ov_seq:
+            if where == "join":
+                cur.wait_stream(ov)
+            elif where == "ov":
+                ov.wait_stream(cur)
+                with torch.cuda.stream(ov):
+                    g.replay()
+            else:
+                g.replay()
+
+    def _p_loss(self):
+        from . import losses as Ls
+        lib, st = _lib.load(), _lib.stream_ptr()
+        B, w, out = self.N, self.w, self._out
         # pose_final = reduce_mean(pose_pred, [1,2]) (nets_optflow_depth.py:183-186)
         for run_key, d in (("pl", "lr"), ("pr", "rl")):
             pp = out[run_key][4]
@@ -643,12 +755,6 @@ class DepthThenCamTrainer(Trainer):
             gpp = self.d_out[run_key][4]
             _lib.check(lib.tde_spatial_mean_bwd(B, gpp.shape[1] * gpp.shape[2], 6, ptr(gpp), 6, 0,
                                                 ptr(self.g_pose[d]), st), "pose mean bwd")
-        # each net runs twice (shared variables): the first backward call overwrites its gradients,
-        # the second accumulates -- no zeroed gradient buffer needed
-        for k, prog, first in (("pr", self.pair, True), ("pl", self.pair, False), ("sr", self.single, True),
-                               ("sl", self.single, False)):
-            prog.backward(self.runs[k], [IN_PLACE] * len(self.d_out[k]), on_grads=self.hook(prog.chunk),
-                          grad_accumulate=not first)
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
