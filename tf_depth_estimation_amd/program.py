@@ -25,6 +25,15 @@ from . import _lib
 from ._lib import ConvDesc, ptr
 
 
+def _env_nonneg(name, default):
+    """Non-negative integer tuning knob from the environment (missing / non-numeric / negative: default)."""
+    try:
+        v = int(os.environ.get(name, ""))
+    except ValueError:
+        return default
+    return v if v >= 0 else default
+
+
 def _env_pos(name, default):
     """Positive integer tuning knob from the environment (missing / non-numeric / non-positive: default)."""
     try:
@@ -317,6 +326,11 @@ class NetProgram:
         # compute stream (fused launch): the side stream's backlog at the end of backward is what the compute
         # stream waits for
         self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 1)
+        # layers whose forward output has at most this many rows (N*OH*OW) keep the fused data + filter gradient
+        # launch on the compute stream: at the deep levels the data gradient alone leaves most CUs idle, so the
+        # filter-gradient blocks ride along, instead of queueing on the side stream behind the high-resolution
+        # layers' filter gradients (0: every layer but the tail goes to the side stream)
+        self.wgrad_inline_m = _env_nonneg("TDE_WGRAD_INLINE_M", 0)
         self._ws2 = {}
         self._dzl = {}
         self._wsplit = {}       # (N, conv math) -> pre-split weight images (_split_plan)
@@ -686,7 +700,8 @@ class NetProgram:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
             if isinstance(op, ConvBN):
-                use_side = side is not None and conv_rank[i] >= self.wgrad_tail
+                use_side = (side is not None and conv_rank[i] >= self.wgrad_tail and
+                            N * op.dst.H * op.dst.W > self.wgrad_inline_m)
                 d = op.desc(N)
                 self._use_split(d, i, N)
                 # dz (the conv's output gradient) is the y view of a conv's descriptor, the x view of a deconv's
