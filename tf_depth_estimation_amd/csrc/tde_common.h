@@ -45,6 +45,15 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// XCD-contiguous logical block index: the hardware deals blocks round-robin over the 8 XCDs (each with its
+// own L2), so logical blocks [x*q + min(x, r), ...) of XCD x = physical b with b % 8 == x.  A bijection for any
+// nb; used where neighbouring blocks read neighbouring 16-byte pieces of the same cache lines (per-channel-quad
+// BatchNorm kernels), so a line is pulled into one L2 instead of eight.  Placement is a speed hint only.
+__device__ __forceinline__ int tde_xcd_block(int b, int nb) {
+  const int x = b & 7, q = nb >> 3, r = nb & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 __device__ __forceinline__ float tde_sign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
 // Block-wide sum of a double (blockDim.x == 256), result valid in thread 0.
