@@ -565,11 +565,12 @@ def test_adam_matches_tf_form(L):
     close(gp - dev(p0), pr["p"] - p0, tol=1e-4, what="adam delta")
 
 
-# 2 x 192 x 256 is the production shape: scale 0 needs 384 blocks and is capped at 128 (TDE_PYR_MAXB), so
-# every thread of the capped scales walks the `loc += nb * 256` grid stride several times and the block ->
-# scale lookup (bstart) spans capped and uncapped scales
+# 2 x 192 x 256: scale 0 needs 384 blocks and is capped at 192 (TDE_PYR_MAXB), so every thread of the capped
+# scale walks the `loc += nb * 256` grid stride twice and the block -> scale lookup (bstart) spans capped and
+# uncapped scales; 8 x 192 x 256 (config 2's batch) caps scales 0 and 1 (1536 and 384 blocks -> 192 each)
 @pytest.mark.parametrize("recip,nonfinite,acc,N,H,W", [(0, 0, 0, 2, 24, 32), (1, 1, 1, 2, 24, 32), (0, 1, 0, 2, 24, 32),
-                                                       (0, 1, 0, 2, 192, 256), (1, 0, 1, 2, 192, 256)])
+                                                       (0, 1, 0, 2, 192, 256), (1, 0, 1, 2, 192, 256),
+                                                       (0, 1, 0, 8, 192, 256)])
 def test_loss_depth_pyramid_matches_separate_terms(L, recip, nonfinite, acc, N, H, W):
     """tde_loss_depth_pyramid (all scales, one launch) == tde_resize_area_fwd + tde_loss_smooth2 +
     tde_loss_l1 per scale, values and gradients, including the write (acc=0) and add modes."""

@@ -369,10 +369,12 @@ int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int cof
   return tde_launch_status();
 }
 
-// blocks per scale at most: every block ends in two fp64 atomics on the same two accumulators
-// (rocprofv3, config 2: 4096 -> 61 us, 512 -> 38 us, 128 -> 30 us per step)
+// blocks per scale at most: every block ends in two fp64 atomics on the same two accumulators, and the
+// full-resolution scale's blocks each walk (scale pixels / cap) pixels (rocprofv3, config 2: 4096 -> 61 us,
+// 512 -> 38 us, 128 -> 30 us per step; round 2 re-sweep, scripts/r02s7_pyrmaxb.sh: 128 / 160 / 192 / 224 ->
+// 30.3 / 23.1 / 21.8 / 22.9 us (config 2), 28.4 / 23.5 / 20.9 / 19.9 us (config 4))
 // (TDE_PYR_MAXB tuning knob; a missing, non-numeric or non-positive value means the default)
-static const long g_pyr_maxb = tde_env_pos("TDE_PYR_MAXB", 128);
+static const long g_pyr_maxb = tde_env_pos("TDE_PYR_MAXB", 192);
 
 int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
   TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
