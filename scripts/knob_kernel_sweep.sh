@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 KNOB=$1; PAT=$2; WLS=$3; VALS=$4
 for w in $WLS; do for b in $VALS; do
-  d="$PWD/gpurun_out/prof_knob_${w}_$b"
+  d="$PWD/gpurun_out/prof_knob_${w}_$(basename "$b")"
   env "$KNOB=$b" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv \
     -- python3 bench.py --workload $w --steps 20 --warmup 5 --no-cpu-baseline > "$d.log" 2>&1 || exit 1
   f=$(find "$d" -name "*kernel_stats.csv" | head -1)

@@ -40,14 +40,17 @@ __global__ void __launch_bounds__(256) fill_kernel(long n, float* x, float val) 
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] = val;
 }
 
+// I = unsigned when every element offset fits 32 bits (the row split is then a 32-bit division, not the
+// long-division sequence of a 64-bit one)
+template <typename I>
 __global__ void __launch_bounds__(256) copy_view_kernel(int M, int C, const float* s, int scs, int sco, float* d,
                                                         int dcs, int dco, int acc) {
-  const long total = (long)M * C;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / C;
-    const int c = (int)(i - r * C);
-    const float v = s[r * scs + sco + c];
-    float* o = d + r * dcs + dco + c;
+  const I total = (I)M * (I)C;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const I r = i / (I)C;
+    const I c = i - r * (I)C;
+    const float v = s[r * (I)scs + (I)sco + c];
+    float* o = d + r * (I)dcs + (I)dco + c;
     *o = acc ? *o + v : v;
   }
 }
@@ -158,8 +161,15 @@ int tde_fill(size_t n, float* x, float value, void* stream) {
 int tde_copy_view(int M, int C, const float* src, int s_cstride, int s_coff, float* dst, int d_cstride, int d_coff,
                   int accumulate, void* stream) {
   TDE_CHECK_ARG(M > 0 && C > 0 && src && dst);
-  hipLaunchKernelGGL(copy_view_kernel, dim3(ew_grid((long)M * C)), dim3(256), 0, static_cast<hipStream_t>(stream), M,
-                     C, src, s_cstride, s_coff, dst, d_cstride, d_coff, accumulate);
+  TDE_CHECK_ARG(s_cstride >= C && d_cstride >= C && s_coff >= 0 && d_coff >= 0);
+  const long span = (long)M * (s_cstride > d_cstride ? s_cstride : d_cstride) + (s_coff > d_coff ? s_coff : d_coff);
+  const dim3 grid(ew_grid((long)M * C));
+  if (span < 0x7fffffffL)
+    hipLaunchKernelGGL(copy_view_kernel<unsigned>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), M, C, src,
+                       s_cstride, s_coff, dst, d_cstride, d_coff, accumulate);
+  else
+    hipLaunchKernelGGL(copy_view_kernel<long>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), M, C, src,
+                       s_cstride, s_coff, dst, d_cstride, d_coff, accumulate);
   return tde_launch_status();
 }
 
