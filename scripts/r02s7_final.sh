@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-me
 rc=$?; tail -3 gpurun_out/final_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final_smoke.log 2>&1
 rc=$?; tail -2 gpurun_out/final_smoke.log; [ $rc -ne 0 ] && exit $rc
-STEPS=100 bash scripts/bench_all.sh r02s7 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof_r02s7_config2" -o run --output-format csv \
-  -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_r02s7_config2.log 2>&1 || exit 1
-find gpurun_out/prof_r02s7_config2 -name "*stats*"
+STEPS=100 bash scripts/bench_all.sh ${TAG:-r02s7} || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof_${TAG:-r02s7}_config2" -o run --output-format csv \
+  -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_${TAG:-r02s7}_config2.log 2>&1 || exit 1
+find gpurun_out/prof_${TAG:-r02s7}_config2 -name "*stats*"
