@@ -2,22 +2,24 @@
 """Training-throughput benchmark (BASELINE.json metric: training image-pairs/sec at 256x192).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config3|config4|config5]
-                    [--batch B] [--no-graph] [--no-cpu-baseline]
+                    [--batch B] [--no-graph] [--no-cpu-baseline] [--no-secondary]
 For N > 1 launch with `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`:
-one process per GPU, per-GPU batch fixed (weak scaling), gradients averaged with one RCCL
-all-reduce per flat parameter chunk per step.
+one process per GPU, per-GPU batch fixed (weak scaling), gradients averaged with bucketed RCCL
+all-reduces overlapped with backward.
 
 A step = one pass of the hot path over one synthetic batch already resident in HBM: network
-forward(s), fused loss head (values + gradients), backward(s), Adam.  The default workload is
-BASELINE configs[1] (config 2, train_depth_only.py, per-GPU batch 8); config 4 (the 8-GPU DDP
-photometric config, per-GPU batch 8 = 64/8), config 3 (batch 32) and config 5 (640x480, per-GPU
-batch 2 = 16/8) are selectable.  The step is recorded once into a hipGraph and replayed.
+forward(s), fused loss head (values + gradients), backward(s), Adam.  The default workload is the
+metric's pair path, config 4 (train_depth_then_cam_lr.py:123-154,211-355: 2x disp_net + 2x 4-scale
+depth_net, photometric warp loss, per-GPU batch 8 = the 8-GPU shard of global batch 64): 1 unit =
+1 image pair.  Config 2 (BASELINE configs[1], single images) and config 3 (pairs, batch 32) are
+timed after it on rank 0 at N = 1 as the `secondary` object; config 5 is selectable.  The step is
+recorded into hipGraphs and replayed.
 
 Prints ONE JSON line on rank 0 with
   roofline    : the MFMA implicit-GEMM conv family (fwd + dgrad + wgrad): algorithmic FLOPs of the
                 step's convs / their summed HIP-event time, measured live on an instrumented step on
-                the stream the kernels run on, against the fp32 MFMA dense peak (157.3 TFLOP/s,
-                MI355X_MICROARCH.md);
+                the stream the kernels run on, against the dense fp16 MFMA peak / 3 (fp16x3 math);
+                mfma_busy / traffic from the committed rocprofv3 PMC summary of the same workload;
   cpu_baseline: the oracle's PyTorch-CPU fp32 restatement of the same step ("port": TF-1 cannot
                 run here), timed on a bounded sample on this host's cores, rank 0 at N = 1 only.
 """
@@ -184,10 +186,33 @@ def depth_l1_vs_ref(name, N, seed=7):
 
 
 # ---------------------------------------------------------------- CPU baseline (oracle restatement)
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Host threads for the CPU leg: every core this process may run on (sched_getaffinity), capped by an
+    explicit OMP_NUM_THREADS (the GPU box sets it to its per-GPU CPU share; os.cpu_count() there reports the
+    whole machine, and oversubscribing it would understate the CPU path)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        cap = 0
+    return min(n, cap) if cap > 0 else n
+
+
 def cpu_baseline(name, N, budget_s=12.0):
     from oracle import losses as OL
     from oracle import nets as ON
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     H, W = WORKLOADS[name][:2]
     batch = make_batch(name, N, 0)
@@ -229,62 +254,16 @@ def cpu_baseline(name, N, budget_s=12.0):
         if el >= budget_s or n >= 20:
             break
     return dict(value=round(N * n / el, 3), unit="image-pairs/s", cores=threads, kind="port",
+                cpu_model=cpu_model(), host_cpus=os.cpu_count(),
                 sample=f"{n} {name} training steps x {N} samples at {W}x{H}, PyTorch-CPU fp32 restatement "
                        f"(oracle/), {el:.1f}s wall")
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--math", default="fp16x3", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r", "fp16x3"],
-                    help="conv arithmetic (include/tde.h tde_set_conv_math): exact fp32 MFMA, bf16x3 split "
-                         "precision, the fp32-accurate 3-way bf16 split (LDS-staged / register-split) or the "
-                         "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
-    ap.add_argument("--adam-overlap", default="off", choices=["off", "side", "wgrad"],
-                    help="N = 1: run each gradient bucket's Adam as soon as backward finalises it, on its own side "
-                         "stream or on the filter-gradient stream")
-    ap.add_argument("--adam-bucket-mb", type=float, default=16.0)
-    ap.add_argument("--deferred-adam", default="off", choices=["on", "off"],
-                    help="N = 1: run each step's Adam at the start of the next step on a side stream, overlapped with "
-                         "its forward (per-bucket waits; bit-identical updates; every timed step still runs one "
-                         "full Adam).  Measured: config 2 1.1 %% slower, config 4 equal (HBM contention)")
-    ap.add_argument("--wgrad-overlap", default="on", choices=["on", "off"],
-                    help="filter gradients on a side stream, off backward's data-gradient chain (a parallel graph "
-                         "branch; bit-identical results)")
-    ap.add_argument("--net-overlap", default="on", choices=["on", "off"],
-                    help="N = 1, config 4: depth_net's calls on a second stream beside disp_net's (independent "
-                         "programs; one graph per piece, replayed with stream waits; bit-identical results). "
-                         "Measured config 4 605 -> 665 samples/s")
-    ap.add_argument("--sync-bn", action="store_true",
-                    help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
-                         "runs eagerly, RCCL is not captured)")
-    ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
-                    help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+def build_trainer(args, name, N, world, rank):
+    """Trainer for `name` with the benched options (exchange, overlaps); returns (trainer, options dict)."""
     from tf_depth_estimation_amd import train
-    from tf_depth_estimation_amd.program import KernelTimer
-
-    H, W, Nd, gflop_unit, desc = WORKLOADS[args.workload]
-    N = args.batch or Nd
-    from tf_depth_estimation_amd import _lib
-    _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[args.math]), "conv math")
-    tr = make_trainer(args.workload, N)
-    tr.set_batch(*[t.cuda() for t in make_batch(args.workload, N, seed=1000 + rank)])
+    tr = make_trainer(name, N)
+    tr.set_batch(*[t.cuda() for t in make_batch(name, N, seed=1000 + rank)])
     if world > 1:
         if args.ddp == "overlap":
             tr.enable_ddp(world, bucket_mb=args.bucket_mb)
@@ -303,9 +282,14 @@ def main():
                    not args.sync_bn and len(tr.programs()) > 1)
     if net_overlap:
         tr.enable_net_overlap()
-    progs = tr.programs()
+    return tr, dict(deferred=deferred, net_overlap=net_overlap)
 
-    # instrumented eager step: per-family HIP-event times for the roofline (outside the timed region)
+
+def instrumented_step(tr):
+    """One eager step with per-family HIP-event spans on the stream the kernels run on (outside the timed
+    region; the instrumented step runs its programs serially on one stream)."""
+    from tf_depth_estimation_amd.program import KernelTimer
+    progs = tr.programs()
     tr.step_eager()
     tr.flush()       # no update in flight during the instrumented step
     timer = KernelTimer()
@@ -314,26 +298,24 @@ def main():
     tr.step_eager()
     for p in progs:
         p.timer = None
-    fam = timer.totals()
-    conv = [fam[k] for k in ("conv_fwd", "conv_bwd", "conv_dgrad", "conv_wgrad") if k in fam]
-    conv_ms = sum(c[0] for c in conv)
-    conv_flops = sum(c[1] for c in conv)
-    conv_launches = sum(c[2] for c in conv)
+    tr.flush()
+    return timer.totals(), timer.nbytes
 
-    use_graph = not args.no_graph and not args.sync_bn
+
+def timed_steps(tr, steps, warmup, world, rank, use_graph):
     if use_graph:
         tr.capture()
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         tr.step()
         if i % 50 == 49:
-            log(f"[bench] rank {rank} step {i + 1}/{args.steps}")
+            log(f"[bench] rank {rank} step {i + 1}/{steps}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -342,6 +324,69 @@ def main():
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
+    return el
+
+
+def conv_family(fam):
+    conv = [fam[k] for k in ("conv_fwd", "conv_bwd", "conv_dgrad", "conv_wgrad") if k in fam]
+    return sum(c[0] for c in conv), sum(c[1] for c in conv), sum(c[2] for c in conv)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="config4", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the workload's)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--math", default="fp16x3", choices=["fp32", "bf16x3", "bf16x6", "bf16x6r", "fp16x3"],
+                    help="conv arithmetic (include/tde.h tde_set_conv_math): exact fp32 MFMA, bf16x3 split "
+                         "precision, the fp32-accurate 3-way bf16 split (LDS-staged / register-split) or the "
+                         "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary workloads (config 2 and 3 timed after the headline at N = 1)")
+    ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--adam-overlap", default="off", choices=["off", "side", "wgrad"],
+                    help="N = 1: run each gradient bucket's Adam as soon as backward finalises it, on its own side "
+                         "stream or on the filter-gradient stream")
+    ap.add_argument("--adam-bucket-mb", type=float, default=16.0)
+    ap.add_argument("--deferred-adam", default="off", choices=["on", "off"],
+                    help="N = 1: run each step's Adam at the start of the next step on a side stream, overlapped with "
+                         "its forward (per-bucket waits; bit-identical updates; every timed step still runs one "
+                         "full Adam).  Measured: config 2 1.1 %% slower, config 4 equal (HBM contention)")
+    ap.add_argument("--wgrad-overlap", default="on", choices=["on", "off"],
+                    help="filter gradients on a side stream, off backward's data-gradient chain (a parallel graph "
+                         "branch; bit-identical results)")
+    ap.add_argument("--net-overlap", default="on", choices=["on", "off"],
+                    help="config 4: depth_net's calls on a second stream beside disp_net's (independent "
+                         "programs; one graph per piece, replayed with stream waits; bit-identical results). "
+                         "Measured config 4 605 -> 665 samples/s")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
+                         "runs eagerly, RCCL is not captured)")
+    ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
+                    help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from tf_depth_estimation_amd import _api, _lib, variables
+
+    H, W, Nd, gflop_unit, desc = WORKLOADS[args.workload]
+    N = args.batch or Nd
+    _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[args.math]), "conv math")
+    tr, opts = build_trainer(args, args.workload, N, world, rank)
+    fam, fam_bytes = instrumented_step(tr)
+    conv_ms, conv_flops, conv_launches = conv_family(fam)
+    use_graph = not args.no_graph and not args.sync_bn
+    el = timed_steps(tr, args.steps, args.warmup, world, rank, use_graph)
     loss = tr.total_loss()
     tr.flush()       # deferred Adam: apply the last step's owed update (outside the timed region)
 
@@ -353,8 +398,8 @@ def main():
             # useful work
             per = 6 if args.math in ("bf16x6", "bf16x6r") else 3
             ins = "v_mfma_f32_16x16x32_f16" if args.math == "fp16x3" else "v_mfma_f32_16x16x32_bf16"
-            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> + halo_conv_kernel (conv fwd+dgrad+wgrad, "
-                           f"{args.math}: {per} x {ins} per fp32 product)")
+            kernel_name = (f"igemmx_kernel<{_lib.CONV_MATH[args.math]},...> + halo_conv_kernel + hwh_kernel (conv "
+                           f"fwd+dgrad+wgrad, {args.math}: {per} x {ins} per fp32 product)")
             peak = round(BF16_MFMA_PEAK / per, 1)
             peak_note = f"dense bf16/fp16 MFMA peak {BF16_MFMA_PEAK} TFLOP/s / {per} MFMAs per fp32 product"
         else:
@@ -362,6 +407,7 @@ def main():
             peak_note = "dense fp32 MFMA peak"
         value = world * N * args.steps / el
         achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        dtype = {"fp16x3": "fp16x3", "fp32": "f32"}.get(args.math, args.math)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -373,7 +419,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": dtype,
+            "dtype_note": ("fp32 tensors end to end; the convolutions split each fp32 operand into scaled fp16 hi/lo "
+                           "parts and run 3 fp16 MFMAs per product with fp32 accumulation (fp32-class accuracy, "
+                           "DESIGN.md §2); BatchNorm, heads, loss head and Adam compute in fp32 (fp64 reductions)"
+                           if args.math == "fp16x3" else f"conv math {args.math}"),
             "data": "synthetic (SURVEY.md §8d shapes/distributions); random-init Glorot weights",
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
@@ -381,9 +431,10 @@ def main():
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
                        "wgrad_overlap": args.wgrad_overlap == "on",
                        "adam_overlap": args.adam_overlap if world == 1 else "off",
-                       "deferred_adam": deferred,
-                       "net_overlap": net_overlap,
-                       "unit_note": "1 unit = 1 training sample (an image pair; config 2/5 train on one image of it)"},
+                       "deferred_adam": opts["deferred"],
+                       "net_overlap": opts["net_overlap"],
+                       "unit_note": "1 unit = 1 training sample: an image pair (configs 3/4); configs 2/5 train on "
+                                    "one image of it"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "peak_note": peak_note, "traffic": None,
@@ -395,13 +446,46 @@ def main():
         }
         tr_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.math}_b{N}.json")
         if os.path.exists(tr_path):
-            # HBM bytes from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload (scripts/pmc.sh,
-            # a separate profiled run: counters cannot be read inside this timed process)
+            # HBM bytes and MFMA-pipe busy from rocprofv3 --pmc passes of this workload (scripts/pmc_step.sh, a
+            # separate profiled run: counters cannot be read inside this timed process)
             with open(tr_path) as fh:
-                conv_t = json.load(fh)["families"].get("conv", {})
-            out["roofline"]["traffic"] = conv_t.get("hbm_bytes_per_step")
-            out["roofline"]["traffic_unit"] = "bytes per step, conv family (igemm + split-K reduce)"
-            out["roofline"]["traffic_source"] = os.path.relpath(tr_path, ROOT)
+                pm = json.load(fh)
+            conv_t = pm["families"].get("conv", {})
+            rf = out["roofline"]
+            rf["traffic"] = conv_t.get("hbm_bytes_per_step")
+            rf["traffic_unit"] = "bytes per step, conv family (igemm + halo + split-K reduce)"
+            rf["traffic_algorithmic"] = sum(v for k, v in fam_bytes.items() if k.startswith("conv_"))
+            if "mfma_busy" in conv_t:
+                rf["mfma_busy"] = round(conv_t["mfma_busy"], 4)
+                rf["mfma_busy_note"] = ("SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs) over the conv "
+                                        "family's dispatches (includes the 2 redundant fp16 products of fp16x3 and "
+                                        "tile padding)")
+                cyc = conv_t.get("gui_active_cycles_per_step")
+                if cyc and conv_t.get("hbm_bytes_per_step"):
+                    rf["hbm_gbs"] = round(conv_t["hbm_bytes_per_step"] / (cyc / 2.1e9) / 1e9, 1)
+                    rf["hbm_gbs_note"] = "PMC bytes / conv-family busy cycles at an assumed 2.1 GHz"
+            rf["traffic_source"] = os.path.relpath(tr_path, ROOT)
+        if world == 1 and not args.no_secondary:
+            sec = {}
+            for name in ("config2", "config3"):
+                if name == args.workload:
+                    continue
+                log(f"[bench] secondary workload {name} ...")
+                del tr
+                _api.clear_programs()
+                variables.get_store().reset()
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+                tr, o2 = build_trainer(args, name, WORKLOADS[name][2], 1, 0)
+                f2, _ = instrumented_step(tr)
+                cm, cf, _ = conv_family(f2)
+                e2 = timed_steps(tr, args.steps, args.warmup, 1, 0, use_graph)
+                n2 = WORKLOADS[name][2]
+                sec[name] = {"value": round(n2 * args.steps / e2, 3), "unit": "image-pairs/s",
+                             "ms_per_step": round(e2 / args.steps * 1e3, 4), "per_gpu_batch": n2,
+                             "workload": WORKLOADS[name][4],
+                             "conv_tflops": round(cf / (cm * 1e-3) / 1e12, 3) if cm > 0 else None}
+            out["secondary"] = sec
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] timing CPU baseline ...")
             out["cpu_baseline"] = cpu_baseline(args.workload, N)

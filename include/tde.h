@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 5
+#define TDE_ABI_VERSION 6
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
@@ -182,7 +182,8 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
 /* ---------------------------------------------------------------- few-channel heads
  * slim.conv2d(..., normalizer_fn=None, activation_fn=sigmoid|None) with bias: disp heads
  * (nets_optflow_depth.py:122-144: DISP_SCALING*sigmoid(.) [+MIN_DISP]), flow heads (nets_depth.py:169-191),
- * mask heads (nets_optflow_depth.py:193-198) and pose/pred 1x1 (:181).  K <= 8.
+ * mask heads (nets_optflow_depth.py:193-198), pose/pred 1x1 (:181) and the 3-channel linear disp heads of
+ * nets.py:122-144.  K in {1, 2, 3, 6}.
  * act: 0 linear (y = z), 1 y = scale*sigmoid(z) + offset.  Backward takes y (not z). */
 size_t tde_head_workspace_size(const tde_conv_desc_t* d);
 int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias,
@@ -220,6 +221,15 @@ int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,
                float* dbeta, int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes,
                void* stream);
+
+/* BN-free conv / conv2d_transpose layers with bias + ReLU (the BN-free disp_net of
+ * nets_optflow_depth_pairtest.py:76-147: normalizer_fn commented out at :83-84, so slim.conv2d adds biases):
+ * forward = tde_conv2d_fwd_bias_act / tde_deconv2d_fwd_bias_act with the trained weights and biases; backward:
+ * dz = dy * relu'(y) written dense [M][C] (y, dy are channel views of the layer's output and its gradient),
+ * dbias (+)= sum_rows dz (fp64, fixed order), dz_absmax as tde_bn_bwd.  Workspace: tde_bn_workspace_size(M, C). */
+int tde_bias_relu_bwd(int M, int C, const float* y, int y_cstride, int y_coff, const float* dy, int dy_cstride,
+                      int dy_coff, int relu, float* dz, float* dbias, int accumulate_dbias, float* dz_absmax,
+                      void* ws, size_t ws_bytes, void* stream);
 
 /* SyncBN (BatchNorm over the batch of ALL data-parallel replicas), in two phases around
  * the caller's all-reduce of `sums` (fp64 [2][C]):

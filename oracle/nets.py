@@ -7,6 +7,8 @@ product's layer-program builder so that a mistake in one does not hide in the ot
   * `depth_net`           nets_optflow_depth.py:151-276  (2 scales) and
                           nets_optflow_depth_pairtest.py:151-276 (4 scales, BN default decay 0.999)
   * `disp_net_depthflow`  nets_depth.py:76-199           (BN decay 0.999, DISP_SCALING 10, MIN_DISP 0.001)
+  * `disp_net_sfm`        nets.py:76-147                 (BN decay 0.999, 3-channel linear heads)
+  * `disp_net(bn=False)`  nets_optflow_depth_pairtest.py:76-147 (BN-free: conv + bias + ReLU)
 
 Parameters live in a flat dict keyed by TF variable names:
   `<scope>/<layer>/weights`, `<scope>/<layer>/biases`, `<scope>/<layer>/BatchNorm/beta`; BN moving
@@ -139,7 +141,7 @@ def _decoder(c, H, W, cnv1b, cnv2b, cnv3b, cnv4b, cnv5b, cnv6b, cnv7b, scale, mi
 
 
 def disp_net(P, tgt_image, is_training=True, scope="depth_net", bn=True, decay=0.99,
-             disp_scaling=4.0, min_disp=0.0):
+             disp_scaling=4.0, min_disp=0.0, head_ch=1, head_act="sigmoid"):
     """nets_optflow_depth.disp_net (nets_optflow_depth.py:76-147).  `bn=False` gives the BN-free
     variant of nets_optflow_depth_pairtest.py:77,83-85 (slim then adds biases)."""
     H, W = tgt_image.shape[1], tgt_image.shape[2]
@@ -147,7 +149,14 @@ def disp_net(P, tgt_image, is_training=True, scope="depth_net", bn=True, decay=0
     feats = _encoder(c, tgt_image)
     cnv7 = c.conv(feats[5], 512, 3, 2, "cnv7")
     cnv7b = c.conv(cnv7, 512, 3, 1, "cnv7b")
-    return _decoder(c, H, W, *feats, cnv7b, disp_scaling, min_disp)
+    return _decoder(c, H, W, *feats, cnv7b, disp_scaling, min_disp, head_ch=head_ch, head_act=head_act)
+
+
+def disp_net_sfm(P, tgt_image, is_training=True, scope="depth_net"):
+    """nets.disp_net (nets.py:76-147): the same encoder / decoder with 3-channel LINEAR disparity heads
+    (activation_fn=None, normalizer_fn=None, :122-144; DISP_SCALING / MIN_DISP are not applied), 3-channel
+    bilinear up-samplings in the concats, slim's default BN decay 0.999 (:77)."""
+    return disp_net(P, tgt_image, is_training, scope, bn=True, decay=0.999, head_ch=3, head_act=None)
 
 
 def depth_net(P, tgt_image, is_training=True, scope="depth_cam_net", levels=4, decay=None,

@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--label", default="")
+    ap.add_argument("--sq", default=None, help="dir of a third pass with SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE")
     a = ap.parse_args()
     fetch = load(a.fetch, "FETCH_SIZE")
     write = load(a.write, "WRITE_SIZE")
@@ -69,10 +70,40 @@ def main():
         f["launches_per_step"] += launches
     for f in fams.values():
         f["hbm_bytes_per_step"] = f["read_bytes_per_step"] + f["write_bytes_per_step"]
+    if a.sq:
+        # MFMA pipe busy: SQ_VALU_MFMA_BUSY_CYCLES counts SIMD-cycles an MFMA occupies (16 per
+        # v_mfma_f32_16x16x32_f16, MI355X_MICROARCH.md cycle table), summed over all 1024 SIMDs; GRBM_GUI_ACTIVE is
+        # the dispatch's GPU-busy cycles summed over the 8 XCDs.  busy = MFMA cycles / (GUI cycles / 8 * 1024)
+        mb = load(a.sq, "SQ_VALU_MFMA_BUSY_CYCLES")
+        gui = load(a.sq, "GRBM_GUI_ACTIVE")
+        sqb = load(a.sq, "SQ_BUSY_CYCLES")
+        acc = {}
+        for name in set(mb) | set(gui):
+            fam = family(name)
+            m, g = acc.get(fam, (0.0, 0.0))
+            acc[fam] = (m + mb.get(name, (0.0, 0))[0], g + gui.get(name, (0.0, 0))[0])
+        for fam, (m, g) in acc.items():
+            f = fams.setdefault(fam, {})
+            f["mfma_busy_cycles_per_step"] = m / a.steps
+            f["gui_active_cycles_per_step"] = g / 8.0 / a.steps
+            f["mfma_busy"] = m / (g / 8.0 * 1024.0) if g > 0 else None
+        per_kernel = []
+        for name in mb:
+            g = gui.get(name, (0.0, 0))[0]
+            if g > 0:
+                per_kernel.append((name, mb[name][0] / (g / 8.0 * 1024.0), g / 8.0 / a.steps, mb[name][1] / a.steps,
+                                   sqb.get(name, (0.0, 0))[0] / a.steps))
+        per_kernel.sort(key=lambda r: -r[2])
+        top = [{"kernel": n[:120], "mfma_busy": round(b, 4), "gui_cycles_per_step": round(c), "launches_per_step": l,
+                "sq_busy_cycles_per_step": round(q)} for n, b, c, l, q in per_kernel[:40]]
     out = {"label": a.label, "steps": a.steps,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950 "
                      "16-B/lane read calibration, MI355X_MICROARCH.md §HBM), KB -> bytes, summed per family / steps",
            "families": fams}
+    if a.sq:
+        out["mfma_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (own pass): "
+                              "mfma_busy = MFMA SIMD-cycles / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)")
+        out["top_kernels_by_cycles"] = top
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

@@ -100,3 +100,32 @@ def test_product_host_logic_matches_oracle(tmp_path):
     np.testing.assert_array_equal(dl.get_multi_scale_intrinsics(K, 4, np.float32(8 / 3), np.float32(0.5)),
                                   OD.get_multi_scale_intrinsics(K, 4, np.float32(8 / 3), np.float32(0.5)))
     np.testing.assert_array_equal(_csv_record("1, 2,,4\n", 4, ","), OD.decode_csv_record("1, 2,,4\n", 4))
+
+
+def _die(code):
+    import os
+    os._exit(code)
+
+
+def test_dead_decode_worker_raises_not_hangs():
+    """a decode worker that dies mid-task (OOM kill, decoder crash) must surface as an error in the
+    loader instead of blocking the producer forever (multiprocessing.Pool replaces the worker but never
+    completes its task)."""
+    import multiprocessing as mp
+    import threading
+    import types
+    from tf_depth_estimation_amd.imageselect_Dataloader_optflow import DataLoader
+    pool = mp.get_context("spawn").Pool(1)
+    try:
+        fake = types.SimpleNamespace(_task_timeout=60.0, _stop=threading.Event(), _worker_procs=list(pool._pool))
+        fu = pool.apply_async(_die, (3,))
+        with pytest.raises(RuntimeError, match="exited with code 3"):
+            DataLoader._await(fake, fu)
+        fake = types.SimpleNamespace(_task_timeout=0.5, _stop=threading.Event(), _worker_procs=[])
+        import time
+        fu = pool.apply_async(time.sleep, (5,))
+        with pytest.raises(TimeoutError):
+            DataLoader._await(fake, fu)
+    finally:
+        pool.terminate()
+        pool.join()

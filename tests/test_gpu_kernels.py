@@ -396,6 +396,11 @@ HEAD_CASES = [
     (2, 150, 130, 32, 2, 5, 0, 1.0, 0.0, 32, 0),     # ragged rows and columns, 2 channel groups (dgrad)
     (1, 190, 200, 64, 1, 3, 1, 10.0, 0.001, 68, 4),  # 4 channel groups, offset view, ragged
     (2, 130, 160, 32, 1, 3, 0, 1.0, 0.0, 32, 0),     # disp2-like
+    # 3-channel LINEAR disparity heads of nets.disp_net (nets.py:122-144: activation_fn=None, no BN, no scaling)
+    (2, 24, 32, 128, 3, 3, 0, 1.0, 0.0, 128, 0),     # disp4 at 96x128 input
+    (2, 48, 64, 64, 3, 3, 0, 1.0, 0.0, 64, 0),       # disp3
+    (2, 96, 128, 32, 3, 3, 0, 1.0, 0.0, 32, 0),      # disp2 (direct kernels: K = 3 is never tiled)
+    (1, 192, 256, 16, 3, 3, 0, 1.0, 0.0, 20, 4),     # disp1, offset view
 ]
 
 
@@ -470,9 +475,35 @@ def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     close(yi[:, yco:yco + C], yir, what="bn infer")
 
 
+@pytest.mark.parametrize("M,C,ycs,yco,relu,acc", [(8 * 96 * 128, 32, 68, 32, 1, 0), (32, 512, 1024, 512, 1, 1),
+                                                  (8 * 12 * 16, 256, 256, 0, 1, 1), (2049, 20, 20, 0, 0, 0),
+                                                  (2 * 192 * 256, 16, 20, 0, 1, 1)])
+def test_bias_relu_bwd(L, M, C, ycs, yco, relu, acc):
+    """BN-free conv layers (nets_optflow_depth_pairtest.py:83-85): dz = dy * relu'(y), dbias (+)= sum dz,
+    max|dz| bound -- against the float64 formula (exact: a mask and fp64 sums)."""
+    lib = L.load()
+    st = L.stream_ptr()
+    y = torch.relu(rnd(M, ycs, seed=40))
+    y[::7] = 0.0
+    dy = rnd(M, ycs, seed=41)
+    db0 = rnd(C, seed=42)
+    gy, gdy = dev(y), dev(dy)
+    dz = torch.empty(M, C, device="cuda")
+    db = dev(db0)
+    amax = torch.zeros(L.BOUND_SLOTS, device="cuda")
+    ws = torch.zeros(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
+    L.check(lib.tde_bias_relu_bwd(M, C, L.ptr(gy), ycs, yco, L.ptr(gdy), ycs, yco, relu, L.ptr(dz), L.ptr(db), acc,
+                                  L.ptr(amax), L.ptr(ws), ws.numel() * 4, st))
+    yv, gv = y[:, yco:yco + C], dy[:, yco:yco + C]
+    ref = torch.where(yv > 0, gv, torch.zeros_like(gv)) if relu else gv
+    close(dz, ref, tol=0.0, what="bias_relu dz")
+    close(db, ref.sum(0) + (db0 if acc else 0), tol=1e-6, what="dbias")
+    assert amax.max().item() == dz.abs().max().item()
+
+
 @pytest.mark.parametrize("kind,N,H,W,C,OH,OW", [("nearest", 2, 4, 4, 8, 3, 4), ("nearest", 1, 16, 20, 4, 15, 20),
                                                  ("bilinear", 2, 24, 32, 1, 48, 64), ("bilinear", 2, 6, 8, 2, 12, 16),
-                                                 ("bilinear", 1, 5, 7, 1, 10, 14)])
+                                                 ("bilinear", 1, 5, 7, 1, 10, 14), ("bilinear", 2, 24, 32, 3, 48, 64)])
 def test_resize_fwd_bwd(L, kind, N, H, W, C, OH, OW):
     lib = L.load()
     st = L.stream_ptr()

@@ -260,3 +260,102 @@ def test_config2_train_step_parity(conv_math):
     for name in p0:
         err = (tr.chunk.view(name).double().cpu() - params[name]).abs().max().item()
         assert err <= 1e-3 * 2e-4 + 1e-7, f"{name}: adam update err {err:.2e}"
+
+
+def test_nets_sfm_disp_net_forward_parity(conv_math):
+    """nets.disp_net (nets.py:76-147, refine_depth.py:16): 3-channel LINEAR disparity heads, 3-channel
+    bilinear up-samplings in the concats (64+64+3, 32+32+3, 16+3), BN decay 0.999; training and inference."""
+    from tf_depth_estimation_amd import nets, variables
+    x = images(2, 64, 96, 3, 20)
+    with variables.variable_scope("model"):
+        outs, ep = nets.disp_net(x.cuda(), is_training=True)
+    assert [tuple(o.shape) for o in outs] == [(2, 64, 96, 3), (2, 32, 48, 3), (2, 16, 24, 3), (2, 8, 12, 3)]
+    chunk = ep["program"].chunk
+    assert tuple(chunk.view("model/depth_net/disp1/weights").shape) == (3, 3, 16, 3)
+    assert tuple(chunk.view("model/depth_net/icnv3/weights").shape) == (3, 3, 131, 64)
+    P = oracle_params_from(chunk, "")
+    for st in P.bn.values():
+        st.moving_mean.zero_(); st.moving_variance.fill_(1.0)
+    ref = ON.disp_net_sfm(P, x.double(), True, scope="model/depth_net")
+    tol = OUT_TOL_BF16X3 if conv_math == 1 else OUT_TOL
+    for i, (o, r) in enumerate(zip(outs, ref)):
+        e = rel_err(o, r)
+        assert e <= tol, f"disp{i + 1}: rel err {e:.2e}"
+    for bn_name, st in P.bn.items():     # decay 0.999 moving averages
+        m, v = chunk.moving(bn_name)
+        assert rel_err(m, st.moving_mean) <= tol, bn_name
+        assert rel_err(v, st.moving_variance) <= tol, bn_name
+    with variables.variable_scope("model", reuse=True):
+        outs_i, _ = nets.disp_net(x.cuda(), is_training=False)
+    P = oracle_params_from(chunk, "")
+    ref_i = ON.disp_net_sfm(P, x.double(), False, scope="model/depth_net")
+    for i, (o, r) in enumerate(zip(outs_i, ref_i)):
+        assert rel_err(o, r) <= tol, f"inference disp{i + 1}"
+
+
+def test_nets_sfm_disp_net_gradients():
+    """Linear functional of the 3-channel-head net's outputs: whole-gradient criterion (BN backward)."""
+    from tf_depth_estimation_amd import nets, variables
+    x = images(2, 64, 96, 3, 21)
+    xg = x.cuda().requires_grad_(True)
+    with variables.variable_scope("model"):
+        outs, ep = nets.disp_net(xg, is_training=True)
+    chunk = ep["program"].chunk
+    chunk.grad.zero_()
+    g = torch.Generator().manual_seed(22)
+    R = [torch.randn(o.shape, generator=g, dtype=torch.float64) for o in outs]
+    sum((o * r.float().cuda()).sum() for o, r in zip(outs, R)).backward()
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        P = oracle_params_from(chunk, "", dt)
+        for st in P.bn.values():
+            st.moving_mean.zero_(); st.moving_variance.fill_(1.0)
+        xr = x.to(dt).requires_grad_(True)
+        ref = ON.disp_net_sfm(P, xr, True, scope="model/depth_net")
+        sum((o * r.to(dt)).sum() for o, r in zip(ref, R)).backward()
+        grads[dt] = dict({k: v.grad for k, v in P.vars.items()}, input=xr.grad)
+    gpu = dict({k: chunk.grad_view(k) for k in chunk.names()}, input=xg.grad)
+    check_grads_global(gpu, grads[torch.float64], grads[torch.float32], GRAD_FACTOR[4])
+    # the heads' own tensors (well conditioned: linear heads right at the loss) per tensor
+    for n in [k for k in grads[torch.float64] if "/disp" in k]:
+        assert rel_err(gpu[n], grads[torch.float64][n]) <= 1e-3, n
+
+
+def test_pairtest_bn_free_disp_net_parity():
+    """nets_optflow_depth_pairtest.disp_net (:76-147): normalizer commented out (:83-84), every layer is
+    conv + bias + ReLU.  Outputs at 1e-4 and EVERY parameter gradient per tensor (no BatchNorm backward
+    cancellation here, so the per-tensor bar applies)."""
+    from tf_depth_estimation_amd import nets_optflow_depth_pairtest as npt
+    from tf_depth_estimation_amd import variables
+    x = images(2, 64, 96, 3, 23)
+    xg = x.cuda().requires_grad_(True)
+    with variables.variable_scope("model"):
+        outs, ep = npt.disp_net(xg, is_training=True)
+    chunk = ep["program"].chunk
+    assert not chunk.bn_offsets, "BN-free net must own no BatchNorm variables"
+    assert "model/depth_net/cnv1/biases" in chunk.offsets and "model/depth_net/upcnv1/biases" in chunk.offsets
+    # non-zero biases so the bias path is exercised (slim initialises them to 0)
+    gb = torch.Generator().manual_seed(24)
+    with torch.no_grad():
+        for n in chunk.names():
+            if n.endswith("/biases"):
+                chunk.view(n).copy_(0.05 * torch.randn(chunk.view(n).shape, generator=gb))
+    with variables.variable_scope("model", reuse=True):
+        outs, _ = npt.disp_net(xg, is_training=True)
+    chunk.grad.zero_()
+    g = torch.Generator().manual_seed(25)
+    R = [torch.randn(o.shape, generator=g, dtype=torch.float64) for o in outs]
+    sum((o * r.float().cuda()).sum() for o, r in zip(outs, R)).backward()
+    grads, refs = {}, {}
+    for dt in (torch.float64, torch.float32):
+        P = oracle_params_from(chunk, "", dt)
+        xr = x.to(dt).requires_grad_(True)
+        ref = ON.disp_net(P, xr, True, scope="model/depth_net", bn=False)
+        refs[dt] = ref
+        sum((o * r.to(dt)).sum() for o, r in zip(ref, R)).backward()
+        grads[dt] = dict({k: v.grad for k, v in P.vars.items()}, input=xr.grad)
+    for i, (o, r) in enumerate(zip(outs, refs[torch.float64])):
+        e = rel_err(o, r)
+        assert e <= OUT_TOL, f"disp{i + 1}: rel err {e:.2e}"
+    gpu = dict({k: chunk.grad_view(k) for k in chunk.names()}, input=xg.grad)
+    check_grads(gpu, grads[torch.float64], grads[torch.float32])

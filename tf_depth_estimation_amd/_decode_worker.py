@@ -52,10 +52,13 @@ def read_cam_proj(cam_path, proj_path):
     return cam, pv[:-1].reshape(2, 4, 4), pv[-1]
 
 
-def load_sample(shm_name, off, cap, img_path, lab_off, lab_count, lab_path, cam_path, proj_path):
+def load_sample(shm_name, off, cap, img_path, lab_off, lab_count, lab_path, cam_path, proj_path, drop=()):
     """One sample: the image into the segment at `off` (if it fits `cap` bytes), the raw float32 label
-    (lab_count values) at `lab_off`, and the parsed camera / projection files.
+    (lab_count values) at `lab_off`, and the parsed camera / projection files.  `drop`: segments the loader
+    has unlinked (a slot outgrew them); this worker closes its handles on them first.
     Returns (h, w, the image if it did not fit else None, cam, projs, m_scale)."""
+    if drop:
+        detach(drop)
     h, w, big = decode_into(shm_name, off, cap, img_path)
     v = np.fromfile(lab_path, dtype="<f4")
     if v.size != lab_count:

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
@@ -112,6 +112,8 @@ _SIGS = {
                                  P, c_size_t, P]),
     "tde_bn_fwd_infer": (c_int, [c_int, c_int, P, P, c_float, P, P, P, c_int, c_int, c_int, P]),
     "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, P, c_size_t, P]),
+    "tde_bias_relu_bwd": (c_int, [c_int, c_int, P, c_int, c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_size_t,
+                                  P]),
     "tde_bn_sums": (c_int, [c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P]),
     "tde_bn_fwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, c_float, c_float, c_int, P, P, P, P, P,
                                      c_int, c_int, c_int, P]),
@@ -201,6 +203,17 @@ def dedicated_stream():
         raise TdeError(f"hipStreamCreateWithFlags failed ({rc})")
     _own_streams.append(s)
     return torch.cuda.ExternalStream(s.value)
+
+
+def owned_stream(owner, name):
+    """A dedicated stream (dedicated_stream) cached on `owner` under `name`: created once per owner and role, so
+    re-enabling an overlap or re-capturing a step never allocates another HIP stream, and no two roles ever share
+    one (the pool aliasing dedicated_stream avoids)."""
+    cache = owner.__dict__.setdefault("_tde_streams", {})
+    st = cache.get(name)
+    if st is None:
+        st = cache[name] = dedicated_stream()
+    return st
 
 
 def call(name, *args):

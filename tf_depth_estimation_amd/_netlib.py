@@ -120,17 +120,19 @@ def check_sizes(H, W, levels=4):
     return hs, ws
 
 
-def disp_net_spec(H, W, cin, scope="depth_net", decay=0.99, scale=4.0, offset=0.0, bn=True):
-    """nets_optflow_depth.disp_net (nets_optflow_depth.py:76-147)."""
+def disp_net_spec(H, W, cin, scope="depth_net", decay=0.99, scale=4.0, offset=0.0, bn=True, head_ch=1, head_act=1):
+    """nets_optflow_depth.disp_net (nets_optflow_depth.py:76-147); bn=False: the BN-free variant of
+    nets_optflow_depth_pairtest.py:76-147 (conv + bias + ReLU); head_ch=3, head_act=0: nets.disp_net
+    (nets.py:76-147, 3-channel linear disparity heads, BN decay 0.999)."""
     hs, ws = check_sizes(H, W)
     spec = NetSpec(scope, H, W, cin)
-    dec = Decoder(spec, hs, ws, "", 1, 4)
+    dec = Decoder(spec, hs, ws, "", head_ch, 4)
     feats = build_encoder(spec, dec.skip_slots(4), decay, bn=bn)
     cnv7 = spec.dense("cnv7", hs[7], ws[7], 512)
     spec.add(ConvBN("cnv7", feats["cnv6b"], cnv7, 512, 3, 2, bn=bn, decay=decay))
     cnv7b = spec.dense("cnv7b", hs[7], ws[7], 512)
     spec.add(ConvBN("cnv7b", cnv7, cnv7b, 512, 3, 1, bn=bn, decay=decay))
-    spec.outputs = build_decoder(spec, dec, feats, cnv7b, H, W, hs, ws, decay, 1, 1, scale, offset, bn=bn)
+    spec.outputs = build_decoder(spec, dec, feats, cnv7b, H, W, hs, ws, decay, head_ch, head_act, scale, offset, bn=bn)
     spec.end_points = feats
     return spec
 

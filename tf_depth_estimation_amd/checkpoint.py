@@ -383,6 +383,11 @@ class Saver:
         from . import variables
         out = {}
         for ch in variables.get_store().chunks.values():
+            # a deferred-Adam trainer may still owe this chunk the last step's update (Trainer.flush): apply it
+            # before the variables are read or overwritten
+            fl = getattr(ch, "pending_flush", None)
+            if fl is not None:
+                fl()
             out.update(ch.state_dict())
             if self.optimizer:
                 for n in ch.names():

@@ -434,6 +434,68 @@ __global__ void __launch_bounds__(256) bn_fold_kernel(long total, int cin, int K
   }
 }
 
+// BN-free conv / deconv layers (nets_optflow_depth_pairtest.py:76-147: normalizer_fn commented out at :83-84,
+// so slim adds biases and applies ReLU): dz = dy * relu'(y) written dense [M][C] (the conv backward's gradient
+// operand), per-chunk fp64 bias sums part[chunk][C], max|dz| into the operand bound.  Grid (row chunk, group of
+// 16 channel quads) as bn_part_kernel.
+__global__ void __launch_bounds__(256) bias_relu_part_kernel(int M, int C, const float* y, int ycs, int yco,
+                                                             const float* dy, int dycs, int dyco, int relu,
+                                                             int rows_per_chunk, float* dz, double* part, float* amax) {
+  __shared__ double sh[2][256 * 4];
+  const int q0 = blockIdx.y * 16;
+  const int nq = min(16, C / 4 - q0);
+  const int ty_n = 256 / nq;
+  const int tx = threadIdx.x % nq, ty = threadIdx.x / nq;
+  const int c = 4 * (q0 + tx);
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  float mx = 0.f;
+  const int r0 = blockIdx.x * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  if (ty < ty_n) {
+    for (int rb = r0 + ty; rb < r1; rb += 64 * ty_n) {
+      const int rend = min(r1, rb + 64 * ty_n);
+      float f0[4] = {0, 0, 0, 0};
+#pragma unroll 8
+      for (int r = rb; r < rend; r += ty_n) {
+        const f4 yv = *reinterpret_cast<const f4*>(y + (long)r * ycs + yco + c);
+        const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = (!relu || yv[j] > 0.f) ? gv[j] : 0.f;
+          f0[j] += o[j];
+          mx = fmaxf(mx, fabsf(o[j]));
+        }
+        *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s0[j] += f0[j];
+    }
+  }
+  rowlane_combine(s0, s1, nq, ty_n, &sh[0][0]);
+  if (ty == 0) {
+    double* o = part + (long)blockIdx.x * C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[c + j] = s0[j];
+  }
+  block_absmax_to(mx, amax);
+}
+
+// dbias[c] (+)= sum over the chunk partials in chunk order (fixed order: deterministic).
+__global__ void __launch_bounds__(256) bias_sum_kernel(int C, int nparts, const double* part, float* dbias, int acc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double a[4] = {0, 0, 0, 0};
+  int p = 0;
+  for (; p + 3 < nparts; p += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += part[(long)(p + u) * C + c];
+  }
+  for (; p < nparts; ++p) a[0] += part[(long)p * C + c];
+  const double s = (a[0] + a[1]) + (a[2] + a[3]);
+  dbias[c] = acc ? dbias[c] + (float)s : (float)s;
+}
+
 int ew_grid(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -631,6 +693,24 @@ int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                      dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
+  return tde_launch_status();
+}
+
+int tde_bias_relu_bwd(int M, int C, const float* y, int y_cstride, int y_coff, const float* dy, int dy_cstride,
+                      int dy_coff, int relu, float* dz, float* dbias, int accumulate_dbias, float* dz_absmax, void* ws,
+                      size_t ws_bytes, void* stream) {
+  TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && y && dy && dz && dbias);
+  TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && dy_cstride % 4 == 0 &&
+                dy_coff % 4 == 0 && dy_coff + C <= dy_cstride);
+  TDE_CHECK_ARG(tde_aligned16(y) && tde_aligned16(dy) && tde_aligned16(dz));
+  if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const BnChunks pp = bn_chunk_plan(M, C, 1);
+  double* part = reinterpret_cast<double*>(tde_ws_body(ws));
+  hipLaunchKernelGGL(bias_relu_part_kernel, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, y, y_cstride, y_coff,
+                     dy, dy_cstride, dy_coff, relu, pp.rows_per_chunk, dz, part, dz_absmax);
+  hipLaunchKernelGGL(bias_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, pp.chunks, part, dbias,
+                     accumulate_dbias);
   return tde_launch_status();
 }
 

@@ -1562,6 +1562,49 @@ static bool bn_ok(const tde_bn_train_t* bn, int C) {
 
 }  // namespace
 
+// Gradient-operand bound for fp16x3 (conv math 4) when the caller passes none: the split scales each operand by
+// a power of two from its bound, and an unscaled gradient (|dy| ~ 1e-6) would keep only ~2^-25 absolute precision.
+// One pre-pass (16 blocks, each the max|.| of a strided share of the view into its own slot: no atomics) writes
+// the bound into the last 256 bytes of the caller's workspace, past everything the conv plans use (every
+// workspace query includes them: with_bound_scratch).
+static size_t with_bound_scratch(size_t n) { return (n + 255) / 256 * 256 + 256; }
+
+__global__ void __launch_bounds__(256) operand_absmax_kernel(long quads, int cq, const float* p, int cs, int co,
+                                                             float* out) {
+  __shared__ float sm[4];
+  float m = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < quads; i += 256L * gridDim.x) {
+    const long r = i / cq;
+    const int q = (int)(i - r * cq);
+    const f4 v = *reinterpret_cast<const f4*>(p + r * cs + co + 4 * q);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+
+// db = *d, with the gradient operand's bound (view 1: y of d; view 0: x of d) computed when math 4 needs one
+// and the caller gave none.
+static int bound_grad_operand(const tde_conv_desc_t* d, tde_conv_desc_t& db, int yview, const float* g, void* ws,
+                              size_t ws_bytes, void* stream) {
+  db = *d;
+  const float* have = yview ? d->y_absmax : d->x_absmax;
+  if (g_conv_math != 4 || have != nullptr) return TDE_OK;
+  if (!ws || ws_bytes < 256 + 64 || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  float* slot = reinterpret_cast<float*>(static_cast<char*>(ws) + ((ws_bytes - 256) & ~(size_t)15));
+  const long rows = yview ? (long)d->N * d->OH * d->OW : (long)d->N * d->H * d->W;
+  const int C = yview ? d->K : d->C;
+  const int cs = yview ? d->y_cstride : d->x_cstride, co = yview ? d->y_coff : d->x_coff;
+  static_assert(TDE_BOUND_SLOTS == 16, "one pre-pass block per bound slot");
+  hipLaunchKernelGGL(operand_absmax_kernel, dim3(TDE_BOUND_SLOTS), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     rows * (C / 4), C / 4, g, cs, co, slot);
+  if (yview) db.y_absmax = slot; else db.x_absmax = slot;
+  return tde_launch_status();
+}
+
 extern "C" {
 
 int tde_set_conv_math(int mode) {
@@ -1594,13 +1637,15 @@ int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const i
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op) {
   // op 3 = forward + batch norm + ReLU (tde_conv2d_fwd_bn)
   if (!desc_ok(d) || op < 0 || op > 3) return 0;
-  return plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_FWD : (op == 1 ? MODE_DGRAD : MODE_WGRAD), op == 3);
+  return with_bound_scratch(
+      plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_FWD : (op == 1 ? MODE_DGRAD : MODE_WGRAD), op == 3));
 }
 
 size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op) {
   // deconv fwd = DGRAD, bwd_data = FWD, bwd_filter = WGRAD of the virtual conv; op 3 = fwd + BN + ReLU
   if (!desc_ok(d) || op < 0 || op > 3) return 0;
-  return plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_DGRAD : (op == 1 ? MODE_FWD : MODE_WGRAD), op == 3);
+  return with_bound_scratch(
+      plan_ws_bytes(*d, op == 0 || op == 3 ? MODE_DGRAD : (op == 1 ? MODE_FWD : MODE_WGRAD), op == 3));
 }
 
 int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y, int accumulate,
@@ -1623,22 +1668,32 @@ int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, 
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
                         void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx));
-  ConvArgs a = make_args(*d);
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 1, dy, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  ConvArgs a = make_args(db);
   a.dy = dy; a.w = w; a.dx = dx;
-  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
                           void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(dw));
-  ConvArgs a = make_args(*d);
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 1, dy, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  ConvArgs a = make_args(db);
   a.x = x; a.dy = dy; a.dw = dw;
-  return run<MODE_WGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream) {
-  return tde_conv2d_bwd_data(d, x_small, w, y_big, accumulate, ws, ws_bytes, stream);
+  // the deconv input is an activation (no gradient-operand bound needed): the virtual DGRAD directly
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big));
+  ConvArgs a = make_args(*d);
+  a.dy = x_small; a.w = w; a.dx = y_big;
+  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 // Folded-BN inference conv: y = relu?(conv(x, w_folded) + bias) into the y view of d.
@@ -1669,21 +1724,24 @@ int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const fl
 }
 
 size_t tde_conv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
-  return desc_ok(d) ? bwd_ws_bytes(*d, MODE_DGRAD) : 0;
+  return desc_ok(d) ? with_bound_scratch(bwd_ws_bytes(*d, MODE_DGRAD)) : 0;
 }
 
 size_t tde_deconv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
-  return desc_ok(d) ? bwd_ws_bytes(*d, MODE_FWD) : 0;
+  return desc_ok(d) ? with_bound_scratch(bwd_ws_bytes(*d, MODE_FWD)) : 0;
 }
 
 int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, const float* w, float* dx,
                    int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx) &&
                 tde_aligned16(dw));
-  ConvArgs a1 = make_args(*d), a2 = make_args(*d);
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 1, dy, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  ConvArgs a1 = make_args(db), a2 = make_args(db);
   a1.dy = dy; a1.w = w; a1.dx = dx;
   a2.x = x; a2.dy = dy; a2.dw = dw;
-  return run_bwd<MODE_DGRAD>(d, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  return run_bwd<MODE_DGRAD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, const float* w,
@@ -1691,20 +1749,33 @@ int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float*
                      void* stream) {
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(x_small) && tde_aligned16(w) &&
                 tde_aligned16(dx_small) && tde_aligned16(dw));
-  ConvArgs a1 = make_args(*d), a2 = make_args(*d);
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  ConvArgs a1 = make_args(db), a2 = make_args(db);
   a1.x = dy_big; a1.w = w; a1.y = dx_small;          // data gradient = Conv2D(dy_big) (virtual FWD)
   a2.x = dy_big; a2.dy = x_small; a2.dw = dw;        // filter gradient (virtual WGRAD)
-  return run_bwd<MODE_FWD>(d, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  return run_bwd<MODE_FWD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,
                           int accumulate, void* ws, size_t ws_bytes, void* stream) {
-  return tde_conv2d_fwd(d, dy_big, w, dx_small, accumulate, ws, ws_bytes, stream);
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(w) && tde_aligned16(dx_small));
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  return tde_conv2d_fwd(&db, dy_big, w, dx_small, accumulate, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, float* dw,
                             int accumulate, void* ws, size_t ws_bytes, void* stream) {
-  return tde_conv2d_bwd_filter(d, dy_big, x_small, dw, accumulate, ws, ws_bytes, stream);
+  TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(x_small) && tde_aligned16(dw));
+  tde_conv_desc_t db;
+  const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
+  if (rc != TDE_OK) return rc;
+  ConvArgs a = make_args(db);
+  a.x = dy_big; a.dy = x_small; a.dw = dw;
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -1,5 +1,6 @@
-// Few-output-channel conv heads (K <= 8): disparity heads (nets_optflow_depth.py:122-144,
-// DISP_SCALING*sigmoid(conv+b) [+MIN_DISP]), flow heads (nets_depth.py:169-191, 2-ch linear), exp-mask
+// Few-output-channel conv heads (K in {1,2,3,6}): disparity heads (nets_optflow_depth.py:122-144,
+// DISP_SCALING*sigmoid(conv+b) [+MIN_DISP]; nets.py:122-144, 3-ch linear), flow heads (nets_depth.py:169-191,
+// 2-ch linear), exp-mask
 // logits (nets_optflow_depth.py:193-198, k 3/5/7) and pose/pred 1x1 (:181).  These GEMMs have N = 1..6
 // and are HBM/L2-bound (arithmetic intensity ~K flop/B), so they are direct convolutions on the vector
 // ALU with the activation and its derivative fused, not MFMA tiles padded to 16 columns.
@@ -548,7 +549,7 @@ __global__ void __launch_bounds__(256) head_twgrad_kernel(const HeadArgs p, int 
 
 // taps per wgrad block: TT * 4 * KC accumulators per thread
 template <int KC>
-struct WgTaps { static constexpr int TT = KC == 1 ? 9 : (KC == 2 ? 5 : 2); };
+struct WgTaps { static constexpr int TT = KC == 1 ? 9 : (KC == 2 ? 5 : (KC == 3 ? 3 : 2)); };
 
 constexpr int WG_MAX_CHUNKS = 1024;
 
@@ -712,7 +713,7 @@ static const long g_head_blocks = tde_env_pos("TDE_HEAD_BLOCKS", 2048);
 WgPlan wg_plan(const tde_conv_desc_t* d) {
   WgPlan w;
   const long M = (long)d->N * d->OH * d->OW;
-  const int TT = d->K == 1 ? 9 : (d->K == 2 ? 5 : 2);
+  const int TT = d->K == 1 ? 9 : (d->K == 2 ? 5 : (d->K == 3 ? 3 : 2));
   w.tgroups = (d->KH * d->KW + TT - 1) / TT;
   const int P = 256 / (d->C / 4);
   // >= g_head_ppl pixels per thread lane, ~2048 blocks in total, <= WG_MAX_CHUNKS partial rows
@@ -877,6 +878,7 @@ int launch_dgrad(const HeadArgs& a, hipStream_t st) {
   switch (KVAL) {                                                                            \
     case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
     case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
     case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
     default: return TDE_ERR_UNSUPPORTED;                                                     \
   }
@@ -907,6 +909,7 @@ int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   switch (d->K) {
     case 1: launch_fwd<1>(a, M, st); break;
     case 2: launch_fwd<2>(a, M, st); break;
+    case 3: launch_fwd<3>(a, M, st); break;
     case 6: launch_fwd<6>(a, M, st); break;
     default: return TDE_ERR_UNSUPPORTED;
   }
@@ -918,7 +921,7 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
                  float offset, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(head_desc_ok(d) && d->stride == 1 && x && w && y && dy && tde_aligned16(x));
   TDE_CHECK_ARG(d->x_cstride % 4 == 0 && d->x_coff % 4 == 0);
-  TDE_CHECK_ARG(d->K == 1 || d->K == 2 || d->K == 6);
+  TDE_CHECK_ARG(d->K == 1 || d->K == 2 || d->K == 3 || d->K == 6);
   if (ws_bytes < tde_head_workspace_size(d) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   ws = tde_ws_body(ws);
   HeadArgs a = make_head_args(d);
@@ -953,6 +956,7 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
       switch (d->K) {
         case 1: rc = launch_dgrad<1>(a, st); break;
         case 2: rc = launch_dgrad<2>(a, st); break;
+        case 3: rc = launch_dgrad<3>(a, st); break;
         default: rc = launch_dgrad<6>(a, st); break;
       }
       if (rc != TDE_OK) return rc;
@@ -968,6 +972,7 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
     switch (d->K) {
       case 1: rc = launch_dgrad<1>(a, st); break;
       case 2: rc = launch_dgrad<2>(a, st); break;
+      case 3: rc = launch_dgrad<3>(a, st); break;
       default: rc = launch_dgrad<6>(a, st); break;
     }
     if (rc != TDE_OK) return rc;

@@ -88,7 +88,8 @@ class GradSync:
         self.pending = {}
         self.device = self.chunks[0].grad.device if self.chunks else torch.device("cpu")
         self.gpu = self.device.type == "cuda"
-        self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
+        # a dedicated HIP stream (never one of torch's pooled streams, which a capture stream may alias)
+        self.comm = _lib.dedicated_stream() if self.gpu else None
         self.capturing = None       # set by Trainer.capture: callable(buckets) closing a graph segment
         self.log = []               # launch order (names), for tests
         self.begin_step()

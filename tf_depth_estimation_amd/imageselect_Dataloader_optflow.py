@@ -77,7 +77,7 @@ class _Slot:
 class DataLoader(object):
     def __init__(self, dataset_dir, batch_size, image_height, image_width, num_source, num_scales, split,
                  resizedheight=240, resizedwidth=720, shuffle=True, num_epochs=1500, seed=None, workers=8,
-                 prefetch=2, decode_procs=0):
+                 prefetch=2, decode_procs=0, task_timeout=300.0):
         self.dataset_dir = dataset_dir
         self.batch_size = batch_size
         self.image_height = image_height
@@ -95,7 +95,9 @@ class DataLoader(object):
         self._procs = max(0, int(decode_procs))
         self._started = False
         self._held = None
-        self._retired = []
+        self._retired = []              # (segment, slot) replaced when a slot's shared staging grew
+        self._drop_names = []           # names of unlinked segments the workers should let go of
+        self._task_timeout = float(task_timeout)   # seconds one worker task may take before the loader raises
         self.last_indices = None
         self._lib = _lib.load()
 
@@ -177,7 +179,7 @@ class DataLoader(object):
                 self._ppool.terminate()
                 self._ppool.join()
                 self._ppool = None
-            for sh in [sl.shm for sl in self._slots if sl.shm is not None] + self._retired:
+            for sh in [sl.shm for sl in self._slots if sl.shm is not None] + [r[0] for r in self._retired]:
                 sh.close()
                 try:
                     sh.unlink()
@@ -222,6 +224,9 @@ class DataLoader(object):
             for sl in self._slots:
                 sl.shm = shared_memory.SharedMemory(create=True, size=B * stride + lab)
             self._ppool = mp.get_context("spawn").Pool(self._procs)
+            # the pool silently replaces a worker that dies (OOM kill, a decoder crash) and never completes the
+            # task it held: the loader watches the original workers and raises instead of waiting forever
+            self._worker_procs = list(getattr(self._ppool, "_pool", []))
         self._free = queue.Queue()
         for sl in self._slots:
             self._free.put(sl)
@@ -283,11 +288,12 @@ class DataLoader(object):
                 if self._ppool is not None:
                     # whole samples in the worker processes (image + label into shared memory, cam / proj parsed)
                     f, HW = self._files, self.image_height * self.image_width
+                    drop = tuple(self._drop_names)
                     futs = [self._ppool.apply_async(
                         _decode_worker.load_sample,
                         (slot.shm.name, b * slot.stride, slot.stride, f["image_file_list"][i],
                          B * slot.stride + b * HW * 4, HW, f["gt_depth_file_list"][i], f["cam_file_list"][i],
-                         f["tgt2src_proj_list"][i])) for b, i in enumerate(idx)]
+                         f["tgt2src_proj_list"][i], drop)) for b, i in enumerate(idx)]
                     pending.append((slot, futs, True))
                 else:
                     futs = [self._pool.submit(self._sample, slot, b, i) for b, i in enumerate(idx)]
@@ -296,6 +302,25 @@ class DataLoader(object):
                     self._finish(*pending.popleft())
         except BaseException as e:       # surfaced by load_train_batch
             self._q.put(e)
+
+    def _await(self, fu):
+        """Result of one worker task; raises (instead of blocking forever) when a worker died, the loader was
+        closed, or the task outlived task_timeout."""
+        import time
+        deadline = time.monotonic() + self._task_timeout
+        while not fu.ready():
+            fu.wait(0.5)
+            if fu.ready():
+                break
+            if self._stop.is_set():
+                raise RuntimeError("DataLoader closed while a batch was loading")
+            dead = [p for p in self._worker_procs if p.exitcode is not None]
+            if dead:
+                raise RuntimeError(f"DataLoader: decode worker pid {dead[0].pid} exited with code {dead[0].exitcode}; "
+                                   "the sample it was loading is lost")
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"DataLoader: a decode task took longer than {self._task_timeout:.0f} s")
+        return fu.get()
 
     def _sample(self, slot, b, i):
         """One sample into slot row b: image bytes at hdr + b * stride (the image back if it does not fit),
@@ -322,8 +347,22 @@ class DataLoader(object):
             # worker-loaded samples: (h, w, image if it did not fit, cam, projs, m); shared staging -> pinned
             res = []
             for fu in futs:
-                h, w, big, cam, projs, m = fu.get()
+                h, w, big, cam, projs, m = self._await(fu)
                 res.append([h, w, cam, projs, m, big])
+            # this slot's batches now come from its current segment: a segment it outgrew earlier is written by
+            # no task any more -- unlink it, and let the workers drop their handles at their next task
+            keep = []
+            for sh, owner in self._retired:
+                if owner is slot:
+                    self._drop_names.append(sh.name)
+                    sh.close()
+                    try:
+                        sh.unlink()
+                    except FileNotFoundError:
+                        pass
+                else:
+                    keep.append((sh, owner))
+            self._retired = keep
             n = B * slot.stride
             seg = slot.shm.buf
             slot.stage.numpy()[slot.hdr:slot.hdr + n] = np.ndarray((n,), np.uint8, seg, 0)
@@ -344,7 +383,7 @@ class DataLoader(object):
                 from multiprocessing import shared_memory
                 old_shm = slot.shm
                 slot.shm = shared_memory.SharedMemory(create=True, size=B * stride + slot.label_h.numel() * 4)
-                self._retired.append(old_shm)
+                self._retired.append((old_shm, slot))
         st = slot.stage.numpy()
         offs = slot.hdr + np.arange(B, dtype=np.int64) * slot.stride
         st[:8 * B] = offs.view(np.uint8)

@@ -417,12 +417,15 @@ class NetProgram:
         """Inference weights: each conv/deconv's moving statistics folded into its weights and a bias
         (tde_bn_fold; batch_prediction.py:41-44 runs disp_net with is_training=False).  A snapshot of the
         current variables: call again after a checkpoint restore or further training."""
+        fl = getattr(self.chunk, "pending_flush", None)
+        if fl is not None:
+            fl()            # a deferred-Adam trainer's owed update first (Trainer.flush)
         lib = _lib.load()
         st = _lib.stream_ptr()
         folded = {}
         for op in self.spec.ops:
             if not (isinstance(op, ConvBN) and op.bn):
-                continue
+                continue     # (BN-free layers run their own weights and biases)
             w = self.P(f"{op.layer}/weights")
             beta = self.P(f"{op.layer}/BatchNorm/beta")
             mm, mv = self.chunk.moving(f"{self.prefix}/{op.layer}/BatchNorm")
@@ -451,11 +454,14 @@ class NetProgram:
         any gradient-exchange launch point: join_wgrad()).  The two GEMMs are the separate data- and
         filter-gradient calls (their own tile plans, not the fused launch's shared tile), so results equal
         serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
-        self.wgrad_stream = (SERIAL if serial else torch.cuda.Stream()) if on else None
+        # dedicated HIP streams, one per role and program (torch.cuda.Stream() recycles a fixed pool: a pooled
+        # side stream can alias a capture stream or another program's side stream, _lib.dedicated_stream)
+        self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0")) if on else None
         # TDE_WGRAD_STREAMS > 1: the filter-gradient groups alternate over that many side streams (each with its
         # own workspace), so independent filter gradients may run concurrently with each other
         n = 1 if (serial or not on) else _env_pos("TDE_WGRAD_STREAMS", 1)
-        self.wgrad_streams = [self.wgrad_stream] + [torch.cuda.Stream() for _ in range(n - 1)] if on else []
+        self.wgrad_streams = ([self.wgrad_stream] + [_lib.owned_stream(self, f"wgrad{j}") for j in range(1, n)]
+                              if on else [])
         self._wg_rr = 0
         return self
 
@@ -572,7 +578,16 @@ class NetProgram:
                 w = self.P(f"{op.layer}/weights")
                 z = run.z[i] if op.bn else None
                 if not op.bn:
-                    raise NotImplementedError("BN-free conv/deconv layers")
+                    # BN-free layer (nets_optflow_depth_pairtest.py:83-85): conv + bias + ReLU in one launch,
+                    # written straight into the consumer's channel view (training and inference alike)
+                    fd = op.folded_desc(N)
+                    if not fold_bn:
+                        self._use_split(fd, i, N)
+                    fn = lib.tde_deconv2d_fwd_bias_act if op.deconv else lib.tde_conv2d_fwd_bias_act
+                    with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
+                        _lib.check(fn(ctypes_ref(fd), run.vptr(op.src), ptr(w), ptr(self.P(f"{op.layer}/biases")), 1,
+                                      run.vptr(op.dst), ptr(ws), wsb, st), op.layer)
+                    continue
                 M = N * op.dst.H * op.dst.W
                 beta = self.P(f"{op.layer}/BatchNorm/beta")
                 sm = run.stats[i]
@@ -710,10 +725,17 @@ class NetProgram:
                 else:
                     d.y_absmax = run.absmax_ptr(i)
                 M = N * op.dst.H * op.dst.W
-                sm = run.stats[i]
+                sm = run.stats.get(i)
                 if side is not None:
                     dz = self._dz_layer(N, i, M * op.K)
-                if self.bn_sync is not None:
+                if not op.bn:
+                    # BN-free layer: dz = dy * relu'(y), bias gradient (fixed-order fp64 sums)
+                    with self._span("bn_bwd"):
+                        _lib.check(lib.tde_bias_relu_bwd(M, op.K, run.vptr(op.dst), op.dst.buf.cs, op.dst.coff,
+                                                         run.vptr(op.dst, True), op.dst.buf.cs, op.dst.coff, 1, ptr(dz),
+                                                         ptr(self.G(f"{op.layer}/biases")), pacc, run.absmax_ptr(i),
+                                                         ptr(ws), wsb, st), op.layer + " bias_relu_bwd")
+                elif self.bn_sync is not None:
                     # SyncBN backward: local (sum g, sum g*xhat) -> all-reduced copy -> dz from the global means,
                     # dbeta from the local sum (the gradient all-reduce averages it like every parameter)
                     ls, gs = self._sums(i, op.K, 1), self._sums(i, op.K, 2)

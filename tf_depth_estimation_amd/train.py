@@ -72,7 +72,7 @@ class AdamOverlap:
                 for n in b.names:
                     self.by_param[(id(o.chunk), n)] = b
         self.uses = {id(o.chunk): (uses or {}).get(id(o.chunk), 1) for o in self.opts}
-        self.side = torch.cuda.Stream()
+        self.side = _lib.dedicated_stream()
 
     def begin_step(self):
         self.count = {k: 0 for k in self.by_param}
@@ -146,7 +146,7 @@ class DeferredAdam:
 
     def __init__(self, opts, first_mb=2.0):
         self.opts = list(opts)
-        self.side = torch.cuda.Stream()
+        self.side = _lib.dedicated_stream()
         self.buckets = {}
         for o in self.opts:
             c = o.chunk
@@ -248,7 +248,7 @@ class Trainer:
         if on and (self.grad_sync is not None or self.adam_ov is not None or self.dadam is not None or
                    getattr(self, "sync_bn", False)):
             raise ValueError("net overlap is for the single-GPU step without exchange / Adam overlap / SyncBN")
-        self.net_stream = _lib.dedicated_stream() if on else None
+        self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
     def _overlap_stream(self):
@@ -263,8 +263,14 @@ class Trainer:
         The parameters then lag the gradients by one update until flush()."""
         if self.grad_sync is not None or self.adam_ov is not None:
             raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap")
+        if self.net_stream is not None:
+            # the overlapped capture has no _begin() piece: a deferred update would never be launched
+            raise ValueError("deferred Adam and net overlap are exclusive")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
         self.dadam = DeferredAdam(opts, first_mb)
+        for o in opts:
+            # checkpoint.Saver and the read-out methods apply an owed update first (the parameters lag by one)
+            o.chunk.pending_flush = self.flush
         for p in self.programs():
             # the backward overwrites the gradients the update reads: it starts after every bucket is done
             p.pre_op, p.params_ready, p.pre_backward = self.dadam.pre_op, self.dadam.params_ready, self.dadam.end_forward
@@ -283,6 +289,8 @@ class Trainer:
         so the compute stream never waits for it until the end of the step."""
         if self.grad_sync is not None:
             raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
+        if self.net_stream is not None:
+            raise ValueError("Adam overlap and net overlap are exclusive")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
         streams = {}
         if on_wgrad_stream:
@@ -369,7 +377,7 @@ class Trainer:
         """Warm up on a side stream (allocates every lazily created buffer), then record."""
         if getattr(self, "sync_bn", False):
             raise NotImplementedError("SyncBN all-reduces inside the forward/backward: run step() eagerly")
-        s = torch.cuda.Stream()
+        s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
@@ -378,7 +386,7 @@ class Trainer:
         gs = self.grad_sync
         if gs is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+            with torch.cuda.graph(g, stream=_lib.owned_stream(self, "capture"), capture_error_mode=CAPTURE_MODE):
                 self._begin()
                 self.phase_compute()
                 self._update()
@@ -386,16 +394,16 @@ class Trainer:
             return self.graphs
         if not hasattr(gs, "begin_step"):       # plain exchange after backward
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, capture_error_mode=CAPTURE_MODE):
+            with torch.cuda.graph(g1, stream=_lib.owned_stream(self, "capture"), capture_error_mode=CAPTURE_MODE):
                 self.phase_compute()
-            with torch.cuda.graph(g2, capture_error_mode=CAPTURE_MODE):
+            with torch.cuda.graph(g2, stream=_lib.owned_stream(self, "capture"), capture_error_mode=CAPTURE_MODE):
                 self.phase_update()
             self.graphs = [g1, g2]
             return self.graphs
         # segmented capture: graph boundaries at bucket launch points
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        cs = torch.cuda.Stream()
+        cs = _lib.owned_stream(self, "capture")
         segs = []
         state = {"g": torch.cuda.CUDAGraph()}
 
@@ -675,7 +683,7 @@ class DepthThenCamTrainer(Trainer):
         with the same stream waits as the eager overlapped step."""
         if self._overlap_stream() is None:
             return super().capture(warmup)
-        s = torch.cuda.Stream()
+        s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
@@ -683,7 +691,7 @@ class DepthThenCamTrainer(Trainer):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        main, ov = _lib.dedicated_stream(), self.net_stream
+        main, ov = _lib.owned_stream(self, "capture"), self.net_stream
         pieces = self._pieces() + [("main", self._update)]
         seq = []
         self._out = {}
