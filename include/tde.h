@@ -131,6 +131,7 @@ typedef struct {
   float* save_mean; float* save_invstd;
   float* y; int y_cstride, y_coff;
   int relu;
+  int groups;              /* row groups (0 or 1: one), see tde_bn_fwd_train */
 } tde_bn_train_t;
 /* z dense [N*OH*OW][K] (y_cstride == K, y_coff == 0 in d).  Workspace: tde_conv2d_workspace_size(d, 3). */
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z,
@@ -198,9 +199,14 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
  * (arg_scope nets_optflow_depth.py:82-87).  z is the dense conv output [M][C] (M = N*H*W);
  * y is a channel view (y_cstride, y_coff).  Training normalises with the biased batch variance and
  * updates moving_mean/moving_var in place (v -= (v - batch) * (1 - decay)); `bessel` selects the
- * FusedBatchNorm n/(n-1) correction of the variance fed to the moving average. */
+ * FusedBatchNorm n/(n-1) correction of the variance fed to the moving average.
+ * groups G (1..8, G | M): the M rows are G equal consecutive row groups, each normalised over its OWN rows --
+ * the G calls of one shared-variable network on different images (train_depth_then_cam_lr.py:130-136: disp_net
+ * on the left and on the right image, separate BN batches) batched into one launch.  save_mean / save_invstd
+ * are then [G][C], the moving averages take G updates in group order, and the backward's dbeta is the sum of
+ * the groups' (in group order; the first overwrites unless accumulate_dbeta). */
 size_t tde_bn_workspace_size(int M, int C);
-int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps, float decay,
+int tde_bn_fwd_train(int M, int C, int groups, const float* z, const float* beta, float eps, float decay,
                      int bessel, float* moving_mean, float* moving_var, float* save_mean,
                      float* save_invstd, float* y, int y_cstride, int y_coff, int relu,
                      void* ws, size_t ws_bytes, void* stream);
@@ -217,7 +223,7 @@ int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const floa
  * dz_absmax (nullable): TDE_BOUND_SLOTS device floats whose max is raised to max|dz| (atomic max; the caller
  * zeroes them first) -- the bound of dz as the gradient operand of the conv backward in conv math 4
  * (tde_conv_desc_t.y_absmax). */
-int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd,
+int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean, const float* save_invstd,
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz,
                float* dbeta, int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes,
                void* stream);
@@ -348,7 +354,8 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* args, void* stream);
  *   exp    : exp_w    * mean_pix(CE(logits, [0,1]))               (compute_exp_reg_loss, :87-91)
  *   consist: consist_w* mean_pix(|z - bilinear(1/disp_other,(u,v))| * softmax(logits)[1])
  * loss[0..2] += (photo, exp, consist); gradients are ADDED into g_disp / g_flow / g_logits (same views
- * as the inputs), scattered with float atomics into g_other, and reduced per batch element into
+ * as the inputs), scattered with float atomics (or, with det_ws, deterministically) into g_other, and reduced
+ * per batch element into
  * g_P[b][12] = dL/dP (fp64, +=), from which tde_pose_grad chains to the 6-DoF pose vector. */
 typedef struct {
   int B, H, W;
@@ -365,8 +372,16 @@ typedef struct {
   double* loss;                                      /* [3] */
   float* g_disp; float* g_flow; float* g_logits; float* g_other;
   double* g_P;                                       /* [B][12] or NULL (pose is data) */
+  /* Deterministic mode (NULL: off): a device workspace of >= tde_warp_loss_det_workspace_size(B, H, W) bytes.
+   * The g_other scatter then runs as 64-bit fixed-point integer atomics (associative: the same sum in any
+   * order, scaled from max(1/disp_other)^2 so no pixel can overflow) added into g_other once, and the loss
+   * parts / g_P leave each block as partials summed in block order -- run-to-run bit-identical results, at
+   * the cost of 3 more launches.  The fixed-point sums are exact to ~2^-40 of the largest possible one. */
+  void* det_ws;
+  size_t det_ws_bytes;
 } tde_warp_loss_t;
 int tde_warp_loss(const tde_warp_loss_t* args, void* stream);
+size_t tde_warp_loss_det_workspace_size(int B, int H, int W);
 
 /* Forward-only projective_inverse_warp (utils_lr.py:222-256) / bilinear_sampler (:276-366): coords from
  * depth (or 1/disp when depth_is_disp) through P and Kinv, or given coords_in [B,H,W,2] when depth is

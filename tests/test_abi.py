@@ -43,7 +43,7 @@ def test_status_strings_and_arg_checks():
     d = _lib.ConvDesc()
     assert lib.tde_conv2d_workspace_size(ctypes.byref(d), 0) == 0
     assert lib.tde_conv2d_fwd(ctypes.byref(d), None, None, None, 0, None, 0, None) == -1
-    assert lib.tde_bn_fwd_train(0, 3, None, None, 1e-3, 0.99, 1, None, None, None, None, None, 4, 0, 1, None, 0,
+    assert lib.tde_bn_fwd_train(0, 3, 1, None, None, 1e-3, 0.99, 1, None, None, None, None, None, 4, 0, 1, None, 0,
                                 None) == -1
 
 

@@ -324,6 +324,85 @@ def test_conv_fused_bn_relu(L, case):
     assert torch.equal(z, z2) and torch.equal(sm, sm2) and torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("case", [c for c in BN_FUSED_CASES if c[1] % 2 == 0] + [(False, 4, 192, 256, 16, 16, 3, 1)])
+def test_conv_fused_bn_grouped(L, case):
+    """Row-grouped BatchNorm (tde_bn_train_t.groups = 2: the left / right calls of one shared-variable network
+    batched, train_depth_then_cam_lr.py:130-136): each half of the batch is normalised over its own rows, the
+    moving averages take the halves' updates in order, y = relu(BN_g(z)) per half -- on every fused path
+    (small, epilogue partials, split-K / deconv -> grouped standalone pass, halo tile partials)."""
+    deconv, N, H, W, C, K, k, s = case
+    G = 2
+    lib = L.load()
+    st = L.stream_ptr()
+    if deconv:
+        cin, cout = C, K
+        OHb, OWb = 2 * H, 2 * W
+        _, pt, _ = T.same_pad(OHb, k, 2)
+        _, pl, _ = T.same_pad(OWb, k, 2)
+        d = conv_desc(L, N=N, H=OHb, W=OWb, C=cout, OH=H, OW=W, K=cin, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
+                      w_cin=cout, x_cstride=cout, x_coff=0, y_cstride=cin, y_coff=0)
+        x = rnd(N, H, W, cin, seed=51)
+        w = rnd(k, k, cout, cin, seed=52) * 0.2
+        zr = T.conv2d_transpose_same(x, w, 2)
+        fn, q = lib.tde_deconv2d_fwd_bn, lib.tde_deconv2d_workspace_size
+    else:
+        OH, pt, _ = T.same_pad(H, k, s)
+        OW, pl, _ = T.same_pad(W, k, s)
+        d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
+                      w_cin=C, x_cstride=C, x_coff=0, y_cstride=K, y_coff=0)
+        x = rnd(N, H, W, C, seed=51)
+        w = rnd(k, k, C, K, seed=52) * 0.2
+        zr = T.conv2d_same(x, w, s)
+        fn, q = lib.tde_conv2d_fwd_bn, lib.tde_conv2d_workspace_size
+    Kc = zr.shape[-1]
+    M = zr.numel() // Kc
+    Mg = M // G
+    ws = torch.zeros(q(ctypes.byref(d), 3) // 4 + 16, device="cuda")
+    beta = dev(rnd(Kc, seed=53) * 0.2)
+    mm, mv = torch.zeros(Kc, device="cuda"), torch.ones(Kc, device="cuda")
+    sm = torch.empty(2, G * Kc, device="cuda")
+    z = torch.empty(zr.shape, device="cuda")
+    ycs, yco = Kc + 4, 4
+    y = torch.zeros(M, ycs, device="cuda")
+    bn = L.BnTrain(L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(y), ycs, yco, 1,
+                   G)
+    L.check(fn(ctypes.byref(d), L.ptr(dev(x)), L.ptr(dev(w)), L.ptr(z), ctypes.byref(bn), L.ptr(ws), ws.numel() * 4,
+               st))
+    close(z, zr, what="z")
+    z64 = zr.double().reshape(M, Kc)
+    mm_r, mv_r = torch.zeros(Kc, dtype=torch.float64), torch.ones(Kc, dtype=torch.float64)
+    for g in range(G):
+        zg = z64[g * Mg:(g + 1) * Mg]
+        mean, var = zg.mean(0), zg.var(0, unbiased=False)
+        close(sm[0, g * Kc:(g + 1) * Kc], mean, tol=1e-5, what=f"group {g} mean")
+        close(sm[1, g * Kc:(g + 1) * Kc], 1.0 / torch.sqrt(var + 1e-3), tol=1e-5, what=f"group {g} invstd")
+        mm_r = mm_r - (mm_r - mean) * 0.01
+        mv_r = mv_r - (mv_r - var * Mg / (Mg - 1)) * 0.01
+        ref = torch.relu((zg - mean) / torch.sqrt(var + 1e-3) + beta.double().cpu())
+        close(y[g * Mg:(g + 1) * Mg, yco:yco + Kc], ref, what=f"group {g} bn+relu")
+    close(mm, mm_r, tol=1e-5, what="moving mean (two updates)")
+    close(mv, mv_r, tol=1e-5, what="moving var (two updates)")
+    # backward over the groups: dz per group, dbeta summed over the groups
+    dy = rnd(M, Kc, seed=54)
+    gdy = torch.zeros(M, ycs, device="cuda")
+    gdy[:, yco:yco + Kc] = dev(dy)
+    dz = torch.empty(M, Kc, device="cuda")
+    dbeta = torch.zeros(Kc, device="cuda")
+    wsb = torch.zeros(lib.tde_bn_workspace_size(M, Kc) // 4 + 16, device="cuda")
+    L.check(lib.tde_bn_bwd(M, Kc, G, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(gdy), ycs, yco,
+                           L.ptr(dz), L.ptr(dbeta), 0, 1, None, L.ptr(wsb), wsb.numel() * 4, st))
+    zr_ = zr.double().reshape(M, Kc).clone().requires_grad_(True)
+    outs = []
+    for g in range(G):
+        zg = zr_[g * Mg:(g + 1) * Mg]
+        mean, var = zg.mean(0), zg.var(0, unbiased=False)
+        outs.append(torch.relu((zg - mean) / torch.sqrt(var + 1e-3) + beta.double().cpu()))
+    torch.cat(outs).backward(dy)
+    close(dz, zr_.grad, tol=5e-5, what="grouped bn dz")
+    ym = torch.cat(outs).detach() > 0
+    close(dbeta, (dy * ym).sum(0), tol=5e-5, what="grouped dbeta")
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv2d_bwd_fused(L, case):
     """tde_conv2d_bwd: data + filter gradient in one fused launch == the separate reference gradients
@@ -448,7 +527,7 @@ def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     sm = torch.empty(2, C, device="cuda")
     y = torch.zeros(M, ycs, device="cuda")
     ws = torch.zeros(lib.tde_bn_workspace_size(M, C) // 4 + 16, device="cuda")
-    L.check(lib.tde_bn_fwd_train(M, C, L.ptr(gz), L.ptr(gb), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
+    L.check(lib.tde_bn_fwd_train(M, C, 1, L.ptr(gz), L.ptr(gb), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
                                  L.ptr(sm[1]), L.ptr(y), ycs, yco, 1, L.ptr(ws), ws.numel() * 4, st))
     zr = z.clone().reshape(1, 1, M, C).requires_grad_(True)
     stt = T.BNState(C)
@@ -463,7 +542,7 @@ def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     dz = torch.empty(M, C, device="cuda")
     dbeta = torch.zeros(C, device="cuda")
     amax = torch.zeros(L.BOUND_SLOTS, device="cuda")
-    L.check(lib.tde_bn_bwd(M, C, L.ptr(gz), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(gb), L.ptr(gdy), ycs, yco, L.ptr(dz),
+    L.check(lib.tde_bn_bwd(M, C, 1, L.ptr(gz), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(gb), L.ptr(gdy), ycs, yco, L.ptr(dz),
                            L.ptr(dbeta), 1, 1, L.ptr(amax), L.ptr(ws), ws.numel() * 4, st))
     close(dz, zr.grad.reshape(M, C), tol=5e-5, what="bn dz")
     assert amax.max().item() == dz.abs().max().item(), "dz_absmax: max|dz| over the slots"
@@ -666,11 +745,11 @@ def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
     mm, mv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
     sm = torch.empty(2, C, device="cuda")
     y = torch.empty(M, C, device="cuda")
-    L.check(lib.tde_bn_fwd_train(M, C, L.ptr(z), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
+    L.check(lib.tde_bn_fwd_train(M, C, 1, L.ptr(z), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm), L.ptr(mv), L.ptr(sm[0]),
                                  L.ptr(sm[1]), L.ptr(y), C, 0, 1, L.ptr(ws), ws.numel() * 4, st))
     dz = torch.empty(M, C, device="cuda")
     db = torch.empty(C, device="cuda")
-    L.check(lib.tde_bn_bwd(M, C, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(dy), C, 0, L.ptr(dz),
+    L.check(lib.tde_bn_bwd(M, C, 1, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(dy), C, 0, L.ptr(dz),
                            L.ptr(db), 0, 1, None, L.ptr(ws), ws.numel() * 4, st))
     # two replicas
     parts = [(0, M1), (M1, M2)]

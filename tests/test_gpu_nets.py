@@ -316,9 +316,11 @@ def test_nets_sfm_disp_net_gradients():
         grads[dt] = dict({k: v.grad for k, v in P.vars.items()}, input=xr.grad)
     gpu = dict({k: chunk.grad_view(k) for k in chunk.names()}, input=xg.grad)
     check_grads_global(gpu, grads[torch.float64], grads[torch.float32], GRAD_FACTOR[4])
-    # the heads' own tensors (well conditioned: linear heads right at the loss) per tensor
-    for n in [k for k in grads[torch.float64] if "/disp" in k]:
-        assert rel_err(gpu[n], grads[torch.float64][n]) <= 1e-3, n
+    # the heads' own tensors per tensor (their dz also carries the gradient back from the next level's concat,
+    # i.e. through a training-mode BN backward: held relative to the fp32 oracle's own error)
+    check_grads({n: gpu[n] for n in grads[torch.float64] if "/disp" in n},
+                {n: v for n, v in grads[torch.float64].items() if "/disp" in n},
+                {n: v for n, v in grads[torch.float32].items() if "/disp" in n}, GRAD_FACTOR[4])
 
 
 def test_pairtest_bn_free_disp_net_parity():

@@ -73,12 +73,14 @@ def step_math(request):
     _lib.check(lib.tde_set_conv_math(prev))
 
 
-@pytest.mark.parametrize("term", list(C4_TERMS))
-def test_config4_depth_then_cam_step(term, step_math):
+@pytest.mark.parametrize("term,twin", [(t, True) for t in C4_TERMS] + [("all", False)])
+def test_config4_depth_then_cam_step(term, twin, step_math):
+    """twin=True (default): each net's two calls as one row-grouped batch-2B call (grouped BatchNorm);
+    twin=False: the four separate calls.  Both against the oracle's four separate calls."""
     from tf_depth_estimation_amd import train
     B, H, W = 2, 64, 96
     w = C4_TERMS[term] or dict(OL.W_CONFIG4)
-    tr = train.DepthThenCamTrainer(B, H, W, weights=w)
+    tr = train.DepthThenCamTrainer(B, H, W, weights=w, twin=twin)
     il, ir = texture(B, H, W, 1), texture(B, H, W, 2)
     g = np.random.default_rng(3)
     lab = g.uniform(0.1, 2.0, (B, H, W, 1))
@@ -263,10 +265,10 @@ def test_adam_overlap_matches_plain(cfg, graph, where):
     """Bucketed Adam on a side stream during backward (Trainer.enable_adam_overlap; a graph branch under
     capture) updates every element as the single Adam launch after backward: parameters and moments
     bit-identical.  Config 2 after three steps; config 4 (shared-variable nets: a bucket is final only at
-    its net's second backward call) after one step with the depth / consistency weight 0, so its
-    float-atomic scatter adds only zeros and the step is deterministic (two plain runs are checked to
-    agree bit for bit first).  With that term on, run-to-run rounding of the atomics makes Adam's first
-    update flip sign on near-zero gradients, which no tolerance separates from a wrong bucket.
+    its net's second backward call) after one step with every loss term on (depth / consistency weight 20) in
+    the deterministic warp-loss mode (Trainer.enable_deterministic: fixed-point scatter, fixed-order block sums;
+    two plain runs are checked to agree bit for bit first).  With float atomics, run-to-run rounding makes
+    Adam's first update flip sign on near-zero gradients, which no tolerance separates from a wrong bucket.
     where="wgrad": the buckets run on the programs' filter-gradient streams (enable_wgrad_overlap), against
     the same split backward run serially with the single Adam launch after it."""
     from tf_depth_estimation_amd import _api, train, variables
@@ -282,7 +284,7 @@ def test_adam_overlap_matches_plain(cfg, graph, where):
             tr.set_batch(torch.tensor(g.uniform(-0.5, 0.5, (B, H, W, 3)), dtype=torch.float32).cuda(),
                          torch.tensor(g.uniform(0.25, 4.0, (B, H, W, 1)), dtype=torch.float32).cuda())
         else:
-            tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+            tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
             lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
             tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
                          torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
@@ -316,9 +318,8 @@ def test_wgrad_overlap_matches_serial(cfg, graph):
     capture, joined at the end of backward; the BN backward alternates two dz buffers and waits for the
     filter gradient that last read the one it overwrites) against the same split calls serially on one
     stream: bit-identical.  Config 2 after three steps; config 4 (two backward calls per shared-variable
-    chunk, accumulating on the side stream; two programs, two side streams) after one step with the
-    depth / consistency weight 0, so its float-atomic scatter adds only zeros and the step is deterministic
-    (checked: two serial runs agree bit for bit first)."""
+    chunk, accumulating on the side stream; two programs, two side streams) after one step with all loss
+    terms in the deterministic warp-loss mode (checked: two serial runs agree bit for bit first)."""
     from tf_depth_estimation_amd import _api, train, variables
     steps = 3 if cfg == "config2" else 1
 
@@ -332,7 +333,7 @@ def test_wgrad_overlap_matches_serial(cfg, graph):
             tr.set_batch(torch.tensor(g.uniform(-0.5, 0.5, (B, H, W, 3)), dtype=torch.float32).cuda(),
                          torch.tensor(g.uniform(0.25, 4.0, (B, H, W, 1)), dtype=torch.float32).cuda())
         else:
-            tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+            tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
             lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
             tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
                          torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
@@ -359,9 +360,9 @@ def test_wgrad_overlap_matches_serial(cfg, graph):
 def test_deferred_adam_matches_plain(cfg, graph):
     """Trainer.enable_deferred_adam: each step's Adam runs at the start of the next step on a side stream,
     overlapped with that forward (per-bucket waits, the weight splits issued once their bucket is final).
-    After flush() the parameters and Adam moments equal the plain trainer's bit for bit (config 4 with the
-    consistency weight 0: its float-atomic scatter is the only non-deterministic term, see above); the loss
-    of every step matches too (the forward sees the same parameters; up to the fp64 atomics' summation order)."""
+    After flush() the parameters and Adam moments equal the plain trainer's bit for bit (config 4 with all
+    terms, deterministic warp-loss mode); the loss of every step matches too (the forward sees the same
+    parameters; up to the other loss kernels' fp64 atomics' summation order)."""
     from tf_depth_estimation_amd import _api, train, variables
     steps = 3
 
@@ -375,7 +376,7 @@ def test_deferred_adam_matches_plain(cfg, graph):
             tr.set_batch(torch.tensor(g.uniform(-0.5, 0.5, (B, H, W, 3)), dtype=torch.float32).cuda(),
                          torch.tensor(g.uniform(0.25, 4.0, (B, H, W, 1)), dtype=torch.float32).cuda())
         else:
-            tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+            tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
             lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
             tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
                          torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
@@ -409,14 +410,14 @@ def test_net_overlap_matches_serial(graph, wgrad):
     """Trainer.enable_net_overlap (config 4): depth_net's forward and backward calls on a second stream beside
     disp_net's (a parallel graph branch under capture) give the serial step's parameters, gradients and Adam
     moments bit for bit after two steps -- the programs share nothing, and each program's calls keep their
-    order.  Consistency weight 0: its float-atomic scatter is the only non-deterministic term (see above)."""
+    order.  All loss terms, deterministic warp-loss mode."""
     from tf_depth_estimation_amd import _api, train, variables
 
     def run(overlap):
         variables.get_store().reset(seed=1)
         _api.clear_programs()
         B, H, W = 2, 64, 96
-        tr = train.DepthThenCamTrainer(B, H, W, weights=dict(smooth=1.0, data=10.0, depth=0.0, exp=1.0, cam=5.0))
+        tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
         lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
         tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
                      torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
@@ -448,3 +449,45 @@ def test_net_overlap_rejects_exchange_hooks():
     tr.enable_adam_overlap(bucket_mb=0.5)
     with pytest.raises(ValueError):
         tr.enable_net_overlap()
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_deterministic_warp_scatter(graph):
+    """Trainer.enable_deterministic (tde_warp_loss det_ws): the config-4 step with every loss term on
+    (consistency weight 20, whose gather gradient scatters into the other view's disparity) is run-to-run
+    bit-identical -- gradients, parameters, moments -- and agrees with the float-atomic mode to rounding."""
+    from tf_depth_estimation_amd import _api, train, variables
+
+    def run(det):
+        variables.get_store().reset(seed=1)
+        _api.clear_programs()
+        B, H, W = 2, 64, 96
+        tr = train.DepthThenCamTrainer(B, H, W)
+        if det:
+            tr.enable_deterministic()
+        lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
+        lab[np.random.default_rng(4).uniform(size=lab.shape) < 0.05] = np.nan
+        tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
+                     torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
+                     small_pose(B, 4).cuda())
+        tr.enable_wgrad_overlap()
+        if graph:
+            tr.capture(warmup=1)
+        tr.step()
+        torch.cuda.synchronize()
+        grads = [c.grad.clone() for c in tr.chunks]
+        tr.step()
+        torch.cuda.synchronize()
+        return tr.loss_parts(), grads, [(c.flat.clone(), c.adam_m.clone(), c.adam_v.clone()) for c in tr.chunks]
+
+    pa, ga, sa = run(True)
+    pb, gb, sb = run(True)
+    assert pa == pb, "deterministic loss parts differ between runs"
+    for x, y in zip(ga, gb):
+        assert torch.equal(x, y), "deterministic gradients differ between runs"
+    for a, b in zip(sa, sb):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+    _, gf, _ = run(False)
+    for x, y in zip(ga, gf):
+        e = ((x.double() - y.double()).norm() / y.double().norm()).item()
+        assert e <= 1e-4, f"deterministic vs atomic gradient rel-L2 {e:.2e}"

@@ -36,7 +36,7 @@ class BnTrain(ctypes.Structure):
     """Mirror of tde_bn_train_t (include/tde.h): batch norm + ReLU fused behind a conv."""
     _fields_ = [("beta", P), ("eps", c_float), ("decay", c_float), ("bessel", c_int), ("moving_mean", P),
                 ("moving_var", P), ("save_mean", P), ("save_invstd", P), ("y", P), ("y_cstride", c_int),
-                ("y_coff", c_int), ("relu", c_int)]
+                ("y_coff", c_int), ("relu", c_int), ("groups", c_int)]
 
 
 class WarpLossArgs(ctypes.Structure):
@@ -48,7 +48,8 @@ class WarpLossArgs(ctypes.Structure):
                 ("logits", P), ("logit_cs", c_int), ("logit_co", c_int),
                 ("disp_other", P), ("other_cs", c_int), ("other_co", c_int),
                 ("photo_w", c_float), ("exp_w", c_float), ("consist_w", c_float),
-                ("loss", P), ("g_disp", P), ("g_flow", P), ("g_logits", P), ("g_other", P), ("g_P", P)]
+                ("loss", P), ("g_disp", P), ("g_flow", P), ("g_logits", P), ("g_other", P), ("g_P", P),
+                ("det_ws", P), ("det_ws_bytes", c_size_t)]
 
 
 class DepthLoss(ctypes.Structure):
@@ -73,6 +74,7 @@ _SIGS = {
     "tde_image_resize_unpack": (c_int, [P, P]),
     "tde_loss_depth_pyramid": (c_int, [P, P]),
     "tde_warp_loss": (c_int, [P, P]),
+    "tde_warp_loss_det_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),
     "tde_pose_prep": (c_int, [c_int, P, P, P, P, P, P, P]),
     "tde_pose_grad": (c_int, [c_int, c_int, P, P, ctypes.c_long, P, P, P, c_int, P]),
@@ -108,10 +110,11 @@ _SIGS = {
     "tde_head_fwd": (c_int, [P, P, P, P, P, c_int, c_float, c_float, P]),
     "tde_head_bwd": (c_int, [P, P, P, P, P, P, c_int, P, P, c_int, c_int, c_float, c_float, P, c_size_t, P]),
     "tde_bn_workspace_size": (c_size_t, [c_int, c_int]),
-    "tde_bn_fwd_train": (c_int, [c_int, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, c_int, c_int, c_int,
-                                 P, c_size_t, P]),
+    "tde_bn_fwd_train": (c_int, [c_int, c_int, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, c_int, c_int,
+                                 c_int, P, c_size_t, P]),
     "tde_bn_fwd_infer": (c_int, [c_int, c_int, P, P, c_float, P, P, P, c_int, c_int, c_int, P]),
-    "tde_bn_bwd": (c_int, [c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, P, c_size_t, P]),
+    "tde_bn_bwd": (c_int, [c_int, c_int, c_int, P, P, P, P, P, c_int, c_int, P, P, c_int, c_int, P, P, c_size_t,
+                           P]),
     "tde_bias_relu_bwd": (c_int, [c_int, c_int, P, c_int, c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_size_t,
                                   P]),
     "tde_bn_sums": (c_int, [c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P]),

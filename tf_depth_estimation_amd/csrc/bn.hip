@@ -42,7 +42,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 template <int MODE>
 __global__ void __launch_bounds__(256) bn_part_kernel(int M, int C, const float* z, const float* dy, int dycs, int dyco,
                                                       const float* mean, const float* invstd, const float* beta,
-                                                      int relu, int rows_per_chunk, double* part) {
+                                                      int relu, const BnChunks cp, double* part) {
   __shared__ double sh[2][256 * 4];
   const int q0 = blockIdx.y * 16;
   const int nq = min(16, C / 4 - q0);
@@ -50,13 +50,14 @@ __global__ void __launch_bounds__(256) bn_part_kernel(int M, int C, const float*
   const int tx = threadIdx.x % nq, ty = threadIdx.x / nq;
   const int c = 4 * (q0 + tx);
   double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  const int r0 = blockIdx.x * rows_per_chunk;
-  const int r1 = min(M, r0 + rows_per_chunk);
+  int r0, r1;
+  bn_chunk_rows(cp, blockIdx.x, r0, r1);
   if (ty < ty_n) {
     f4 mu = {0, 0, 0, 0}, is = {0, 0, 0, 0}, bt = {0, 0, 0, 0};
     if (MODE == 1) {
-      mu = *reinterpret_cast<const f4*>(mean + c);
-      is = *reinterpret_cast<const f4*>(invstd + c);
+      const int g = blockIdx.x / cp.per_g;      // the chunk's row group: its statistics
+      mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+      is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
       bt = *reinterpret_cast<const f4*>(beta + c);
     }
     // fp32 partials over <= 64 rows per lane, flushed into fp64; unrolled so several rows' loads are
@@ -98,12 +99,15 @@ __global__ void __launch_bounds__(256) bn_part_kernel(int M, int C, const float*
 // waves through LDS (one barrier; the round-1 version walked 1024 lanes down 9 LDS levels with a barrier
 // each).  MODE 0 publishes mean / invstd and updates the moving averages; MODE 1 writes
 // coef = (mean g, mean g*xhat) and dbeta; MODE 2 the raw sums.
+// Row groups (G >= 1; M = rows per group): group g reduces partials [g * nparts/G, (g+1) * nparts/G) and writes
+// its statistics at [g][C] (coef [g][2][C]); the moving averages take one update per group and dbeta the
+// groups' sums in group order -- what G consecutive slim.batch_norm calls of a shared-variable network do.
 // NT = 256 lanes for up to 512 partial rows, 1024 above (more loads in flight for the long reductions).
 template <int MODE, int NT>
 __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int nparts, const double* part, float eps,
                                                          float decay, int bessel, float* mm, float* mv,
                                                          float* save_mean, float* save_invstd, float* dbeta,
-                                                         int acc, float* coef, double* sums = nullptr) {
+                                                         int acc, float* coef, double* sums = nullptr, int G = 1) {
   constexpr int FIN_ST = NT / 4, NWV = NT / 64;
   __shared__ double sh[2][NWV][4];
   const int cl = threadIdx.x & 3, st = threadIdx.x >> 2;
@@ -116,57 +120,71 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int npart
     if (MODE == 0 && mm) { mm0 = mm[c]; mv0 = mv[c]; }
     if (MODE == 1 && dbeta && acc) db0 = dbeta[c];
   }
-  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-  int k = st;
-  for (; k + 3 * FIN_ST < nparts; k += 4 * FIN_ST) {
+  const int pg = nparts / G;
+  bool first = !acc;
+  for (int g = 0; g < G; ++g) {
+    const double* pp = part + (long)g * pg * 2 * C;
+    double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    int k = st;
+    for (; k + 3 * FIN_ST < pg; k += 4 * FIN_ST) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] += part[(long)(k + u * FIN_ST) * 2 * C + c];
-      b[u] += part[(long)(k + u * FIN_ST) * 2 * C + C + c];
+      for (int u = 0; u < 4; ++u) {
+        a[u] += pp[(long)(k + u * FIN_ST) * 2 * C + c];
+        b[u] += pp[(long)(k + u * FIN_ST) * 2 * C + C + c];
+      }
+    }
+    for (int u = 0; k < pg; k += FIN_ST, ++u) {
+      a[u] += pp[(long)k * 2 * C + c];
+      b[u] += pp[(long)k * 2 * C + C + c];
+    }
+    double ra = (a[0] + a[1]) + (a[2] + a[3]), rb = (b[0] + b[1]) + (b[2] + b[3]);
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {   // the 16 lanes of this wave with the same channel (lane bits 2..5)
+      ra += __shfl_xor(ra, o, 64);
+      rb += __shfl_xor(rb, o, 64);
+    }
+    if (g > 0) __syncthreads();          // the publishing lanes have read the previous group's sums
+    if (lane < 4) { sh[0][wv][lane] = ra; sh[1][wv][lane] = rb; }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      double s = 0, s2 = 0;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) { s += sh[0][w][cl]; s2 += sh[1][w][cl]; }
+      if (MODE == 2) {   // raw per-channel sums (SyncBN: all-reduced by the caller, then *_from_sums)
+        sums[(long)g * 2 * C + c] = s;
+        sums[(long)g * 2 * C + C + c] = s2;
+      } else if (MODE == 0) {
+        const double mean = s / M;
+        double var = s2 / M - mean * mean;
+        if (var < 0) var = 0;
+        save_mean[(long)g * C + c] = (float)mean;
+        save_invstd[(long)g * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (mm) {
+          const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
+          mm0 = mm0 - (mm0 - (float)mean) * (1.f - decay);
+          mv0 = mv0 - (mv0 - (float)vu) * (1.f - decay);
+        }
+      } else {
+        db0 = first ? (float)s : db0 + (float)s;
+        first = false;
+        coef[(long)g * 2 * C + c] = (float)(s / M);
+        coef[(long)g * 2 * C + C + c] = (float)(s2 / M);
+      }
     }
   }
-  for (int u = 0; k < nparts; k += FIN_ST, ++u) {
-    a[u] += part[(long)k * 2 * C + c];
-    b[u] += part[(long)k * 2 * C + C + c];
-  }
-  double ra = (a[0] + a[1]) + (a[2] + a[3]), rb = (b[0] + b[1]) + (b[2] + b[3]);
-#pragma unroll
-  for (int o = 4; o < 64; o <<= 1) {   // the 16 lanes of this wave with the same channel (lane bits 2..5)
-    ra += __shfl_xor(ra, o, 64);
-    rb += __shfl_xor(rb, o, 64);
-  }
-  if (lane < 4) { sh[0][wv][lane] = ra; sh[1][wv][lane] = rb; }
-  __syncthreads();
-  if (threadIdx.x >= 4) return;
-  double s = 0, s2 = 0;
-#pragma unroll
-  for (int w = 0; w < NWV; ++w) { s += sh[0][w][cl]; s2 += sh[1][w][cl]; }
-  if (MODE == 2) {   // raw per-channel sums (SyncBN: all-reduced by the caller, then *_from_sums)
-    sums[c] = s;
-    sums[C + c] = s2;
-  } else if (MODE == 0) {
-    const double mean = s / M;
-    double var = s2 / M - mean * mean;
-    if (var < 0) var = 0;
-    save_mean[c] = (float)mean;
-    save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (mm) {
-      const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
-      mm[c] = mm0 - (mm0 - (float)mean) * (1.f - decay);
-      mv[c] = mv0 - (mv0 - (float)vu) * (1.f - decay);
-    }
-  } else {
-    if (dbeta) dbeta[c] = acc ? db0 + (float)s : (float)s;
-    coef[c] = (float)(s / M);
-    coef[C + c] = (float)(s2 / M);
+  if (threadIdx.x < 4) {
+    if (MODE == 0 && mm) { mm[c] = mm0; mv[c] = mv0; }
+    if (MODE == 1 && dbeta) dbeta[c] = db0;
   }
 }
 
 // y = relu((z - mean) * invstd + beta): rows split over blocks, a thread owns one channel quad of a row
 // lane (no 64-bit division in the index math).
+// Row groups: rows [g*Mg, (g+1)*Mg) use the statistics at [g][C] (a thread moves to the next group's
+// statistics when its row walk crosses a group boundary).
 __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float* z, const float* mean,
                                                        const float* invstd, const float* beta, int relu, float* y,
-                                                       int ycs, int yco, int rows_per_block) {
+                                                       int ycs, int yco, int rows_per_block, int Mg) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
   if (cq < 256 && threadIdx.x >= rstep * cq) return;
@@ -174,11 +192,18 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); qq < cq; qq += (cq >= 256 ? 256 : cq)) {
     const int c = 4 * qq;
-    const f4 mu = *reinterpret_cast<const f4*>(mean + c);
-    const f4 is = *reinterpret_cast<const f4*>(invstd + c);
+    int g = (r0 + rl) / Mg, gend = (g + 1) * Mg;
+    f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+    f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
 #pragma unroll 4
     for (int r = r0 + rl; r < r1; r += rstep) {
+      if (r >= gend) {
+        g = r / Mg;
+        gend = (g + 1) * Mg;
+        mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+        is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+      }
       const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
       f4 o;
 #pragma unroll
@@ -211,7 +236,7 @@ __device__ __forceinline__ void block_absmax_to(float m, float* amax) {
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const float* z, const float* dy, int dycs,
                                                            int dyco, const float* mean, const float* invstd,
                                                            const float* beta, const float* coef, int relu,
-                                                           float* dz, int rows_per_block, float* amax) {
+                                                           float* dz, int rows_per_block, float* amax, int Mg) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
   const bool active = cq >= 256 || threadIdx.x < rstep * cq;
@@ -220,13 +245,22 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
   float mx = 0.f;
   for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); active && qq < cq; qq += (cq >= 256 ? 256 : cq)) {
     const int c = 4 * qq;
-    const f4 mu = *reinterpret_cast<const f4*>(mean + c);
-    const f4 is = *reinterpret_cast<const f4*>(invstd + c);
+    int g = (r0 + rl) / Mg, gend = (g + 1) * Mg;
+    f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+    f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
-    const f4 mg = *reinterpret_cast<const f4*>(coef + c);
-    const f4 mgx = *reinterpret_cast<const f4*>(coef + C + c);
+    f4 mg = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + c);
+    f4 mgx = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + C + c);
 #pragma unroll 4
     for (int r = r0 + rl; r < r1; r += rstep) {
+      if (r >= gend) {
+        g = r / Mg;
+        gend = (g + 1) * Mg;
+        mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+        is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+        mg = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + c);
+        mgx = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + C + c);
+      }
       const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
       const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
       f4 o;
@@ -281,7 +315,8 @@ constexpr int SMALL_R = BN_SMALL_M / 256;
 __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const float* z, const float* beta, float eps,
                                                            float decay, int bessel, float* mm, float* mv,
                                                            float* save_mean, float* save_invstd, float* y, int ycs,
-                                                           int yco, int relu) {
+                                                           int yco, int relu, int G) {
+  // M = rows per group (<= BN_SMALL_M); the G groups run one after the other in the block
   __shared__ double sh[2][4][4];
   __shared__ float s_mu[4], s_is[4];
   const int c = bn_quad_block() * 4;
@@ -290,113 +325,128 @@ __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const f
   const f4 bt = *reinterpret_cast<const f4*>(beta + c);
   float mm0 = 0.f, mv0 = 0.f;
   if (threadIdx.x < 4 && mm) { mm0 = mm[c + threadIdx.x]; mv0 = mv[c + threadIdx.x]; }
-  f4 v[SMALL_R];
-  float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
+  for (int g = 0; g < G; ++g) {
+    const float* zg = z + (long)g * M * C;
+    f4 v[SMALL_R];
+    float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < SMALL_R; ++i) {
-    const int r = threadIdx.x + 256 * i;
-    v[i] = r < M ? *reinterpret_cast<const f4*>(z + (long)r * C + c) : f4{0, 0, 0, 0};
+    for (int i = 0; i < SMALL_R; ++i) {
+      const int r = threadIdx.x + 256 * i;
+      v[i] = r < M ? *reinterpret_cast<const f4*>(zg + (long)r * C + c) : f4{0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { fa[j] += v[i][j]; fb[j] += v[i][j] * v[i][j]; }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
-    if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    const int j = threadIdx.x, cc = c + j;
-    const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
-    const double s2 = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
-    const double mean = s / M;
-    double var = s2 / M - mean * mean;
-    if (var < 0) var = 0;
-    const float mu = (float)mean, is = (float)(1.0 / sqrt(var + (double)eps));
-    s_mu[j] = mu; s_is[j] = is;
-    save_mean[cc] = mu;
-    save_invstd[cc] = is;
-    if (mm) {
-      const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
-      mm[cc] = mm0 - (mm0 - mu) * (1.f - decay);
-      mv[cc] = mv0 - (mv0 - (float)vu) * (1.f - decay);
+      for (int j = 0; j < 4; ++j) { fa[j] += v[i][j]; fb[j] += v[i][j] * v[i][j]; }
     }
-  }
-  __syncthreads();
+    if (g > 0) __syncthreads();          // the previous group's apply has read s_mu / s_is
 #pragma unroll
-  for (int i = 0; i < SMALL_R; ++i) {
-    const int r = threadIdx.x + 256 * i;
-    if (r < M) {
-      f4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float t = (v[i][j] - s_mu[j]) * s_is[j] + bt[j];
-        o[j] = (relu && t < 0.f) ? 0.f : t;
+    for (int j = 0; j < 4; ++j) {
+      const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
+      if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int j = threadIdx.x, cc = c + j;
+      const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
+      const double s2 = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
+      const double mean = s / M;
+      double var = s2 / M - mean * mean;
+      if (var < 0) var = 0;
+      const float mu = (float)mean, is = (float)(1.0 / sqrt(var + (double)eps));
+      s_mu[j] = mu; s_is[j] = is;
+      save_mean[(long)g * C + cc] = mu;
+      save_invstd[(long)g * C + cc] = is;
+      if (mm) {
+        const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
+        mm0 = mm0 - (mm0 - mu) * (1.f - decay);
+        mv0 = mv0 - (mv0 - (float)vu) * (1.f - decay);
       }
-      *reinterpret_cast<f4*>(y + (long)r * ycs + yco + c) = o;
+    }
+    __syncthreads();
+    float* yg = y + (long)g * M * ycs;
+#pragma unroll
+    for (int i = 0; i < SMALL_R; ++i) {
+      const int r = threadIdx.x + 256 * i;
+      if (r < M) {
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float t = (v[i][j] - s_mu[j]) * s_is[j] + bt[j];
+          o[j] = (relu && t < 0.f) ? 0.f : t;
+        }
+        *reinterpret_cast<f4*>(yg + (long)r * ycs + yco + c) = o;
+      }
     }
   }
+  if (threadIdx.x < 4 && mm) { mm[c + threadIdx.x] = mm0; mv[c + threadIdx.x] = mv0; }
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const float* z, const float* mean,
                                                            const float* invstd, const float* beta, const float* dy,
                                                            int dycs, int dyco, float* dz, float* dbeta, int acc,
-                                                           int relu, float* amax) {
+                                                           int relu, float* amax, int G) {
+  // M = rows per group (<= BN_SMALL_M); the G groups run one after the other in the block; dbeta takes the
+  // groups' sums in group order (the first overwrites unless accumulating)
   __shared__ double sh[2][4][4];
   __shared__ float s_mg[4], s_mgx[4];
   const int c = bn_quad_block() * 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const f4 mu = *reinterpret_cast<const f4*>(mean + c);
-  const f4 is = *reinterpret_cast<const f4*>(invstd + c);
   const f4 bt = *reinterpret_cast<const f4*>(beta + c);
-  const float db0 = (threadIdx.x < 4 && dbeta && acc) ? dbeta[c + threadIdx.x] : 0.f;
-  f4 xr[SMALL_R], gr[SMALL_R];
-  float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < SMALL_R; ++i) {
-    const int r = threadIdx.x + 256 * i;
-    xr[i] = f4{0, 0, 0, 0}; gr[i] = f4{0, 0, 0, 0};
-    if (r < M) {
-      const f4 v = *reinterpret_cast<const f4*>(z + (long)r * C + c);
-      const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xh = (v[j] - mu[j]) * is[j];
-        const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
-        xr[i][j] = xh; gr[i][j] = g;
-        fa[j] += g; fb[j] += g * xh;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
-    if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    const int j = threadIdx.x;
-    const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
-    const double sx = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
-    s_mg[j] = (float)(s / M);
-    s_mgx[j] = (float)(sx / M);
-    if (dbeta) dbeta[c + j] = acc ? db0 + (float)s : (float)s;
-  }
-  __syncthreads();
+  float db = (threadIdx.x < 4 && dbeta && acc) ? dbeta[c + threadIdx.x] : 0.f;
+  bool first = !acc;
   float mx = 0.f;
+  for (int g = 0; g < G; ++g) {
+    const f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+    const f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+    const long row0 = (long)g * M;
+    f4 xr[SMALL_R], gr[SMALL_R];
+    float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < SMALL_R; ++i) {
-    const int r = threadIdx.x + 256 * i;
-    if (r < M) {
-      f4 o;
+    for (int i = 0; i < SMALL_R; ++i) {
+      const int r = threadIdx.x + 256 * i;
+      xr[i] = f4{0, 0, 0, 0}; gr[i] = f4{0, 0, 0, 0};
+      if (r < M) {
+        const f4 v = *reinterpret_cast<const f4*>(z + (row0 + r) * C + c);
+        const f4 gv = *reinterpret_cast<const f4*>(dy + (row0 + r) * dycs + dyco + c);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
-        mx = fmaxf(mx, fabsf(o[j]));
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (v[j] - mu[j]) * is[j];
+          const float gg = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
+          xr[i][j] = xh; gr[i][j] = gg;
+          fa[j] += gg; fb[j] += gg * xh;
+        }
       }
-      *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
+    }
+    if (g > 0) __syncthreads();          // the previous group's apply has read s_mg / s_mgx
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
+      if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int j = threadIdx.x;
+      const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
+      const double sx = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
+      s_mg[j] = (float)(s / M);
+      s_mgx[j] = (float)(sx / M);
+      db = first ? (float)s : db + (float)s;
+      first = false;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SMALL_R; ++i) {
+      const int r = threadIdx.x + 256 * i;
+      if (r < M) {
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
+          mx = fmaxf(mx, fabsf(o[j]));
+        }
+        *reinterpret_cast<f4*>(dz + (row0 + r) * C + c) = o;
+      }
     }
   }
+  if (threadIdx.x < 4 && dbeta) dbeta[c + threadIdx.x] = db;
   block_absmax_to(mx, amax);
 }
 
@@ -513,16 +563,17 @@ int apply_rows_per_block(int M, int C) {
 
 int finalize_blocks(int C) { return C / 4; }
 
+// M = rows per group; nparts = all groups' partials (G | nparts, group-major)
 template <int MODE>
 void finalize_launch(int nparts, int C, hipStream_t st, int M, const double* part, float eps, float decay, int bessel,
                      float* mm, float* mv, float* save_mean, float* save_invstd, float* dbeta, int acc, float* coef,
-                     double* sums) {
-  if (nparts <= 512)
+                     double* sums, int G = 1) {
+  if (nparts / G <= 512)
     hipLaunchKernelGGL((bn_finalize_kernel<MODE, 256>), dim3(finalize_blocks(C)), dim3(256), 0, st, M, C, nparts, part,
-                       eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums);
+                       eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G);
   else
     hipLaunchKernelGGL((bn_finalize_kernel<MODE, 1024>), dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, nparts,
-                       part, eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums);
+                       part, eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G);
 }
 
 }  // namespace
@@ -536,63 +587,86 @@ static long bn_env(const char* n, long d) { return tde_env_pos(n, d); }
 static const long g_bn_elems = bn_env("TDE_BN_ELEMS", 8192);
 static const long g_bn_maxch = bn_env("TDE_BN_MAXCH", 1024);
 
-BnChunks bn_chunk_plan(long M, int C, int work_mult) {
-  // ~g_bn_elems elements (x work_mult, e.g. split-K slabs) per block, <= g_bn_maxch chunks
+BnChunks bn_chunk_plan(long M, int C, int work_mult, int G) {
+  // ~g_bn_elems elements (x work_mult, e.g. split-K slabs) per block, <= g_bn_maxch chunks; with G row groups the
+  // same count split evenly over the groups (every chunk inside one group)
   BnChunks p;
   const int cq = C / 4;
   p.groups = (cq + 15) / 16;
   const int nq = cq < 16 ? cq : 16;
   const int ty_n = 256 / nq;
+  if (G < 1) G = 1;
+  const long Mg = M / G;
   long ch = M * (long)C * (work_mult > 1 ? work_mult : 1) / g_bn_elems / p.groups;
   if (ch > g_bn_maxch) ch = g_bn_maxch;
+  ch = ch / G;
   if (ch < 1) ch = 1;
-  long rpc = (M + ch - 1) / ch;
+  long rpc = (Mg + ch - 1) / ch;
   rpc = (rpc + ty_n - 1) / ty_n * ty_n;
   p.rows_per_chunk = (int)rpc;
-  p.chunks = (int)((M + rpc - 1) / rpc);
+  p.per_g = (int)((Mg + rpc - 1) / rpc);
+  p.Mg = (int)Mg;
+  p.chunks = p.per_g * G;
   return p;
 }
 
+size_t bn_part_bytes(long M, int C) {
+  // any plan of bn_chunk_plan(M, C, 1, G <= BN_MAX_GROUPS) has per_g <= max(1, ch / G) chunks per group, i.e. at
+  // most max(ch, G) partials (ch = the chunk target before the per-group split)
+  const long groups = (C / 4 + 15) / 16;
+  long n = M * (long)C / g_bn_elems / groups;
+  if (n > g_bn_maxch) n = g_bn_maxch;
+  if (n < BN_MAX_GROUPS) n = BN_MAX_GROUPS;
+  return (size_t)n * 2 * C * sizeof(double);
+}
+
 void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream_t st) {
-  hipLaunchKernelGGL(bn_fwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M, C, z, o.beta, o.eps, o.decay, o.bessel,
-                     o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu);
+  const int G = o.groups > 1 ? o.groups : 1;
+  hipLaunchKernelGGL(bn_fwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay, o.bessel,
+                     o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
 }
 
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
                                  hipStream_t st) {
-  finalize_launch<0>(nparts, C, st, M, part, o.eps, o.decay, o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, nullptr,
-                     0, nullptr, nullptr);
+  const int G = o.groups > 1 ? o.groups : 1;
+  finalize_launch<0>(nparts, C, st, M / G, part, o.eps, o.decay, o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd,
+                     nullptr, 0, nullptr, nullptr, G);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, o.save_mean,
-                     o.save_invstd, o.beta, o.relu, o.y, o.ycs, o.yco, rpb);
+                     o.save_invstd, o.beta, o.relu, o.y, o.ycs, o.yco, rpb, M / G);
+}
+
+void bn_fwd_standalone_launch(int M, int C, const float* z, const BnOut& o, double* part, hipStream_t st) {
+  const int G = o.groups > 1 ? o.groups : 1;
+  if (M / G <= BN_SMALL_M) {
+    bn_fwd_small_launch(M, C, z, o, st);
+    return;
+  }
+  const BnChunks pp = bn_chunk_plan(M, C, 1, G);
+  hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0, nullptr,
+                     nullptr, nullptr, 0, pp, part);
+  bn_fwd_from_partials_launch(M, C, z, pp.chunks, part, o, st);
 }
 
 extern "C" {
 
 size_t tde_bn_workspace_size(int M, int C) {
   if (M <= 0 || C <= 0 || C % 4) return 0;
-  return (size_t)bn_chunk_plan(M, C, 1).chunks * 2 * C * sizeof(double) + 2 * (size_t)C * sizeof(float) +
-         64;
+  return bn_part_bytes(M, C) + (size_t)BN_MAX_GROUPS * 2 * C * sizeof(float) + 64;
 }
 
-int tde_bn_fwd_train(int M, int C, const float* z, const float* beta, float eps, float decay, int bessel,
+int tde_bn_fwd_train(int M, int C, int groups, const float* z, const float* beta, float eps, float decay, int bessel,
                      float* moving_mean, float* moving_var, float* save_mean, float* save_invstd, float* y,
                      int y_cstride, int y_coff, int relu, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && beta && save_mean && save_invstd && y);
+  TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) && tde_aligned16(y));
   TDE_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const BnOut o{beta, eps, decay, bessel, moving_mean, moving_var, save_mean, save_invstd, y, y_cstride, y_coff, relu};
-  if (M <= BN_SMALL_M) {
-    bn_fwd_small_launch(M, C, z, o, st);
-    return tde_launch_status();
-  }
-  const BnChunks pp = bn_chunk_plan(M, C, 1);
-  double* part = reinterpret_cast<double*>(tde_ws_body(ws));
-  hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0, nullptr,
-                     nullptr, nullptr, 0, pp.rows_per_chunk, part);
-  bn_fwd_from_partials_launch(M, C, z, pp.chunks, part, o, st);
+  const BnOut o{beta, eps, decay, bessel, moving_mean, moving_var, save_mean, save_invstd, y, y_cstride, y_coff, relu,
+                groups};
+  bn_fwd_standalone_launch(M, C, z, o, reinterpret_cast<double*>(tde_ws_body(ws)), st);
   return tde_launch_status();
 }
 
@@ -616,28 +690,30 @@ int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const floa
   return tde_launch_status();
 }
 
-int tde_bn_bwd(int M, int C, const float* z, const float* save_mean, const float* save_invstd, const float* beta,
-               const float* dy, int dy_cstride, int dy_coff, float* dz, float* dbeta, int accumulate_dbeta, int relu,
-               float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
+int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean, const float* save_invstd,
+               const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz, float* dbeta,
+               int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && save_mean && save_invstd && beta && dy && dz);
+  TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (M <= BN_SMALL_M) {
-    hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M, C, z, save_mean, save_invstd, beta, dy,
-                       dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax);
+  const int G = groups, Mg = M / groups;
+  if (Mg <= BN_SMALL_M) {
+    hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / 4), dim3(256), 0, st, Mg, C, z, save_mean, save_invstd, beta, dy,
+                       dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax, G);
     return tde_launch_status();
   }
-  const BnChunks pp = bn_chunk_plan(M, C, 1);
+  const BnChunks pp = bn_chunk_plan(M, C, 1, G);
   double* part = reinterpret_cast<double*>(tde_ws_body(ws));
-  float* coef = reinterpret_cast<float*>(part + (size_t)pp.chunks * 2 * C);
+  float* coef = reinterpret_cast<float*>(tde_ws_body(ws) + bn_part_bytes(M, C));
   hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride, dy_coff,
-                     save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
-  finalize_launch<1>(pp.chunks, C, st, M, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta,
-                     coef, nullptr);
+                     save_mean, save_invstd, beta, relu, pp, part);
+  finalize_launch<1>(pp.chunks, C, st, Mg, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta,
+                     coef, nullptr, G);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
+                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax, Mg);
   return tde_launch_status();
 }
 
@@ -654,10 +730,10 @@ int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, i
   double* part = reinterpret_cast<double*>(tde_ws_body(ws));
   if (mode == 0)
     hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0,
-                       nullptr, nullptr, nullptr, 0, pp.rows_per_chunk, part);
+                       nullptr, nullptr, nullptr, 0, pp, part);
   else
     hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                       dy_coff, save_mean, save_invstd, beta, relu, pp.rows_per_chunk, part);
+                       dy_coff, save_mean, save_invstd, beta, relu, pp, part);
   finalize_launch<2>(pp.chunks, C, st, M, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
                      sums);
   return tde_launch_status();
@@ -674,7 +750,7 @@ int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const doubl
                      nullptr, eps, decay, bessel, moving_mean, moving_var, save_mean, save_invstd, nullptr, 0, nullptr);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, save_mean, save_invstd,
-                     beta, relu, y, y_cstride, y_coff, rpb);
+                     beta, relu, y, y_cstride, y_coff, rpb, M);
   return tde_launch_status();
 }
 
@@ -692,7 +768,7 @@ int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float
                      local_sums, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
   const int rpb = apply_rows_per_block(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax);
+                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax, M);
   return tde_launch_status();
 }
 

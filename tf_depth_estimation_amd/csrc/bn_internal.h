@@ -4,10 +4,13 @@
 #pragma once
 #include "tde_common.h"
 
-constexpr int BN_SMALL_M = 2048;   // rows of the single-kernel BN path
+constexpr int BN_SMALL_M = 2048;   // rows (per row group) of the single-kernel BN path
+constexpr int BN_MAX_GROUPS = 8;   // row groups of a grouped BN (tde_bn_train_t.groups)
 
 // What a training-mode BN forward writes: statistics, moving averages (mm/mv null: no update) and
-// y = relu?((z - mean) * invstd + beta) into a channel view.
+// y = relu?((z - mean) * invstd + beta) into a channel view.  groups G >= 1: the M rows are G equal consecutive
+// row groups, each normalised over its own rows (G slim.batch_norm calls of one shared-variable network batched
+// into one launch); save_mean / save_invstd are [G][C] and the moving averages take G updates in group order.
 struct BnOut {
   const float* beta;
   float eps, decay;
@@ -15,20 +18,34 @@ struct BnOut {
   float *mm, *mv, *save_mean, *save_invstd;
   float* y;
   int ycs, yco, relu;
+  int groups;
 };
 
 // Row-chunk x 64-channel-group grid of the partial-statistics passes (bn.hip and the conv's split-K
-// reduce): `chunks` fp64 partials [chunk][2][C].
+// reduce): `chunks` fp64 partials [chunk][2][C]; with row groups, `per_g` chunks per group of Mg rows (chunk
+// k covers rows (k / per_g) * Mg + (k % per_g) * rows_per_chunk .. of its group), so every partial belongs to
+// exactly one group and group g owns partials [g * per_g, (g + 1) * per_g).
 struct BnChunks {
   int chunks, rows_per_chunk, groups;
+  int per_g, Mg;
 };
-BnChunks bn_chunk_plan(long M, int C, int work_mult);
+BnChunks bn_chunk_plan(long M, int C, int work_mult, int G = 1);
+__device__ __forceinline__ void bn_chunk_rows(const BnChunks& p, int k, int& r0, int& r1) {
+  const int gi = k / p.per_g, kk = k - gi * p.per_g;
+  r0 = gi * p.Mg + kk * p.rows_per_chunk;
+  r1 = min(gi * p.Mg + p.Mg, r0 + p.rows_per_chunk);
+}
+// fp64 partial bytes a grouped standalone forward / backward BN of M rows x C channels may use
+size_t bn_part_bytes(long M, int C);
 
-// M <= BN_SMALL_M: statistics + finalize + apply in one launch.
+// Mg <= BN_SMALL_M: statistics + finalize + apply in one launch.
 void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream_t st);
-// From `nparts` fp64 partials [part][2][C] of z: finalize (one small launch) + apply (one launch).
+// From `nparts` fp64 partials [part][2][C] of z (G | nparts, group-aligned): finalize (one small launch) + apply
+// (one launch).
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
                                  hipStream_t st);
+// The whole training-mode forward BN of z (partials computed here): small path or partials + finalize + apply.
+void bn_fwd_standalone_launch(int M, int C, const float* z, const BnOut& o, double* part, hipStream_t st);
 
 // Row-lane combine of the partial-sum kernels (bn_part_kernel, splitk_reduce_bn_kernel): thread = ty * nq + tx
 // (256 threads, nq channel quads), s0 / s1 its 4-channel sums.  Leaves the block's sums for quad tx in the

@@ -1168,18 +1168,27 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
 //   BN_SMALL : <= 2048 output rows -- [split-K reduce], then one BN kernel (bn.hip) does it all;
 //   BN_EPI   : no split -- the conv epilogue writes one fp64 partial per row tile;
 //   BN_REDUCE: split-K -- the reduce kernel writes z and one partial per row chunk;
+//   BN_STANDALONE: row groups (tde_bn_train_t.groups > 1) the tiles above would straddle -- [split-K reduce], then
+//              bn.hip's grouped partial pass over z;
 // then bn.hip finalizes and applies (two launches).
-enum { BN_SMALL = 0, BN_EPI = 1, BN_REDUCE = 2 };
+enum { BN_SMALL = 0, BN_EPI = 1, BN_REDUCE = 2, BN_STANDALONE = 3 };
 struct BnPlan {
   int path, nparts;
   BnChunks ch;
   size_t part_bytes;
 };
 
-static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl) {
+static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl, int G = 1) {
   BnPlan b{};
-  if (pl.rows <= BN_SMALL_M) {
+  if (G < 1) G = 1;
+  const int Mg = pl.rows / G;
+  if (Mg <= BN_SMALL_M) {
     b.path = BN_SMALL;
+  } else if (G > 1 && (pl.splits > 1 || mode == MODE_DGRAD || Mg % pl.bm != 0)) {
+    // row groups whose boundaries the epilogue's row tiles (or a deconv's parity-class tiles) do not respect:
+    // the statistics come from a separate grouped partial pass over z
+    b.path = BN_STANDALONE;
+    b.nparts = 0;
   } else if (pl.splits == 1) {
     b.path = BN_EPI;
     if (mode == MODE_DGRAD)
@@ -1196,6 +1205,9 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl) {
     b.nparts = b.ch.chunks;
   }
   b.part_bytes = (size_t)b.nparts * 2 * pl.cols * sizeof(double);
+  // room for the grouped standalone statistics pass (any G: the workspace query does not know it)
+  const size_t sa = bn_part_bytes(pl.rows, pl.cols);
+  if (sa > b.part_bytes) b.part_bytes = sa;
   return b;
 }
 
@@ -1207,7 +1219,12 @@ static size_t halo_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   for (int math = 3; math <= 4; ++math) {
     HaloPlan hp;
     if (mode == MODE_WGRAD || !halo_plan(d, mode == MODE_FWD ? 0 : 1, math, hp)) continue;
-    const size_t m = hp.wbytes + (bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0);
+    size_t pb = bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0;
+    if (bn) {
+      const long Mz = (long)d.N * (mode == MODE_FWD ? (long)d.OH * d.OW : (long)d.H * d.W);
+      if (bn_part_bytes(Mz, hp.Ncols) > pb) pb = bn_part_bytes(Mz, hp.Ncols);
+    }
+    const size_t m = hp.wbytes + pb;
     b = m > b ? m : b;
   }
   return b;
@@ -1384,24 +1401,33 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   HaloPlan hp;
   if (MODE != MODE_WGRAD && halo_plan(*d, MODE == MODE_FWD ? 0 : 1, g_conv_math, hp)) {
     // stride-1, few-channel, high-resolution layer: halo-tiled kernel (halo_conv.hip)
-    const size_t pbytes = bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0;
+    const int G = bn && bn->groups > 1 ? bn->groups : 1;
+    const long Mz = (long)d->N * (MODE == MODE_FWD ? (long)d->OH * d->OW : (long)d->H * d->W);
+    // halo partials are image-major (one per pixel tile of one image): group-aligned when G divides N
+    if (Mz % G != 0) return TDE_ERR_ARG;
+    const bool grouped_sa = G > 1 && (d->N % G != 0 || Mz / G <= BN_SMALL_M);
+    size_t pbytes = bn ? (size_t)hp.nparts * 2 * hp.Ncols * sizeof(double) : 0;
+    if (bn && bn_part_bytes(Mz, hp.Ncols) > pbytes) pbytes = bn_part_bytes(Mz, hp.Ncols);
     if (hp.wbytes + pbytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
     char* body = tde_ws_body(ws);
     double* part = bn ? reinterpret_cast<double*>(body + hp.wbytes) : nullptr;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const float* in = MODE == MODE_FWD ? a.x : a.dy;
     float* z = MODE == MODE_FWD ? a.y : a.dx;
-    if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, part, st, a.bias, a.relu);
+    if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, grouped_sa ? nullptr : part, st, a.bias, a.relu);
     if (bn) {
       const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
-                    bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu};
-      bn_fwd_from_partials_launch(d->N * d->H * d->W, hp.Ncols, z, hp.nparts, part, o, st);
+                    bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
+      if (grouped_sa) bn_fwd_standalone_launch((int)Mz, hp.Ncols, z, o, part, st);
+      else bn_fwd_from_partials_launch((int)Mz, hp.Ncols, z, hp.nparts, part, o, st);
     }
     return tde_launch_status();
   }
   const Plan pl = make_plan(*d, MODE);
   BnPlan bp{};
-  if (bn) bp = bn_plan(*d, MODE, pl);
+  const int G = bn && bn->groups > 1 ? bn->groups : 1;
+  if (pl.rows % G != 0) return TDE_ERR_ARG;
+  if (bn) bp = bn_plan(*d, MODE, pl, G);
   if (pl.ws_bytes + bp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   double* part = reinterpret_cast<double*>(body + pl.slab_bytes);
@@ -1418,9 +1444,11 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   if (bn) {
     // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
     const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
-                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu};
+                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
     if (bp.path == BN_SMALL) {
       bn_fwd_small_launch(pl.rows, pl.cols, z, o, st);
+    } else if (bp.path == BN_STANDALONE) {
+      bn_fwd_standalone_launch(pl.rows, pl.cols, z, o, part, st);
     } else {
       if (bp.path == BN_REDUCE && !skipr)
         hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws,
@@ -1555,7 +1583,8 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
 }
 
 static bool bn_ok(const tde_bn_train_t* bn, int C) {
-  return bn && bn->beta && bn->save_mean && bn->save_invstd && bn->y && C <= 1024 &&
+  return bn && bn->beta && bn->save_mean && bn->save_invstd && bn->y && C <= 1024 && bn->groups >= 0 &&
+         bn->groups <= BN_MAX_GROUPS &&
          ((bn->moving_mean == nullptr) == (bn->moving_var == nullptr)) && bn->y_cstride % 4 == 0 &&
          bn->y_coff % 4 == 0 && bn->y_coff + C <= bn->y_cstride && tde_aligned16(bn->y) && tde_aligned16(bn->beta);
 }

@@ -41,8 +41,30 @@ __device__ __forceinline__ Tap4 taps(float u, float v, int W, int H) {
   return t;
 }
 
-template <bool NEED_G_P>
-__global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a) {
+// Deterministic mode (tde_warp_loss_t.det_ws != NULL): the consistency term's gather gradient is scattered as
+// 64-bit fixed-point integers (integer addition is associative: the sum is the same in any order), scaled so
+// that no destination can overflow: |sum| <= H*W * bound, bound = consist_w/(B*H*W) * max(1/disp_other)^2
+// (warp_det_prep_kernel), scale = 2^(62 - ceil(log2(H*W*bound))); warp_det_finish_kernel adds the sums into
+// g_other once.  The loss parts and dL/dP leave each block as partial rows reduced in block order (no fp64
+// atomics).  Layout of det_ws: [B*H*W] int64 scatter sums | [blocks][15] fp64 partials | 4 B bound slot.
+struct WarpDet {
+  long long* acc;      // [B*H*W] fixed-point scatter sums (zeroed by the prep kernel)
+  double* part;        // [gridDim.x * B][15]
+  unsigned* bound;     // max over the other view of (1/disp)^2, float bits (atomicMax: order-independent)
+};
+
+__device__ __forceinline__ double det_scale(const tde_warp_loss_t& a, const WarpDet& d) {
+  const double mo2 = (double)__uint_as_float(*d.bound);
+  const double hw = (double)a.H * a.W;
+  const double lim = hw * (double)a.consist_w / ((double)a.B * hw) * mo2;
+  if (!(lim > 0.0) || !isfinite(lim)) return 1.0;
+  int e;
+  frexp(lim, &e);                         // lim < 2^e
+  return ldexp(1.0, 62 - e);
+}
+
+template <bool NEED_G_P, bool DET>
+__global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a, const WarpDet det) {
   __shared__ double sh[16][4];
   const int b = blockIdx.y;
   const int HW = a.H * a.W;
@@ -53,6 +75,7 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
 #pragma unroll
   for (int i = 0; i < 12; ++i) gp[i] = 0.0;
   const double inv_n3 = 1.0 / (3.0 * a.B * HW), inv_n = 1.0 / ((double)a.B * HW);
+  const double dscale = DET ? det_scale(a, det) : 0.0;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < HW; idx += gridDim.x * blockDim.x) {
     const int y = idx / a.W, x = idx - y * a.W;
     const long pix = (long)b * HW + idx;
@@ -153,10 +176,21 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
         const float* Dd = Do;
         const long i00 = ((long)t.y0 * a.W + t.x0) * a.other_cs, i01 = ((long)t.y1 * a.W + t.x0) * a.other_cs;
         const long i10 = ((long)t.y0 * a.W + t.x1) * a.other_cs, i11 = ((long)t.y1 * a.W + t.x1) * a.other_cs;
-        if (w00 != 0.f) atomicAdd(Go + i00, -g_o * w00 * o00 * o00);
-        if (w01 != 0.f) atomicAdd(Go + i01, -g_o * w01 * o01 * o01);
-        if (w10 != 0.f) atomicAdd(Go + i10, -g_o * w10 * o10 * o10);
-        if (w11 != 0.f) atomicAdd(Go + i11, -g_o * w11 * o11 * o11);
+        if (DET) {
+          // fixed-point integer scatter into det.acc (dense [B*H*W], one value per pixel of the other view)
+          unsigned long long* A = reinterpret_cast<unsigned long long*>(det.acc) + (long)b * HW;
+          const long j00 = (long)t.y0 * a.W + t.x0, j01 = (long)t.y1 * a.W + t.x0;
+          const long j10 = (long)t.y0 * a.W + t.x1, j11 = (long)t.y1 * a.W + t.x1;
+          if (w00 != 0.f) atomicAdd(A + j00, (unsigned long long)llrint((double)(-g_o * w00 * o00 * o00) * dscale));
+          if (w01 != 0.f) atomicAdd(A + j01, (unsigned long long)llrint((double)(-g_o * w01 * o01 * o01) * dscale));
+          if (w10 != 0.f) atomicAdd(A + j10, (unsigned long long)llrint((double)(-g_o * w10 * o10 * o10) * dscale));
+          if (w11 != 0.f) atomicAdd(A + j11, (unsigned long long)llrint((double)(-g_o * w11 * o11 * o11) * dscale));
+        } else {
+          if (w00 != 0.f) atomicAdd(Go + i00, -g_o * w00 * o00 * o00);
+          if (w01 != 0.f) atomicAdd(Go + i01, -g_o * w01 * o01 * o01);
+          if (w10 != 0.f) atomicAdd(Go + i10, -g_o * w10 * o10 * o10);
+          if (w11 != 0.f) atomicAdd(Go + i11, -g_o * w11 * o11 * o11);
+        }
         (void)Dd;
       }
     }
@@ -204,11 +238,60 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a)
   if (threadIdx.x < nv) {
     const int i = threadIdx.x;
     const double s = sh[i][0] + sh[i][1] + sh[i][2] + sh[i][3];
-    if (i < 3) {
+    if (DET) {
+      det.part[((long)b * gridDim.x + blockIdx.x) * 15 + i] = s;
+    } else if (i < 3) {
       if (s != 0.0) atomicAdd(a.loss + i, s);
     } else {
       atomicAdd(a.g_P + 12 * b + (i - 3), s);
     }
+  }
+}
+
+// Deterministic mode, before the loss kernel: zero the fixed-point sums and raise the bound slot to
+// max (1/disp_other)^2 (atomicMax on the float bits of non-negative values: order-independent).
+__global__ void __launch_bounds__(256) warp_det_prep_kernel(const tde_warp_loss_t a, const WarpDet det, long n) {
+  float m = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += 256L * gridDim.x) {
+    det.acc[i] = 0;
+    if (a.disp_other) {
+      const float o = 1.f / a.disp_other[i * a.other_cs + a.other_co];
+      m = fmaxf(m, o * o);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(det.bound, __float_as_uint(m));
+}
+
+// Deterministic mode, after the loss kernel: g_other += fixed-point sums / scale (one add per pixel), and the
+// last block sums the per-block partials of the loss parts and dL/dP in block order.
+__global__ void __launch_bounds__(256) warp_det_finish_kernel(const tde_warp_loss_t a, const WarpDet det, long n,
+                                                              int gx, int nv) {
+  if (blockIdx.x == gridDim.x - 1) {
+    // loss parts (3) and dL/dP (12 per batch element), fixed order over blocks
+    for (int i = threadIdx.x; i < 3 + 12 * a.B; i += 256) {
+      if (i < 3) {
+        double s = 0.0;
+        for (int bb = 0; bb < a.B; ++bb)
+          for (int x = 0; x < gx; ++x) s += det.part[((long)bb * gx + x) * 15 + i];
+        if (s != 0.0) a.loss[i] += s;
+      } else if (nv == 15) {
+        const int bb = (i - 3) / 12, k = (i - 3) % 12;
+        double s = 0.0;
+        for (int x = 0; x < gx; ++x) s += det.part[((long)bb * gx + x) * 15 + 3 + k];
+        a.g_P[12 * bb + k] += s;
+      }
+    }
+    return;
+  }
+  if (!a.g_other) return;
+  const double inv = 1.0 / det_scale(a, det);
+  const int HW = a.H * a.W;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += 256L * (gridDim.x - 1)) {
+    const long b = i / HW, idx = i - b * HW;
+    float* g = a.g_other + (b * HW + idx) * a.other_cs + a.other_co;
+    *g += (float)((double)det.acc[i] * inv);
   }
 }
 
@@ -658,9 +741,37 @@ int tde_warp_loss(const tde_warp_loss_t* a, void* stream) {
   if (gx > cap) gx = cap;
   dim3 grid(gx, a->B);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (a->g_P && a->disp) hipLaunchKernelGGL(warp_loss_kernel<true>, grid, dim3(256), 0, st, *a);
-  else hipLaunchKernelGGL(warp_loss_kernel<false>, grid, dim3(256), 0, st, *a);
+  const bool gp = a->g_P && a->disp;
+  if (a->det_ws == nullptr) {
+    const WarpDet none{nullptr, nullptr, nullptr};
+    if (gp) hipLaunchKernelGGL((warp_loss_kernel<true, false>), grid, dim3(256), 0, st, *a, none);
+    else hipLaunchKernelGGL((warp_loss_kernel<false, false>), grid, dim3(256), 0, st, *a, none);
+    return tde_launch_status();
+  }
+  const long n = (long)a->B * a->H * a->W;
+  if (a->det_ws_bytes < tde_warp_loss_det_workspace_size(a->B, a->H, a->W) || !tde_aligned16(a->det_ws))
+    return TDE_ERR_WORKSPACE;
+  char* w = static_cast<char*>(a->det_ws);
+  WarpDet det;
+  det.acc = reinterpret_cast<long long*>(w);
+  det.part = reinterpret_cast<double*>(w + 8 * n);
+  det.bound = reinterpret_cast<unsigned*>(w + 8 * n + 8L * 15 * gx * a->B);
+  const int pb = (int)std::min<long>(1024, (n + 255) / 256);
+  if (hipMemsetAsync(det.bound, 0, 4, st) != hipSuccess) return TDE_ERR_HIP;
+  hipLaunchKernelGGL(warp_det_prep_kernel, dim3(pb), dim3(256), 0, st, *a, det, n);
+  if (gp) hipLaunchKernelGGL((warp_loss_kernel<true, true>), grid, dim3(256), 0, st, *a, det);
+  else hipLaunchKernelGGL((warp_loss_kernel<false, true>), grid, dim3(256), 0, st, *a, det);
+  hipLaunchKernelGGL(warp_det_finish_kernel, dim3(pb + 1), dim3(256), 0, st, *a, det, n, gx, gp ? 15 : 3);
   return tde_launch_status();
+}
+
+size_t tde_warp_loss_det_workspace_size(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  static const long maxb = tde_env_pos("TDE_WARP_MAXB", 512);
+  long gx = ((long)H * W + 255) / 256;
+  const long cap = std::max(1L, maxb / B);
+  if (gx > cap) gx = cap;
+  return (size_t)(8L * B * H * W + 8L * 15 * gx * B + 16);
 }
 
 int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const float* K, float* T, float* P,

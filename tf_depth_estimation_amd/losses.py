@@ -127,9 +127,10 @@ def area(src, dst):
 
 def warp_loss(acc, slot0, img_src, img_tgt, P=None, Kinv=None, disp=None, flow=None, wmask=None, logits=None,
               disp_other=None, photo_w=0.0, exp_w=0.0, consist_w=0.0, g_disp=None, g_flow=None, g_logits=None,
-              g_other=None, g_P=None):
+              g_other=None, g_P=None, det_ws=None):
     """One direction of the fused projective-warp loss head (include/tde.h tde_warp_loss).  All NHWC
-    tensors are dense; acc[slot0 .. slot0+2] += (photo, exp, consist)."""
+    tensors are dense; acc[slot0 .. slot0+2] += (photo, exp, consist).  det_ws: a device buffer of at least
+    tde_warp_loss_det_workspace_size bytes selects the deterministic (run-to-run bit-identical) scatter."""
     B, H, W, _ = img_tgt.shape
     a = WarpLossArgs()
     a.B, a.H, a.W = B, H, W
@@ -146,7 +147,16 @@ def warp_loss(acc, slot0, img_src, img_tgt, P=None, Kinv=None, disp=None, flow=N
     a.photo_w, a.exp_w, a.consist_w = photo_w, exp_w, consist_w
     a.loss = dptr(acc, slot0)
     a.g_disp, a.g_flow, a.g_logits, a.g_other, a.g_P = ptr(g_disp), ptr(g_flow), ptr(g_logits), ptr(g_other), ptr(g_P)
+    if det_ws is not None:
+        a.det_ws, a.det_ws_bytes = ptr(det_ws), det_ws.numel() * det_ws.element_size()
     _lib.call("tde_warp_loss", ctypes.byref(a), _lib.stream_ptr())
+
+
+def det_workspace(B, H, W):
+    """Device buffer for the deterministic warp-loss scatter of one (B, H, W) call (reusable by every later call on
+    the same stream at that size or smaller: each call consumes it entirely before it returns)."""
+    n = _lib.load().tde_warp_loss_det_workspace_size(B, H, W)
+    return torch.empty((n + 15) // 16 * 4, device="cuda", dtype=torch.float32)
 
 
 def pose_prep(K, T=None, P=None, Kinv=None, vec=None, mat=None):

@@ -244,10 +244,19 @@ class Workspace:
 
 class NetRun:
     """Per-invocation state of a program: activations, pre-BN outputs and batch statistics (the
-    'tape' the backward pass needs)."""
+    'tape' the backward pass needs).
 
-    def __init__(self, prog, N, device="cuda"):
-        self.prog, self.N, self.device = prog, N, device
+    groups G > 1: the batch holds G equal consecutive sub-batches that are G separate calls of the network in the
+    reference (shared variables, separate BatchNorm batches: disp_net on the left and on the right image,
+    train_depth_then_cam_lr.py:130-136).  Every conv runs ONCE over all N rows (weights shared, twice the rows of
+    the deep levels' GEMMs in one launch), every BatchNorm normalises each sub-batch over its own rows (tde_bn_*
+    groups), and one backward call yields the sum of the calls' parameter gradients -- what TF computes for the
+    shared variables."""
+
+    def __init__(self, prog, N, device="cuda", groups=1):
+        if groups < 1 or N % groups:
+            raise ValueError(f"batch {N} is not {groups} equal groups")
+        self.prog, self.N, self.device, self.groups = prog, N, device, groups
         self.act = {}
         for b in prog.spec.bufs:
             shape = (N, b.H, b.W, b.cs)
@@ -257,7 +266,7 @@ class NetRun:
         for i, op in enumerate(prog.spec.ops):
             if isinstance(op, ConvBN) and op.bn:
                 self.z[i] = torch.empty(op.zshape(N), device=device, dtype=torch.float32)
-                self.stats[i] = torch.empty((2, op.K), device=device, dtype=torch.float32)
+                self.stats[i] = torch.empty((2, groups * op.K), device=device, dtype=torch.float32)
             elif isinstance(op, ConvBN):
                 self.z[i] = None
         # per-op bound max|dz| of the BN backward's output (tde_bn_bwd dz_absmax), the gradient operand bound
@@ -542,6 +551,8 @@ class NetProgram:
         if fold_bn and (is_training or self._folded is None):
             raise ValueError("fold_bn needs is_training=False and weights folded by fold_bn()")
         N = run.N
+        if self.bn_sync is not None and run.groups > 1:
+            raise NotImplementedError("SyncBN over row-grouped runs")
         lib = _lib.load()
         st = _lib.stream_ptr()
         spec = self.spec
@@ -616,7 +627,7 @@ class NetProgram:
                     # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
                     # consumes the conv's split-K partials directly
                     bn = _lib.BnTrain(ptr(beta), 1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
-                                      ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1)
+                                      ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, run.groups)
                     fn = lib.tde_deconv2d_fwd_bn if op.deconv else lib.tde_conv2d_fwd_bn
                     _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb, st),
                                op.layer)
@@ -627,7 +638,8 @@ class NetProgram:
                     with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
                         _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
                     with self._span("bn_fwd"):
-                        _lib.check(lib.tde_bn_fwd_train(M, op.K, ptr(z), ptr(beta), 1e-3, op.decay, int(self.bessel),
+                        _lib.check(lib.tde_bn_fwd_train(M, op.K, run.groups, ptr(z), ptr(beta), 1e-3, op.decay,
+                                                        int(self.bessel),
                                                         ptr(mm), ptr(mv), ptr(sm[0]), ptr(sm[1]), run.vptr(op.dst),
                                                         op.dst.buf.cs, op.dst.coff, 1, ptr(ws), wsb, st), op.layer)
                 else:
@@ -752,7 +764,7 @@ class NetProgram:
                                                         run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " syncbn bwd")
                 else:
                     with self._span("bn_bwd"):
-                        _lib.check(lib.tde_bn_bwd(M, op.K, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
+                        _lib.check(lib.tde_bn_bwd(M, op.K, run.groups, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
                                                   ptr(self.P(f"{op.layer}/BatchNorm/beta")), run.vptr(op.dst, True),
                                                   op.dst.buf.cs, op.dst.coff, ptr(dz),
                                                   ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,

@@ -238,6 +238,18 @@ class Trainer:
     dadam = None
     net_stream = None        # enable_net_overlap: the second program's calls on their own stream
 
+    det_ws = None            # enable_deterministic: workspace of the deterministic warp-loss scatter
+
+    def enable_deterministic(self, on=True):
+        """Run-to-run bit-identical steps: the warp loss head's scatter-add into the other view's disparity
+        gradient (utils_lr.py:330-366 gather -> UnsortedSegmentSum in the reference) and its loss / dL/dP block
+        sums use the fixed-point / fixed-order mode of tde_warp_loss (det_ws) instead of float atomics.  Every
+        other kernel of the step is already order-deterministic (fixed-order split-K / BN / head reductions).
+        Call before capture()."""
+        from . import losses as Ls
+        self.det_ws = Ls.det_workspace(self.N, self.H, self.W) if on else None
+        return self
+
     def enable_net_overlap(self, on=True):
         """Single GPU: run the calls of one network program concurrently with those of the other on a second
         stream (config 4: `depth_net` on both pairs beside `disp_net` on both images, forward and backward;
@@ -559,15 +571,22 @@ class DepthThenCamTrainer(Trainer):
     `depth_net` (nets_optflow_depth_pairtest) on concat(L,R) and concat(R,L) (:142-154), and per scale
     (:211-340): smoothness of 1/disp on the 4 maps, depth L1 with replace_nonfinite on the single left
     net, explainability-masked photometric warp + exp CE + left-right depth consistency in both
-    directions, cam loss at s = 0; total (:355); Adam over both nets (:413-417)."""
+    directions, cam loss at s = 0; total (:355); Adam over both nets (:413-417).
+
+    twin=True (default): each network's two calls run as ONE row-grouped call of batch 2B (NetRun groups=2):
+    [left; right] images through disp_net, [concat(L,R); concat(R,L)] through depth_net -- every conv once over
+    both sub-batches (the deep levels' GEMMs get twice the rows per launch, half the launches), every BatchNorm
+    per sub-batch (the reference's separate BN batches), one backward per network summing both calls' parameter
+    gradients.  twin=False: the four separate calls (the reference's literal schedule)."""
 
     SLOTS = dict(smooth=0, depth=1, photo=2, exp=3, consist=4, cam=5)
-    BACKWARD_USES = 2        # each net runs on both images (shared variables)
 
-    def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None):
+    def __init__(self, batch, H=192, W=256, lr=2e-4, beta1=0.9, weights=None, twin=True):
         from .losses import W_CONFIG4, Arena, new
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG4
+        self.twin = bool(twin)
+        self.BACKWARD_USES = 1 if self.twin else 2     # backward calls per chunk per step
         with variables.variable_scope("model_singledepth"):
             self.single = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
                                            offset=0.0)
@@ -576,37 +595,59 @@ class DepthThenCamTrainer(Trainer):
         self.chunks = [self.single.chunk, self.pair.chunk]
         self.opt = MultiAdam(self.chunks, lr, beta1)
         B = batch
-        self.runs = {k: NetRun(p, B) for k, p in (("sl", self.single), ("sr", self.single), ("pl", self.pair),
-                                                   ("pr", self.pair))}
-        self.img = {"l": new((B, H, W, 3)), "r": new((B, H, W, 3))}
+        so, po = self.single.spec.outputs, self.pair.spec.outputs
+        if self.twin:
+            self.runs = {"s": NetRun(self.single, 2 * B, groups=2), "p": NetRun(self.pair, 2 * B, groups=2)}
+            # images: [left; right] in one tensor, the single net's batched input; the pair net's input
+            # [concat(L,R); concat(R,L)] (:146,152)
+            self.img_lr = new((2 * B, H, W, 3))
+            self.img = {"l": self.img_lr[:B], "r": self.img_lr[B:]}
+            self.pair_in = new((2 * B, H, W, 6))
+        else:
+            self.runs = {k: NetRun(p, B) for k, p in (("sl", self.single), ("sr", self.single), ("pl", self.pair),
+                                                       ("pr", self.pair))}
+            self.img = {"l": new((B, H, W, 3)), "r": new((B, H, W, 3))}
+            self.pair_in = {"lr": new((B, H, W, 6)), "rl": new((B, H, W, 6))}
         self.label = new((B, H, W, 1))
         self.K = new((B, 4, 3, 3))
         self.gt_cam = new((B, 6))
-        self.pair_in = {"lr": new((B, H, W, 6)), "rl": new((B, H, W, 6))}
-        self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
+        if self.twin:
+            # both images' area pyramids in one launch per scale (halves of [2B, H>>s, W>>s, 3] tensors)
+            self.pyr_lr = [self.img_lr] + [new(s) for s in _scale_shapes(2 * B, H, W, 3)[1:]]
+            self.pyr = {"l": [t[:B] for t in self.pyr_lr], "r": [t[B:] for t in self.pyr_lr]}
+        else:
+            self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
         self.Ks = [new((B, 9)) for _ in range(4)]
-        so, po = self.single.spec.outputs, self.pair.spec.outputs
         self.pose = {"lr": new((B, 6)), "rl": new((B, 6))}
         self.g_pose = {"lr": new((B, 6)), "rl": new((B, 6))}
         self.T = {"lr": new((B, 16)), "rl": new((B, 16))}
         self.P = {d: [new((B, 12)) for _ in range(4)] for d in ("lr", "rl")}
         self.Kinv = [new((B, 9)) for _ in range(4)]
-        # everything the loss head accumulates into (loss parts, dL/dP, dL/dT, the four runs' output
-        # gradients) lives in one arena: one zeroing launch per step; the output gradients are the runs'
-        # own gradient buffers (backward reads them in place)
+        # everything the loss head accumulates into (loss parts, dL/dP, dL/dT, the runs' output gradients) lives
+        # in one arena: one zeroing launch per step; the output gradients are the runs' own gradient buffers
+        # (backward reads them in place)
         ar = Arena()
         ia = ar.new((8,), torch.float64)
         igp = {d: ar.new((4, B, 12), torch.float64) for d in ("lr", "rl")}
         igt = {d: ar.new((B, 16)) for d in ("lr", "rl")}
-        ido = {k: [ar.new((B, v.H, v.W, v.C)) for v in (so if k[0] == "s" else po)] for k in self.runs}
+        nb = 2 * B if self.twin else B
+        ido = {k: [ar.new((nb, v.H, v.W, v.C)) for v in (so if k[0] == "s" else po)] for k in self.runs}
         t = ar.finalize()
         self.arena = ar
         self.acc = t[ia]
         self.gP = {d: t[i] for d, i in igp.items()}
         self.gT = {d: t[i] for d, i in igt.items()}
-        self.d_out = {k: [t[i] for i in idx] for k, idx in ido.items()}
+        d_run = {k: [t[i] for i in idx] for k, idx in ido.items()}
         for k, run in self.runs.items():
-            run.bind_output_grads(self.d_out[k])
+            run.bind_output_grads(d_run[k])
+        if self.twin:
+            # the loss head addresses the four calls' outputs / output gradients as the halves of the batched runs
+            self.d_run = d_run
+            self.d_out = {}
+            for k, half in (("sl", 0), ("sr", 1), ("pl", 0), ("pr", 1)):
+                self.d_out[k] = [g[half * B:(half + 1) * B] for g in d_run[k[0]]]
+        else:
+            self.d_out = d_run
 
     def set_batch(self, img_l, img_r, label, K, gt_cam):
         """img_* [B,H,W,3] in [-0.5,0.5]; label = inverse depth [B,H,W,1] (NaN holes allowed);
@@ -636,31 +677,52 @@ class DepthThenCamTrainer(Trainer):
         self.arena.zero()
         # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
         for key, (a, b) in (("lr", ("l", "r")), ("rl", ("r", "l"))):
-            dst = self.pair_in[key]
+            if self.twin:
+                dst = self.pair_in[:self.N] if key == "lr" else self.pair_in[self.N:]
+            else:
+                dst = self.pair_in[key]
             _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[a]), 3, 0, ptr(dst), 6, 0, 0, st), "concat")
             _lib.check(lib.tde_copy_view(M, 3, ptr(self.img[b]), 3, 0, ptr(dst), 6, 3, 0, st), "concat")
 
+    def _halves(self, net, outs):
+        """Twin run outputs -> the two calls' outputs: net "s" -> "sl" (left image) / "sr", "p" -> "pl" (pair L,R)
+        / "pr" (pair R,L)."""
+        B = self.N
+        return {net + "l": [o[:B] for o in outs], net + "r": [o[B:] for o in outs]}
+
     def _p_fwd_pair(self):
-        self._out["pl"] = self.pair.forward(self.runs["pl"], self.pair_in["lr"])
-        self._out["pr"] = self.pair.forward(self.runs["pr"], self.pair_in["rl"])
+        if self.twin:
+            self._out.update(self._halves("p", self.pair.forward(self.runs["p"], self.pair_in)))
+        else:
+            self._out["pl"] = self.pair.forward(self.runs["pl"], self.pair_in["lr"])
+            self._out["pr"] = self.pair.forward(self.runs["pr"], self.pair_in["rl"])
 
     def _p_fwd_single(self):
-        self._out["sl"] = self.single.forward(self.runs["sl"], self.img["l"])
-        self._out["sr"] = self.single.forward(self.runs["sr"], self.img["r"])
+        if self.twin:
+            self._out.update(self._halves("s", self.single.forward(self.runs["s"], self.img_lr)))
+        else:
+            self._out["sl"] = self.single.forward(self.runs["sl"], self.img["l"])
+            self._out["sr"] = self.single.forward(self.runs["sr"], self.img["r"])
 
     # each net runs twice (shared variables): the first backward call overwrites its gradients, the second
-    # accumulates -- no zeroed gradient buffer needed
+    # accumulates -- no zeroed gradient buffer needed.  Twin: one call per net overwrites them.
     def _bwd(self, k, prog, first):
-        prog.backward(self.runs[k], [IN_PLACE] * len(self.d_out[k]), on_grads=self.hook(prog.chunk),
+        prog.backward(self.runs[k], [IN_PLACE] * len(self.runs[k].prog.spec.outputs), on_grads=self.hook(prog.chunk),
                       grad_accumulate=not first)
 
     def _p_bwd_pair(self):
-        self._bwd("pr", self.pair, True)
-        self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
+        if self.twin:
+            self._bwd("p", self.pair, True)
+        else:
+            self._bwd("pr", self.pair, True)
+            self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
 
     def _p_bwd_single(self):
-        self._bwd("sr", self.single, True)
-        self._bwd("sl", self.single, False)
+        if self.twin:
+            self._bwd("s", self.single, True)
+        else:
+            self._bwd("sr", self.single, True)
+            self._bwd("sl", self.single, False)
 
     def phase_compute(self):
         self._out = {}
@@ -734,8 +796,11 @@ class DepthThenCamTrainer(Trainer):
             _lib.check(lib.tde_spatial_mean_fwd(B, pp.shape[1] * pp.shape[2], 6, ptr(pp), 6, ptr(self.pose[d]), st),
                        "pose mean")
         for s in range(1, 4):
-            Ls.area(self.img["l"], self.pyr["l"][s])
-            Ls.area(self.img["r"], self.pyr["r"][s])
+            if self.twin:
+                Ls.area(self.img_lr, self.pyr_lr[s])
+            else:
+                Ls.area(self.img["l"], self.pyr["l"][s])
+                Ls.area(self.img["r"], self.pyr["r"][s])
         for s in range(4):
             for d in ("lr", "rl"):
                 Ls.pose_prep(self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
@@ -755,7 +820,8 @@ class DepthThenCamTrainer(Trainer):
                 Ls.warp_loss(self.acc, S["photo"], self.pyr[src][s], self.pyr[tgt][s], P=self.P[d][s],
                              Kinv=self.Kinv[s], disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s],
                              photo_w=w["data"], exp_w=w["exp"], consist_w=w["depth"], g_disp=self.d_out[run][s],
-                             g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s])
+                             g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s],
+                             det_ws=self.det_ws)
         # pose gradients -> pose_pred (spatial mean backward)
         for run_key, d in (("pl", "lr"), ("pr", "rl")):
             _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
@@ -854,9 +920,10 @@ class OptflowCombineTrainer(Trainer):
                                         None, None, 0, 0, None, None, ptr(self.gflow[s][0]), ptr(self.gflow[s][1]),
                                         ptr(self.wmask[s]), None, st), "gt warp")      # :169-176
             Ls.warp_loss(self.acc, S["photo"], self.pyr["r"][s], self.pyr["l"][s], P=self.P[s], Kinv=self.Kinv[s],
-                         disp=disp, wmask=self.wmask[s], photo_w=w["data"] * ws, g_disp=gd)   # :178-188
+                         disp=disp, wmask=self.wmask[s], photo_w=w["data"] * ws, g_disp=gd,
+                         det_ws=self.det_ws)                                            # :178-188
             Ls.warp_loss(self.acc, S["photo"], self.pyr["r"][s], self.pyr["l"][s], flow=flow, wmask=self.wmask[s],
-                         photo_w=w["data"] * ws, g_flow=gf)                              # :191-198
+                         photo_w=w["data"] * ws, g_flow=gf, det_ws=self.det_ws)         # :191-198
             Ls.l1(flow, self.gflow[s][0], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=0)   # :205-207
             Ls.l1(flow, self.gflow[s][1], gf, w["optflow"] * ws, self.acc, S["optflow"], coff=1)   # :209-210
         # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
@@ -930,7 +997,7 @@ class RefineTrainer(Trainer):
             disp, g = out[s], self.d_out[s]
             Ls.pose_prep(self.Ks[s], P=self.P[s], Kinv=self.Kinv[s], mat=self.pose)
             Ls.warp_loss(self.acc, S["photo"], self.pyr2[s], self.pyr1[s], P=self.P[s], Kinv=self.Kinv[s],
-                         disp=disp, photo_w=1.0, g_disp=g)                                  # :200-212
+                         disp=disp, photo_w=1.0, g_disp=g, det_ws=self.det_ws)              # :200-212
         # one backward call per step writes every parameter gradient: overwrite, no zeroed buffer
         self.prog.backward(self.run, [IN_PLACE] * len(self.d_out), on_grads=self.hook(self.prog.chunk),
                            grad_accumulate=False)
