@@ -278,7 +278,7 @@ def build_trainer(args, name, N, world, rank):
     deferred = args.deferred_adam == "on" and world == 1 and args.adam_overlap == "off" and not args.sync_bn
     if deferred:
         tr.enable_deferred_adam()
-    net_overlap = (args.net_overlap == "on" and world == 1 and args.adam_overlap == "off" and not deferred and
+    net_overlap = (args.net_overlap == "on" and args.adam_overlap == "off" and not deferred and
                    not args.sync_bn and len(tr.programs()) > 1)
     if net_overlap:
         tr.enable_net_overlap()

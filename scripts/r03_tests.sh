@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r03}
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
   > gpurun_out/tests_${TAG}.log 2>&1
 rc=$?; tail -25 gpurun_out/tests_${TAG}.log
 case $rc in 0|1) ;; *) echo "[tests] rc=$rc: stopping"; exit $rc;; esac

@@ -50,7 +50,7 @@ def test_bucket_launches_follow_backward_schedule():
     gs = ddp.GradSync([chunk], 1, bucket_mb=1.0)
     fired, cur = {}, [None]
 
-    def fake_launch(buckets):
+    def fake_launch(buckets, streams=()):
         for b in buckets:
             assert id(b) not in fired
             fired[id(b)] = cur[0]

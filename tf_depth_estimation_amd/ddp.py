@@ -71,11 +71,14 @@ class GradSync:
 
     chunks: ParamChunks updated by the step; uses: {id(chunk): backward calls per step} (default 1)."""
 
-    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None):
+    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None, side_streams=None):
         self.world, self.group = world, group
-        # called before a bucket launch point: orders the compute stream after side streams that write
-        # gradients (NetProgram.join_wgrad), so the launch event covers them
+        # pre_launch(chunk): called before a bucket launch point UNDER CAPTURE -- joins the streams that write the
+        # chunk's gradients beside the capture stream (its program's filter-gradient branch, NetProgram.join_wgrad),
+        # since a graph segment can only end with its forked branches joined.  Eagerly the compute stream never
+        # waits: side_streams(chunk) lists those streams and the comm stream waits on an event at each one's tail.
         self.pre_launch = pre_launch
+        self.side_streams = side_streams
         self.chunks = list(chunks)
         self.buckets = []
         self.by_param = {}
@@ -119,21 +122,23 @@ class GradSync:
                     if self.left[id(b)] == 0:
                         ready.append(b)
             if ready:
-                self._ready(ready)
+                self._ready(ready, chunk)
         return on_grads
 
-    def _ready(self, buckets):
-        if self.pre_launch is not None:
-            self.pre_launch()
+    def _ready(self, buckets, chunk=None):
         for b in buckets:
             b.launched = True
         if self.capturing is not None:
+            if self.pre_launch is not None:
+                self.pre_launch(chunk)
             self.capturing(buckets)      # graph segment boundary; launched at replay
         else:
-            self.launch(buckets)
+            self.launch(buckets, self.side_streams(chunk) if (self.side_streams and chunk is not None) else ())
 
     # ---- the exchange
-    def launch(self, buckets):
+    def launch(self, buckets, streams=()):
+        """All-reduce `buckets` on the comm stream after everything issued so far on the current stream and on
+        `streams` (events: neither the current stream nor the side streams wait for anything)."""
         import torch.distributed as dist
         self.log.extend(list(b.names) for b in buckets)
         if not self.gpu:
@@ -145,6 +150,10 @@ class GradSync:
         ev = torch.cuda.Event()
         ev.record()
         self.comm.wait_event(ev)
+        for sd in streams:
+            e2 = torch.cuda.Event()
+            e2.record(sd)
+            self.comm.wait_event(e2)
         lib = _lib.load()
         with torch.cuda.stream(self.comm):
             st = _lib.stream_ptr()
@@ -156,15 +165,14 @@ class GradSync:
     def leftovers(self):
         return [b for b in self.buckets if not b.launched]
 
-    def finish(self):
-        """Launch what was never reported, then order the compute stream after the comm stream."""
+    def finish(self, streams=()):
+        """Launch what was never reported (after `streams` too), then order the compute stream after the comm
+        stream."""
         rest = self.leftovers()
-        if self.pre_launch is not None:
-            self.pre_launch()
         if rest:
             for b in rest:
                 b.launched = True
-            self.launch(rest)
+            self.launch(rest, streams)
         if self.gpu:
             torch.cuda.current_stream().wait_stream(self.comm)
 

@@ -6,6 +6,8 @@ into a hipGraph (torch.cuda.CUDAGraph) and replay it with zero host work per ste
 
   DepthOnlyTrainer   config 2 -- train_depth_only.py:108-219 (disp_net, smooth + depth L1, Adam)
 """
+import os
+
 import torch
 
 from . import _api, _lib, _netlib, variables
@@ -251,15 +253,14 @@ class Trainer:
         return self
 
     def enable_net_overlap(self, on=True):
-        """Single GPU: run the calls of one network program concurrently with those of the other on a second
-        stream (config 4: `depth_net` on both pairs beside `disp_net` on both images, forward and backward;
-        a parallel graph branch under capture).  The two programs share no buffer, parameter, gradient or
-        moving statistic, and each program's calls keep their order, so the step is bit-identical to the
-        serial one.  Not combinable with the bucketed exchange, Adam overlaps or SyncBN (their hooks and
-        collectives order against the one compute stream)."""
-        if on and (self.grad_sync is not None or self.adam_ov is not None or self.dadam is not None or
-                   getattr(self, "sync_bn", False)):
-            raise ValueError("net overlap is for the single-GPU step without exchange / Adam overlap / SyncBN")
+        """Run the calls of one network program concurrently with those of the other on a second stream
+        (config 4: `depth_net` on both pairs beside `disp_net` on both images, forward and backward; under capture
+        each piece is its own graph on its stream).  The two programs share no buffer, parameter, gradient or
+        moving statistic, and each program's calls keep their order, so the step is bit-identical to the serial
+        one.  With the data-parallel exchange each program's bucket launch points cut its own piece's graphs
+        (enable_ddp).  Not combinable with the Adam overlaps or SyncBN."""
+        if on and (self.adam_ov is not None or self.dadam is not None or getattr(self, "sync_bn", False)):
+            raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / SyncBN")
         self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
@@ -342,13 +343,37 @@ class Trainer:
         else:
             self.phase_update()
 
+    def _program_of(self, chunk):
+        for p in self.programs():
+            if p.chunk is chunk:
+                return p
+        return None
+
+    def _join_chunk_wgrad(self, chunk):
+        """Under capture: join the filter-gradient branch of the program owning `chunk` into the current (that
+        program's) stream -- a graph segment must end with its forked branches joined.  Only that program's:
+        the other program may be mid-capture on its own stream (net overlap)."""
+        p = self._program_of(chunk)
+        if p is not None:
+            p.join_wgrad()
+        else:
+            self.join_wgrad()
+
+    def _chunk_side_streams(self, chunk):
+        """Eagerly: the streams besides the current one that write `chunk`'s gradients (its program's
+        filter-gradient streams); the comm stream waits on events at their tails, nobody else waits."""
+        p = self._program_of(chunk)
+        if p is None or p.wgrad_stream is None or isinstance(p.wgrad_stream, str):
+            return ()
+        return tuple(p.wgrad_streams)
+
     def enable_ddp(self, world, bucket_mb=32.0, group=None):
         from .ddp import GradSync
         if self.adam_ov is not None:
             raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
-                                  pre_launch=self.join_wgrad)
+                                  pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams)
         return self.grad_sync
 
     def enable_sync_bn(self, world, group=None):
@@ -661,7 +686,8 @@ class DepthThenCamTrainer(Trainer):
             self.Ks[s].copy_(self.K[:, s].reshape(-1, 9))
 
     def phase_update(self):
-        self.opt.step()
+        if not self._inline_adam():
+            self.opt.step()
 
     # phase_compute in pieces: "main" pieces on the compute stream, "ov" pieces (depth_net's calls) on the
     # second stream under enable_net_overlap.  Under capture each piece is its own graph (a whole program
@@ -710,12 +736,21 @@ class DepthThenCamTrainer(Trainer):
         prog.backward(self.runs[k], [IN_PLACE] * len(self.runs[k].prog.spec.outputs), on_grads=self.hook(prog.chunk),
                       grad_accumulate=not first)
 
+    def _inline_adam(self):
+        """Plain step (no exchange, no Adam overlap / deferral): each network's Adam runs right after its own
+        backward on that backward's stream -- depth_net's update overlaps disp_net's backward tail (and the
+        other way round) instead of both updates waiting for the join.  The same update arithmetic."""
+        return (self.grad_sync is None and self.adam_ov is None and self.dadam is None and
+                os.environ.get("TDE_C4_INLINE_ADAM", "1") != "0")
+
     def _p_bwd_pair(self):
         if self.twin:
             self._bwd("p", self.pair, True)
         else:
             self._bwd("pr", self.pair, True)
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
+        if self._inline_adam():
+            self.opt.opts[1].step()
 
     def _p_bwd_single(self):
         if self.twin:
@@ -723,6 +758,8 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("sr", self.single, True)
             self._bwd("sl", self.single, False)
+        if self._inline_adam():
+            self.opt.opts[0].step()
 
     def phase_compute(self):
         self._out = {}
@@ -740,10 +777,14 @@ class DepthThenCamTrainer(Trainer):
             else:
                 fn()
 
-    def capture(self, warmup=2):
+    def capture(self, warmup=2, single_graph=None):
         """With the net overlap: one graph per piece, captured on the piece's stream; step() replays them
-        with the same stream waits as the eager overlapped step."""
-        if self._overlap_stream() is None:
+        with the same stream waits as the eager overlapped step.  single_graph=True (or TDE_C4_SINGLE_GRAPH=1,
+        without the bucketed exchange): the whole step as ONE graph, depth_net's calls a forked branch of it."""
+        if single_graph is None:
+            single_graph = os.environ.get("TDE_C4_SINGLE_GRAPH", "0") == "1"
+        if self._overlap_stream() is None or (single_graph and self.grad_sync is None):
+            self.ov_seq = None
             return super().capture(warmup)
         s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
@@ -754,37 +795,82 @@ class DepthThenCamTrainer(Trainer):
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         main, ov = _lib.owned_stream(self, "capture"), self.net_stream
-        pieces = self._pieces() + [("main", self._update)]
+        gs = self.grad_sync
+        seg = gs is not None and hasattr(gs, "begin_step")
+        pieces = self._pieces() + ([] if seg else [("main", self._update)])
         seq = []
         self._out = {}
-        for where, fn in pieces:
-            if where == "join":
-                seq.append((where, None))
-                continue
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(ov if where == "ov" else main):
-                g.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
-                fn()
-                g.capture_end()
-            seq.append((where, g))
+        if seg:
+            gs.begin_step()
+        try:
+            for where, fn in pieces:
+                if where == "join":
+                    seq.append((where, None))
+                    continue
+                stream = ov if where == "ov" else main
+                # a piece is a list of graph segments: with the bucketed exchange, every bucket launch point of the
+                # piece's backward closes the current segment (the program's filter-gradient branch joined first,
+                # _join_chunk_wgrad); replay launches the buckets between segments, on the piece's stream
+                segs = []
+                state = {"g": torch.cuda.CUDAGraph()}
+
+                def cut(buckets, state=state, segs=segs, stream=stream):
+                    state["g"].capture_end()
+                    segs.append((state["g"], list(buckets)))
+                    state["g"] = torch.cuda.CUDAGraph()
+                    state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+
+                with torch.cuda.stream(stream):
+                    if seg:
+                        gs.capturing = cut
+                    state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+                    fn()
+                    state["g"].capture_end()
+                    segs.append((state["g"], []))
+                seq.append((where, segs))
+            if seg:
+                gs.capturing = None
+                leftovers = gs.leftovers()
+                upd = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(main):
+                    upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+                    self.phase_update()
+                    upd.capture_end()
+                self.ov_upd = (leftovers, upd)
+        finally:
+            if seg:
+                gs.capturing = None
         torch.cuda.synchronize()
         self.ov_seq = seq
-        self.graphs = [g for _, g in seq if g is not None]
+        self.graphs = [g for _, segs in seq if segs is not None for g, _ in segs]
+        if seg:
+            self.graphs.append(self.ov_upd[1])
         return self.graphs
 
     def step(self):
         if self.graphs is None or getattr(self, "ov_seq", None) is None:
             return super().step()
         cur, ov = torch.cuda.current_stream(), self.net_stream
-        for where, g in self.ov_seq:
+        gs = self.grad_sync
+        seg = gs is not None and hasattr(gs, "begin_step")
+        if seg:
+            gs.begin_step()
+        for where, segs in self.ov_seq:
             if where == "join":
                 cur.wait_stream(ov)
-            elif where == "ov":
+                continue
+            if where == "ov":
                 ov.wait_stream(cur)
-                with torch.cuda.stream(ov):
+            with torch.cuda.stream(ov if where == "ov" else cur):
+                for g, buckets in segs:
                     g.replay()
-            else:
-                g.replay()
+                    if buckets:
+                        for b in buckets:
+                            b.launched = True
+                        gs.launch(buckets)      # the comm stream waits on this stream's tail
+        if seg:
+            gs.finish()
+            self.ov_upd[1].replay()
 
     def _p_loss(self):
         from . import losses as Ls
