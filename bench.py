@@ -271,18 +271,31 @@ def build_trainer(args, name, N, world, rank):
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     if args.sync_bn:
         tr.enable_sync_bn(world)
+    net_overlap = (args.net_overlap == "on" and args.adam_overlap == "off" and not args.sync_bn and
+                   len(tr.programs()) > 1 and not (args.deferred_adam == "on" and world == 1))
+    wg_progs = []
     if args.wgrad_overlap == "on":
-        tr.enable_wgrad_overlap()
+        only = None
+        if args.wgrad_progs == "auto":
+            # config 4 with the net overlap: only depth_net (the second stream's network, the longer chain) moves
+            # its filter gradients to a side stream; disp_net's stay fused on the compute stream, which then
+            # carries a chain as long as depth_net's (measured: 980 vs 910 pairs/s with both moved, 866 with
+            # only disp_net's)
+            if net_overlap and getattr(tr, "ov_net", None) == "pair" and not os.environ.get("TDE_WGRAD_PROGS"):
+                only = ["pair"]
+        elif args.wgrad_progs != "all":
+            only = args.wgrad_progs.split(",")
+        tr.enable_wgrad_overlap(only=only)
+        wg_progs = [n for n in ("prog", "single", "pair")
+                    if getattr(getattr(tr, n, None), "wgrad_stream", None) is not None]
     if args.adam_overlap != "off" and world == 1:
         tr.enable_adam_overlap(args.adam_bucket_mb, on_wgrad_stream=args.adam_overlap == "wgrad")
     deferred = args.deferred_adam == "on" and world == 1 and args.adam_overlap == "off" and not args.sync_bn
     if deferred:
         tr.enable_deferred_adam()
-    net_overlap = (args.net_overlap == "on" and args.adam_overlap == "off" and not deferred and
-                   not args.sync_bn and len(tr.programs()) > 1)
     if net_overlap:
         tr.enable_net_overlap()
-    return tr, dict(deferred=deferred, net_overlap=net_overlap)
+    return tr, dict(deferred=deferred, net_overlap=net_overlap, wgrad_progs=wg_progs)
 
 
 def instrumented_step(tr):
@@ -359,6 +372,9 @@ def main():
     ap.add_argument("--wgrad-overlap", default="on", choices=["on", "off"],
                     help="filter gradients on a side stream, off backward's data-gradient chain (a parallel graph "
                          "branch; bit-identical results)")
+    ap.add_argument("--wgrad-progs", default="auto",
+                    help="programs whose filter gradients go to a side stream: auto (config 4 with the net overlap: "
+                         "'pair'; else all), all, or a comma list of single,pair,prog (TDE_WGRAD_PROGS when unset)")
     ap.add_argument("--net-overlap", default="on", choices=["on", "off"],
                     help="config 4: depth_net's calls on a second stream beside disp_net's (independent "
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
@@ -429,7 +445,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
-                       "wgrad_overlap": args.wgrad_overlap == "on",
+                       "wgrad_overlap": args.wgrad_overlap == "on", "wgrad_progs": opts.get("wgrad_progs"),
                        "adam_overlap": args.adam_overlap if world == 1 else "off",
                        "deferred_adam": opts["deferred"],
                        "net_overlap": opts["net_overlap"],

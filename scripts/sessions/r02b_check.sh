@@ -13,6 +13,6 @@ rc2=$?; echo "smoke rc=$rc2"; tail -3 gpurun_out/r02b_smoke.log
 timeout -k 10 300 python -u bench.py > gpurun_out/r02b_bench.json 2> gpurun_out/r02b_bench.err
 rc3=$?; echo "bench rc=$rc3"; cat gpurun_out/r02b_bench.json
 [ $rc3 -eq 0 ] || exit $rc3
-bash scripts/r02_prof.sh r02b > /dev/null 2>&1
+bash scripts/sessions/r02_prof.sh r02b > /dev/null 2>&1
 echo "prof rc=$?"; head -40 gpurun_out/kstats_r02b.txt
 exit $rc

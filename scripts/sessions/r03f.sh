@@ -8,4 +8,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_ddp.py tests/test_gpu_train
   --timeout-method thread -k "ddp or deterministic or exchange" > gpurun_out/r03f_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r03f_tests.log
 case $rc in 0|1) ;; *) echo "[r03f] tests rc=$rc: stopping"; exit $rc;; esac
-TAG=r03f bash scripts/r03a.sh
+TAG=r03f bash scripts/sessions/r03a.sh

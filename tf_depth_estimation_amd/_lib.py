@@ -208,6 +208,51 @@ def dedicated_stream():
     return torch.cuda.ExternalStream(s.value)
 
 
+# ---- cross-stream ordering that survives stream capture
+# Root cause of the round-2 capture_end crash (round 3, AMD_LOG_LEVEL=3 + faulthandler, probe/capture_repeat.py):
+# torch's `a.wait_stream(b)` records a TEMPORARY event on b, makes a wait on it and destroys the event at once.
+# Inside a hipStreamBeginCapture region HIP keeps a pointer to that event in the capture's bookkeeping (the
+# fork / join of the captured streams); when it has already been destroyed, hipStreamEndCapture walks freed memory
+# and segfaults (last logged calls: hipEventRecord, hipStreamWaitEvent, hipEventDestroy, hipStreamEndCapture ->
+# crash) -- reproducibly for a whole config-4 step captured as one graph with forked branches, intermittently
+# ("after ~40 captures") when the freed memory happened to survive.  Every cross-stream wait of the hot path goes
+# through wait_stream / wait_event below, which keep the event alive for the life of the process while any
+# capture is open (capture_scope).
+_CAPTURE_DEPTH = [0]
+_CAPTURE_EVENTS = []
+
+
+class capture_scope:
+    """Context manager around every stream-capture region: events used for cross-stream waits inside it are kept."""
+
+    def __enter__(self):
+        _CAPTURE_DEPTH[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _CAPTURE_DEPTH[0] -= 1
+        return False
+
+
+def _keep(ev):
+    if _CAPTURE_DEPTH[0] > 0:
+        _CAPTURE_EVENTS.append(ev)
+
+
+def wait_stream(waiter, waitee):
+    """waiter waits for everything issued so far on waitee (torch's Stream.wait_stream, capture-safe)."""
+    ev = torch.cuda.Event()
+    ev.record(waitee)
+    waiter.wait_event(ev)
+    _keep(ev)
+
+
+def wait_event(stream, ev):
+    """stream waits on ev (capture-safe: ev kept alive while a capture is open)."""
+    stream.wait_event(ev)
+    _keep(ev)
+
+
 def owned_stream(owner, name):
     """A dedicated stream (dedicated_stream) cached on `owner` under `name`: created once per owner and role, so
     re-enabling an overlap or re-capturing a step never allocates another HIP stream, and no two roles ever share

@@ -19,7 +19,7 @@ cv2.bilateralFilter, .tofile) stays on the host with the caller: it is OpenCV, o
 """
 import torch
 
-from . import _api, _netlib, checkpoint, pose_ops, variables
+from . import _api, _lib, _netlib, checkpoint, pose_ops, variables
 from .program import NetRun
 
 # net name -> (variable scope of the net, spec builder, input channels, builder kwargs, reference)
@@ -67,14 +67,15 @@ class Predictor:
         self.graph = None
         if self.fold:
             self.prog.fold_bn()
-        s = torch.cuda.Stream()
+        s = _lib.owned_stream(self, "warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):               # warm-up: allocates every lazily created buffer
             self.outs = self._forward()
         torch.cuda.current_stream().wait_stream(s)
         if self.use_graph:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with _lib.capture_scope(), torch.cuda.graph(g, stream=_lib.owned_stream(self, "capture"),
+                                                        capture_error_mode="thread_local"):
                 self.outs = self._forward()
             self.graph = g
 

@@ -13,9 +13,13 @@
 // operands live m-major in a double-buffered LDS image ([row][k], padded rows); an operand whose
 // 16-byte global vectors run along rows (not k) is transposed in registers (4 rows x 4 k per thread),
 // so every global load is a coalesced dwordx4, every LDS store a ds_write_b128 (fp32) and every
-// fragment read a ds_read_b128 issued up front for the whole k-tile.  Two math modes:
-//   fp32   : 8 v_mfma_f32_16x16x4_f32 per tile pair (exact f32 products, fp32 accumulate);
-//   bf16x3 : 3 v_mfma_f32_16x16x32_bf16 per tile pair on a hi/lo split of each operand.
+// fragment read a ds_read_b128 issued up front for the whole k-tile.  Five math modes (MATH template
+// argument, TDE_CONV_MATH / tde_set_conv_math):
+//   0 fp32    : 8 v_mfma_f32_16x16x4_f32 per tile pair (exact f32 products, fp32 accumulate);
+//   1 bf16x3  : 3 v_mfma_f32_16x16x32_bf16 per tile pair on a hi/lo split of each operand;
+//   2 bf16x6  : 6 bf16 MFMAs on an exact hi/mid/lo split, split once at LDS staging;
+//   3 bf16x6r : the same products, split per fragment in registers after the LDS read;
+//   4 fp16x3  : 3 v_mfma_f32_16x16x32_f16 on a power-of-two-scaled hi/lo fp16 split (the default).
 // Split-K partials go to a caller workspace and are reduced by a second kernel (deterministic; no
 // float atomics).
 #include "tde_common.h"
@@ -1077,6 +1081,10 @@ static const long g_force_splits = env_long("TDE_FORCE_SPLITS", 0);
 static const long g_deep_bn = env_long("TDE_DEEP_BN", 0);
 
 static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to which FWD / DGRAD go skinny
+// FWD / DGRAD GEMMs with at most this many rows (and < 256 tiles) take 64-row tiles (more blocks); above it, and
+// for every WGRAD, 128 (half the weight re-reads of a weight-streaming deep layer per row tile)
+static const long g_bm64_maxm = env_long("TDE_BM64_MAXM", 4096);
+static const long g_wgrad_bm64 = env_long("TDE_WGRAD_BM64", 0);
 
 // fix_bm / fix_bn > 0: plan with that tile (the fused backward launch needs one tile for both GEMMs)
 static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fix_bn = 0) {
@@ -1123,7 +1131,11 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
   long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   // WGRAD reduces over every pixel (Kd ~ 1e5): parallelism comes from split-K, so keep the
   // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.
-  if ((mode != MODE_WGRAD && tiles < 256 && M <= 4096) || g_force_bm == 64 || fix_bm == 64) {
+  // WGRAD of a low-resolution layer (few pixels to reduce over, so split-K cannot add blocks) with < 256 tiles:
+  // 64-row tiles double the blocks of an otherwise under-filled chip (TDE_WGRAD_BM64=0: always 128)
+  const bool wg_small = mode == MODE_WGRAD && g_wgrad_bm64 && tiles < 256 &&
+                        tde_cdiv(Kd, BK) < 2 * g_split_minkt;
+  if ((mode != MODE_WGRAD && tiles < 256 && M <= g_bm64_maxm) || wg_small || g_force_bm == 64 || fix_bm == 64) {
     pl.bm = 64;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }

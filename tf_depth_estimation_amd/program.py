@@ -481,7 +481,7 @@ class NetProgram:
             self._flush_wgrad()
             if self.wgrad_stream is not SERIAL:
                 for sd in self.wgrad_streams:
-                    torch.cuda.current_stream().wait_stream(sd)
+                    _lib.wait_stream(torch.cuda.current_stream(), sd)
 
     def _flush_wgrad(self, ev=None):
         """Issue the deferred filter gradients on the side stream behind ONE wait for the compute stream: on
@@ -498,9 +498,9 @@ class NetProgram:
             self._wg_rr += 1
             side = self.wgrad_streams[sidx]
             if ev is not None:
-                side.wait_event(ev)
+                _lib.wait_event(side, ev)
             else:
-                side.wait_stream(torch.cuda.current_stream())
+                _lib.wait_stream(side, torch.cuda.current_stream())
         ws2 = self._scratch_side(self._wg_N, sidx)
         with torch.cuda.stream(side):
             for fn, _ in pending:

@@ -113,7 +113,7 @@ class AdamOverlap:
                 self.pre_launch()
                 ev = torch.cuda.Event()
                 ev.record()
-            self.side.wait_event(ev)
+            _lib.wait_event(self.side, ev)
             with torch.cuda.stream(self.side):
                 for b in on_side:
                     b.opt.update(b.lo, b.hi)
@@ -122,7 +122,7 @@ class AdamOverlap:
             st = self.streams.get(id(b.chunk))
             if st is None:
                 continue
-            st.wait_event(ev)
+            _lib.wait_event(st, ev)
             with torch.cuda.stream(st):
                 b.opt.update(b.lo, b.hi)
             self.done.add(id(b))
@@ -131,9 +131,9 @@ class AdamOverlap:
         rest = [b for b in self.buckets if id(b) not in self.done]
         if rest:
             self.launch(rest)
-        torch.cuda.current_stream().wait_stream(self.side)
+        _lib.wait_stream(torch.cuda.current_stream(), self.side)
         for st in set(self.streams.values()):
-            torch.cuda.current_stream().wait_stream(st)
+            _lib.wait_stream(torch.cuda.current_stream(), st)
 
 
 class DeferredAdam:
@@ -167,7 +167,7 @@ class DeferredAdam:
         if not self.pending:
             return
         cur = torch.cuda.current_stream()
-        self.side.wait_stream(cur)
+        _lib.wait_stream(self.side, cur)
         with torch.cuda.stream(self.side):
             for o in self.opts:
                 o.begin()
@@ -188,7 +188,7 @@ class DeferredAdam:
             return
         for b in self._needed(prog, i):
             if id(b) not in self.waited:
-                torch.cuda.current_stream().wait_event(b[2])
+                _lib.wait_event(torch.cuda.current_stream(), b[2])
                 self.waited.add(id(b))
 
     def params_ready(self, prog, i):
@@ -201,9 +201,9 @@ class DeferredAdam:
             for bs in self.buckets.values():
                 for b in bs:
                     if id(b) not in self.waited:
-                        cur.wait_event(b[2])
+                        _lib.wait_event(cur, b[2])
                         self.waited.add(id(b))
-            cur.wait_stream(self.side)
+            _lib.wait_stream(cur, self.side)
             self.active = False
 
 
@@ -317,11 +317,19 @@ class Trainer:
                                    pre_launch=self.join_wgrad, streams=streams)
         return self.adam_ov
 
-    def enable_wgrad_overlap(self, on=True, serial=False):
+    def enable_wgrad_overlap(self, on=True, serial=False, only=None):
         """Filter gradients on a side stream, off the backward chain (NetProgram.enable_wgrad_overlap;
-        serial=True: the same split calls on the compute stream, the bit-exact reference of the overlap)."""
-        for p in self.programs():
-            p.enable_wgrad_overlap(on, serial)
+        serial=True: the same split calls on the compute stream, the bit-exact reference of the overlap).
+        only: a list of program attribute names ("single", "pair", "prog") to restrict it to (the others keep
+        the fused data + filter gradient launch on their own stream); default: TDE_WGRAD_PROGS (comma list) or
+        every program."""
+        if only is None and os.environ.get("TDE_WGRAD_PROGS"):
+            only = [x for x in os.environ["TDE_WGRAD_PROGS"].split(",") if x]
+        for name in ("prog", "single", "pair"):
+            p = getattr(self, name, None)
+            if p is None:
+                continue
+            p.enable_wgrad_overlap(on and (only is None or name in only), serial)
         return self
 
     def join_wgrad(self):
@@ -410,8 +418,13 @@ class Trainer:
             gs()
         self._update()
 
-    def capture(self, warmup=2):
-        """Warm up on a side stream (allocates every lazily created buffer), then record."""
+    def capture(self, warmup=2, **kw):
+        """Warm up on a side stream (allocates every lazily created buffer), then record.  Every cross-stream wait
+        made while recording keeps its event alive (_lib.capture_scope: the capture_end crash of round 2)."""
+        with _lib.capture_scope():
+            return self._capture(warmup, **kw)
+
+    def _capture(self, warmup=2):
         if getattr(self, "sync_bn", False):
             raise NotImplementedError("SyncBN all-reduces inside the forward/backward: run step() eagerly")
         s = _lib.owned_stream(self, "capture_warmup")
@@ -611,6 +624,7 @@ class DepthThenCamTrainer(Trainer):
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG4
         self.twin = bool(twin)
+        self.ov_net = os.environ.get("TDE_C4_OV_NET", "pair")   # the network on the second stream (net overlap)
         self.BACKWARD_USES = 1 if self.twin else 2     # backward calls per chunk per step
         with variables.variable_scope("model_singledepth"):
             self.single = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
@@ -694,8 +708,14 @@ class DepthThenCamTrainer(Trainer):
     # forked onto a captured side branch made capture_end crash in a long-lived process -- ROCm 7 graph
     # instantiation, not reproducible alone), and replay interleaves them with stream waits.
     def _pieces(self):
-        return [("main", self._p_inputs), ("ov", self._p_fwd_pair), ("main", self._p_fwd_single), ("join", None),
-                ("main", self._p_loss), ("ov", self._p_bwd_pair), ("main", self._p_bwd_single), ("join", None)]
+        """The step as stream pieces: the overlapped network's calls (`ov_net`, default depth_net = "pair"; env
+        TDE_C4_OV_NET) on the second stream, issued before the other network's on the compute stream."""
+        fwd = {"pair": self._p_fwd_pair, "single": self._p_fwd_single}
+        bwd = {"pair": self._p_bwd_pair, "single": self._p_bwd_single}
+        o = self.ov_net if self.ov_net in fwd else "pair"
+        m = "single" if o == "pair" else "pair"
+        return [("main", self._p_inputs), ("ov", fwd[o]), ("main", fwd[m]), ("join", None),
+                ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
     def _p_inputs(self):
         lib, st = _lib.load(), _lib.stream_ptr()
@@ -768,16 +788,16 @@ class DepthThenCamTrainer(Trainer):
         for where, fn in self._pieces():
             if where == "join":
                 if ov is not None:
-                    cur.wait_stream(ov)
+                    _lib.wait_stream(cur, ov)
             elif where == "ov" and ov is not None:
                 # depth_net on both pairs on the second stream, beside disp_net on both images
-                ov.wait_stream(cur)
+                _lib.wait_stream(ov, cur)
                 with torch.cuda.stream(ov):
                     fn()
             else:
                 fn()
 
-    def capture(self, warmup=2, single_graph=None):
+    def _capture(self, warmup=2, single_graph=None):
         """With the net overlap: one graph per piece, captured on the piece's stream; step() replays them
         with the same stream waits as the eager overlapped step.  single_graph=True (or TDE_C4_SINGLE_GRAPH=1,
         without the bucketed exchange): the whole step as ONE graph, depth_net's calls a forked branch of it."""
@@ -785,7 +805,7 @@ class DepthThenCamTrainer(Trainer):
             single_graph = os.environ.get("TDE_C4_SINGLE_GRAPH", "0") == "1"
         if self._overlap_stream() is None or (single_graph and self.grad_sync is None):
             self.ov_seq = None
-            return super().capture(warmup)
+            return super()._capture(warmup)
         s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
