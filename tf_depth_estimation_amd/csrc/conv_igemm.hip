@@ -34,6 +34,12 @@
 namespace {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
+// WGRAD pixel decode fast path for OW % 4 == 0 (conv_tile R4), off: ~60 VALU less per k-tile, but measured
+// neutral (big3x3 WGRAD 640 vs 649 us, config 4 8.19 vs 8.22 ms; scripts/sessions/r03n.sh) -- the loop waits
+// on its loads, not on address arithmetic -- so it is not worth the second set of WGRAD instantiations
+#ifndef TDE_WGRAD_ROW4
+#define TDE_WGRAD_ROW4 0
+#endif
 constexpr int NT = 256;
 
 struct ConvArgs {
@@ -52,6 +58,7 @@ struct ConvArgs {
   // fp16x3 (math 4) operand bounds |x| <= *bound of the x view, the y view and the weights (null: unscaled
   // x / y, fixed weight scale; split_math.h)
   const float* xmax; const float* ymax; const float* wmax;
+  int xcd;   // igemmx_kernel: XCD-grouped tile order (TDE_XCD_WGRAD)
 };
 
 // The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
@@ -257,7 +264,9 @@ struct SmemSize {
 };
 
 // One output tile (bx, by) of split / class bz.  The kernels below map blocks onto tiles.
-template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
+// R4 (WGRAD, OW % 4 == 0): the row-of-4 pixel decode.  A template argument chosen once per block (a branch
+// inside the k-loop made hipcc drain every load at its merge point: 637 -> 752 us on big3x3 WGRAD).
+template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF, bool R4 = false>
 __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const int by, const int bz,
                                           typename ImgSel<MATH, BM>::T* smem) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
@@ -385,13 +394,28 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         int n = fdiv(pix0, p.fOHW);
         const int r = pix0 - n * p.OH * p.OW;
         int oh = fdiv(r, p.fOW), ow = r - oh * p.OW;
+        if constexpr (R4) {
+          // OW % 4 == 0 (every level down to 6x8; pix0 % 4 == 0): the 4 pixels share (n, oh) and step along
+          // one input row by S, so one row test, one address and per-pixel column tests (the general path
+          // below re-derives both per pixel: ~23 VALU per load)
+          const int ih = oh * p.S + a_i1[i], iw0 = ow * p.S + a_i2[i];
+          const bool rok = pix0 < Kd && (unsigned)ih < (unsigned)p.H;
+          const int b0 = a_pb[i] + ((n * p.H + oh * p.S) * p.W + ow * p.S) * p.xcs;
+          const int step = p.S * p.xcs;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ih = oh * p.S, iw = ow * p.S;
-          const bool ok = pix0 + j < Kd && (unsigned)(ih + a_i1[i]) < (unsigned)p.H &&
-                          (unsigned)(iw + a_i2[i]) < (unsigned)p.W;
-          ra[i][j] = bload(rx, ok ? 4 * (a_pb[i] + ((n * p.H + ih) * p.W + iw) * p.xcs) : OOB);
-          if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
+          for (int j = 0; j < 4; ++j) {
+            const bool ok = rok && (unsigned)(iw0 + j * p.S) < (unsigned)p.W;
+            ra[i][j] = bload(rx, ok ? 4 * (b0 + j * step) : OOB);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ih = oh * p.S, iw = ow * p.S;
+            const bool ok = pix0 + j < Kd && (unsigned)(ih + a_i1[i]) < (unsigned)p.H &&
+                            (unsigned)(iw + a_i2[i]) < (unsigned)p.W;
+            ra[i][j] = bload(rx, ok ? 4 * (a_pb[i] + ((n * p.H + ih) * p.W + iw) * p.xcs) : OOB);
+            if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
+          }
         }
       }
     }
@@ -777,10 +801,31 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 // Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
 // share a pixel slab -- was measured 5-20% SLOWER on config 2's layers: the round-robin order
 // already lets neighbouring tiles, dispatched together, share the slab through the Infinity Cache.)
+// p.xcd (WGRAD, TDE_XCD_WGRAD=1): the grid is re-ordered so that each XCD (hardware block b runs on XCD b % 8)
+// gets one contiguous run of the (x fastest, z slowest) tile order -- the tiles of one split-K pixel slice then
+// share their x / dy rows in ONE L2 instead of pulling them into all eight.
+// TDE_PF2_WAVES: waves per SIMD the two-tiles-in-flight (PF 2) variants must fit (register cap 512 / W)
+#ifndef TDE_PF2_WAVES
+#define TDE_PF2_WAVES 2
+#endif
 template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
-__global__ void __launch_bounds__(NT) igemmx_kernel(const ConvArgs p) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF == 2 ? TDE_PF2_WAVES : 1)))
+igemmx_kernel(const ConvArgs p) {
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
-  conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    int l = tde_xcd_block(bx + gx * (by + gy * bz), gx * gy * gridDim.z);
+    bx = l % gx; l /= gx;
+    by = l % gy; bz = l / gy;
+  }
+  if constexpr (MODE == MODE_WGRAD && TDE_WGRAD_ROW4) {
+    if ((p.OW & 3) == 0) {
+      conv_tile<MATH, MODE, BM, BN, WM, WN, PF, true>(p, bx, by, bz, smem);
+      return;
+    }
+  }
+  conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, bx, by, bz, smem);
 }
 
 // The two backward GEMMs of one layer in ONE launch (horizontal fusion): blocks [0, nd) compute the
@@ -800,6 +845,12 @@ __global__ void __launch_bounds__(NT) igemm_bwd2_kernel(const ConvArgs pd, const
     id -= nd;
     const int bx = id % gxw;
     id /= gxw;
+    if constexpr (TDE_WGRAD_ROW4) {
+      if ((pw.OW & 3) == 0) {
+        conv_tile<MATH, MODE_WGRAD, BM, BN, WM, WN, 1, true>(pw, bx, id % gyw, id / gyw, smem);
+        return;
+      }
+    }
     conv_tile<MATH, MODE_WGRAD, BM, BN, WM, WN, 1>(pw, bx, id % gyw, id / gyw, smem);
   }
 }
@@ -1267,6 +1318,9 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
 // (scripts/r02zm.sh) icnv5 DGRAD 43.6 -> 36.6 us, config 2 2.82 -> 2.80 ms, config 4 13.30 -> 13.18 ms).
 // TDE_CONV_PF: 1 / 2 forces one depth for all (tuning experiments).
 static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
+// TDE_PF128: prefetch depth of the 128-row tiles (2: two k-tiles in flight, capped at 256 VGPRs = 2 waves per
+// SIMD by TDE_PF2_WAVES -- the occupancy the 128-row tiles have anyway, 64 KiB of LDS per workgroup)
+static const long g_pf128 = env_long("TDE_PF128", 1);
 // wave layout of a tile: 2 x 2 waves when BN is a multiple of TDE_WN_DIV, else 4 x 1 (all rows split)
 #ifndef TDE_WN_DIV
 #define TDE_WN_DIV 32
@@ -1286,12 +1340,16 @@ static int tile_math(int bn, int mode = -1) {
   return (g_conv_math == 3 && bn < lim) ? (int)g_narrow_math : g_conv_math;
 }
 
+static const long g_xcd_wgrad = env_long("TDE_XCD_WGRAD", 0);
+
 template <int MODE, int BM, int BN>
-static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t st) {
+static void launch_cfg(const ConvArgs& a0, dim3 grid, hipStream_t st) {
+  ConvArgs a = a0;
+  a.xcd = (MODE == MODE_WGRAD && g_xcd_wgrad) ? 1 : 0;
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int math = tile_math(BN, MODE);
-  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 && math != 4 ? 2 : 1);
+  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? (math != 4 ? 2 : 1) : (int)g_pf128);
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 4 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
@@ -1624,7 +1682,11 @@ __global__ void __launch_bounds__(256) operand_absmax_kernel(long quads, int cq,
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  // |values| >= 0 order as their bit patterns: an unsigned max into one of the TDE_BOUND_SLOTS slots (zeroed
+  // before the launch), spread over the slots so few blocks meet on one address
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned*>(out) + (blockIdx.x & (TDE_BOUND_SLOTS - 1)),
+              __float_as_uint(fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]))));
 }
 
 // db = *d, with the gradient operand's bound (view 1: y of d; view 0: x of d) computed when math 4 needs one
@@ -1639,9 +1701,15 @@ static int bound_grad_operand(const tde_conv_desc_t* d, tde_conv_desc_t& db, int
   const long rows = yview ? (long)d->N * d->OH * d->OW : (long)d->N * d->H * d->W;
   const int C = yview ? d->K : d->C;
   const int cs = yview ? d->y_cstride : d->x_cstride, co = yview ? d->y_coff : d->x_coff;
-  static_assert(TDE_BOUND_SLOTS == 16, "one pre-pass block per bound slot");
-  hipLaunchKernelGGL(operand_absmax_kernel, dim3(TDE_BOUND_SLOTS), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     rows * (C / 4), C / 4, g, cs, co, slot);
+  static_assert((TDE_BOUND_SLOTS & (TDE_BOUND_SLOTS - 1)) == 0, "slot spread mask");
+  // ~4 quads per lane, at least one block per slot, at most 1024 blocks (the first version used one block per
+  // slot: 350 us for a 67 MB dy)
+  const long quads = rows * (C / 4);
+  const int blocks = (int)std::min(1024L, std::max((long)TDE_BOUND_SLOTS, (long)tde_cdiv(quads, 1024L)));
+  const hipError_t me = hipMemsetAsync(slot, 0, TDE_BOUND_SLOTS * sizeof(float), static_cast<hipStream_t>(stream));
+  if (me != hipSuccess) return TDE_ERR_HIP;
+  hipLaunchKernelGGL(operand_absmax_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     quads, C / 4, g, cs, co, slot);
   if (yview) db.y_absmax = slot; else db.x_absmax = slot;
   return tde_launch_status();
 }

@@ -83,9 +83,31 @@ __device__ __forceinline__ unsigned f16_lo_pair(float x0, float x1, float s, uns
   return lo;
 }
 
+// hi = fp16_rne(x*s) by pairs with v_fma_mix too (fma(x, s, 0): x*s is exact, one rounding to fp16, as
+// v_pk_mul_f32 + v_cvt_pk_f16_f32): its fp32 sources are single VGPRs, where v_pk_mul_f32 needs each pair in
+// an aligned register pair -- for the transposed staging (a row of 4 k gathered from 4 loaded vectors) hipcc
+// spent 2 v_mov per pair building them (32 per 128x128 WGRAD k-tile).  Only the sign of an exact zero can
+// differ (-0 * s + 0 = +0), which no fp32 sum of the products can observe.
+__device__ __forceinline__ unsigned f16_hi_pair(float x0, float x1, float s) {
+  unsigned hi;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %2, 0"
+      : "=&v"(hi) : "v"(x0), "v"(s), "v"(x1));
+  return hi;
+}
+
+#ifndef TDE_F16_MIX_HI
+#define TDE_F16_MIX_HI 1
+#endif
+
 __device__ __forceinline__ void split4x2h(f4 v, float s, h4& hi, h4& lo) {
+#if TDE_F16_MIX_HI
+  const h2v a = __builtin_bit_cast(h2v, f16_hi_pair(v[0], v[1], s));
+  const h2v b = __builtin_bit_cast(h2v, f16_hi_pair(v[2], v[3], s));
+#else
   const h2v a = __builtin_convertvector(f2v{v[0], v[1]} * s, h2v);
   const h2v b = __builtin_convertvector(f2v{v[2], v[3]} * s, h2v);
+#endif
   const h2v c = __builtin_bit_cast(h2v, f16_lo_pair(v[0], v[1], s, __builtin_bit_cast(unsigned, a)));
   const h2v d = __builtin_bit_cast(h2v, f16_lo_pair(v[2], v[3], s, __builtin_bit_cast(unsigned, b)));
   hi = h4{a[0], a[1], b[0], b[1]};
