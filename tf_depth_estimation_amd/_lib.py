@@ -208,16 +208,13 @@ def dedicated_stream():
     return torch.cuda.ExternalStream(s.value)
 
 
-# ---- cross-stream ordering that survives stream capture
-# Root cause of the round-2 capture_end crash (round 3, AMD_LOG_LEVEL=3 + faulthandler, probe/capture_repeat.py):
-# torch's `a.wait_stream(b)` records a TEMPORARY event on b, makes a wait on it and destroys the event at once.
-# Inside a hipStreamBeginCapture region HIP keeps a pointer to that event in the capture's bookkeeping (the
-# fork / join of the captured streams); when it has already been destroyed, hipStreamEndCapture walks freed memory
-# and segfaults (last logged calls: hipEventRecord, hipStreamWaitEvent, hipEventDestroy, hipStreamEndCapture ->
-# crash) -- reproducibly for a whole config-4 step captured as one graph with forked branches, intermittently
-# ("after ~40 captures") when the freed memory happened to survive.  Every cross-stream wait of the hot path goes
-# through wait_stream / wait_event below, which keep the event alive for the life of the process while any
-# capture is open (capture_scope).
+# ---- cross-stream ordering inside stream capture
+# torch's `a.wait_stream(b)` records a TEMPORARY event on b, waits on it and destroys it at once; inside a
+# hipStreamBeginCapture region the capture's fork / join bookkeeping refers to that event.  The hot path's
+# cross-stream waits go through wait_stream / wait_event below, which keep their events alive while any capture is
+# open (capture_scope).  This was the first suspect for the config-4 single-graph capture_end segfault; it did not
+# remove it: the bisection (probe/capture_bisect.py) pins that crash on a second-level fork (a stream
+# forked from a captured stream that is not the capture origin), which the piece capture never makes.
 _CAPTURE_DEPTH = [0]
 _CAPTURE_EVENTS = []
 

@@ -37,6 +37,10 @@ constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 // WGRAD pixel decode fast path for OW % 4 == 0 (conv_tile R4), off: ~60 VALU less per k-tile, but measured
 // neutral (big3x3 WGRAD 640 vs 649 us, config 4 8.19 vs 8.22 ms; scripts/sessions/r03n.sh) -- the loop waits
 // on its loads, not on address arithmetic -- so it is not worth the second set of WGRAD instantiations
+// TDE_DBG_PHASE (timing diagnostics only, wrong results): 1 no k-loop global loads, 2 no MFMAs, 3 no staging
+#ifndef TDE_DBG_PHASE
+#define TDE_DBG_PHASE 0
+#endif
 #ifndef TDE_WGRAD_ROW4
 #define TDE_WGRAD_ROW4 0
 #endif
@@ -362,6 +366,18 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   f4 ra1[PF == 2 ? A_PER : 1][A_V], rb1[PF == 2 ? B_PER : 1][B_V];
 
   auto load_tiles = [&](int kt, auto& ra, auto& rb) {
+#if TDE_DBG_PHASE == 1
+    // timing diagnostic (not a result): no global loads in the k-loop
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i)
+#pragma unroll
+      for (int j = 0; j < A_V; ++j) ra[i][j] = f4{1.f, 1.f, 1.f, (float)kt};
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+#pragma unroll
+      for (int j = 0; j < B_V; ++j) rb[i][j] = f4{1.f, 1.f, 1.f, (float)kt};
+    return;
+#endif
     const int kbase = kt * BK3;
     // k decode shared by every A slot (and the DGRAD B slots): s & 7 == tid & 7 for all slots
     const int kq = kbase + 4 * (tid & 7);
@@ -455,6 +471,11 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     else IB::put(Bm, row, k, v);
   };
   auto store_tiles = [&](int buf, auto& ra, auto& rb) {
+#if TDE_DBG_PHASE == 3
+    // timing diagnostic (not a result): no split / LDS staging stores (loads kept alive by one cheap use)
+    if (ra[0][0][0] == 12345.f && rb[0][0][0] == 54321.f) As0[tid] = 0;
+    return;
+#endif
     ET* A = As0 + buf * IA::SIZE;
     ET* Bm = Bs0 + buf * IB::SIZE;
 #pragma unroll
@@ -520,6 +541,18 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
+    } else if constexpr (MATH == 4 && TDE_F16_STAGE && TDE_DBG_PHASE == 2) {
+      // timing diagnostic (not a result): fragment reads, no MFMAs
+      h8 ah[TM], bh[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+      issue();
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b][0] += (float)ah[a][0] * (float)bh[b][0];
     } else if constexpr (MATH == 4 && TDE_F16_STAGE) {
       // fp16x3, staged image: hi / lo fragments straight from the planes (k-chunk q = k 8q..8q+7 for A and B)
       h8 ah[TM], al[TM], bh[TN], bl[TN];
