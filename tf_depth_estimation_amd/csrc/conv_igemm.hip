@@ -63,6 +63,7 @@ struct ConvArgs {
   // x / y, fixed weight scale; split_math.h)
   const float* xmax; const float* ymax; const float* wmax;
   int xcd;   // igemmx_kernel: XCD-grouped tile order (TDE_XCD_WGRAD)
+  int wt;    // epilogue stores written through L2 (sc1; TDE_WT): bit 0 split-K slabs, bit 1 direct outputs
 };
 
 // The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
@@ -820,6 +821,22 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       }
     }
   }
+  if (p.wt & (direct ? 2 : 1)) {
+    // write-through (sc1) stores: the tile's bytes leave no dirty L2 lines for the kernel-end release to write
+    // back (the boundary cost grows with them, MI355X_MICROARCH.md 'boundary' / 'publish-large')
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int n = n0 + wcol0 + b * 16 + r16;
+          if (rowaddr[a][r] >= 0 && n < Nn)
+            asm volatile("global_store_dword %0, %1, off sc1" : : "v"(base + rowaddr[a][r] + n), "v"(acc[a][b][r])
+                         : "memory");
+        }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -1456,8 +1473,11 @@ static bool desc_ok(const tde_conv_desc_t* d) {
   return true;
 }
 
+static const long g_wt = env_long("TDE_WT", 0);
+
 static ConvArgs make_args(const tde_conv_desc_t& d) {
   ConvArgs a{};
+  a.wt = (int)g_wt;
   a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.OH = d.OH; a.OW = d.OW; a.K = d.K;
   a.KH = d.KH; a.KW = d.KW; a.S = d.stride; a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
   a.xcs = d.x_cstride; a.xco = d.x_coff; a.ycs = d.y_cstride; a.yco = d.y_coff;
