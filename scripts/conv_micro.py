@@ -40,6 +40,10 @@ SHAPES = [
     ("upcnv4", 8, 24, 32, 128, 256, 3, 2),
     ("upcnv5", 8, 12, 16, 256, 512, 3, 2),
     ("upcnv6", 8, 6, 8, 512, 512, 3, 2),
+    # the same at config 4's twin batch (16 = the two calls of one network)
+    ("upcnv1_b16", 16, 192, 256, 16, 32, 3, 2),
+    ("upcnv2_b16", 16, 96, 128, 32, 64, 3, 2),
+    ("upcnv3_b16", 16, 48, 64, 64, 128, 3, 2),
 ]
 
 

@@ -246,6 +246,38 @@ def test_deconv2d_fwd_bwd(L, case, conv_tol):
     close(gdw, wr.grad, tol=tol, what="deconv wgrad")
 
 
+@pytest.mark.parametrize("acc", [0, 1])
+def test_deconv_pixel_shuffle_views(L, acc):
+    """The pixel-shuffle deconv forward (conv_igemm.hip MODE_PS: one GEMM over the four parity classes, taken for
+    3x3 stride-2 deconvs with >= TDE_DECONV_PS_MINM input pixels, default 8192) reading its input from a channel
+    view and writing (or accumulating) into a channel view of a wider concat buffer, the other channels untouched:
+    against the fp64 conv2d_transpose (nets_optflow_depth.py:103-140 slim.conv2d_transpose, SAME)."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, h, w_, cin, cout = 3, 48, 64, 32, 16          # 9216 input pixels: above the default threshold
+    H, W = 2 * h, 2 * w_
+    icv, ico, ocv, oco = 40, 4, 48, 16
+    x = rnd(N, h, w_, cin, seed=51)
+    wt = rnd(3, 3, cout, cin, seed=52) * 0.2
+    xin = torch.zeros(N, h, w_, icv, dtype=torch.float64)
+    xin[..., ico:ico + cin] = x
+    out0 = rnd(N, H, W, ocv, seed=53)
+    d = conv_desc(L, N=N, H=H, W=W, C=cout, OH=h, OW=w_, K=cin, KH=3, KW=3, stride=2, pad_top=0, pad_left=0,
+                  w_cin=cout, x_cstride=ocv, x_coff=oco, y_cstride=icv, y_coff=ico)
+    ws = ws_for(L, d, deconv=True)
+    gout = dev(out0)
+    L.check(lib.tde_deconv2d_fwd(ctypes.byref(d), L.ptr(dev(xin)), L.ptr(dev(wt)), L.ptr(gout), acc, L.ptr(ws),
+                                 ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    ref = T.conv2d_transpose_same(x, wt, 2)
+    want = out0.clone()
+    want[..., oco:oco + cout] = ref + (out0[..., oco:oco + cout] if acc else 0)
+    got = gout.double().cpu()
+    close(got[..., oco:oco + cout], want[..., oco:oco + cout], what="pixel-shuffle deconv view")
+    assert torch.equal(got[..., :oco], out0[..., :oco].float().double())
+    assert torch.equal(got[..., oco + cout:], out0[..., oco + cout:].float().double())
+
+
 BN_FUSED_CASES = [
     # deconv?, N, H, W, C(in view), K, k, s      (conv: input H x W;  deconv: input h x w, output 2h x 2w)
     (False, 8, 96, 128, 4, 32, 7, 2),            # cnv1: 768 row tiles, no split

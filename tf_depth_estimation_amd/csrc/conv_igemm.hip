@@ -34,6 +34,13 @@
 namespace {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
+// MODE_PS: the forward of a 3x3 stride-2 deconv (slim.conv2d_transpose, nets_optflow_depth.py:103-140) as ONE
+// pixel-shuffle GEMM instead of 4 parity-class DGRAD GEMMs: rows = input pixels (n, a, b), columns = the 2x2 output
+// block (py, px) x Cout, K = the 2x2 input neighbourhood (a - 1 + th, b - 1 + tw) x Cin -- a stride-1 2x2 forward
+// conv whose B operand is the deconv weight w[kh][kw][c][k] gathered at kh = 2 (1 - th) + py, kw = 2 (1 - tw) + px
+// (zero past the 3x3 kernel: 9 of the 16 taps x class pairs), and whose epilogue scatters column (py, px, c) to
+// output pixel (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes.
+constexpr int MODE_PS = 3;
 // WGRAD pixel decode fast path for OW % 4 == 0 (conv_tile R4), off: ~60 VALU less per k-tile, but measured
 // neutral (big3x3 WGRAD 640 vs 649 us, config 4 8.19 vs 8.22 ms; scripts/sessions/r03n.sh) -- the loop waits
 // on its loads, not on address arithmetic -- so it is not worth the second set of WGRAD instantiations
@@ -64,6 +71,9 @@ struct ConvArgs {
   const float* xmax; const float* ymax; const float* wmax;
   int xcd;   // igemmx_kernel: XCD-grouped tile order (TDE_XCD_WGRAD)
   int wt;    // epilogue stores written through L2 (sc1; TDE_WT): bit 0 split-K slabs, bit 1 direct outputs
+  // MODE_PS: deconv output channels / height / width, weight input channels (w[3][3][ps_C][ps_K])
+  int ps_C, ps_H, ps_W, ps_K;
+  FDiv fpsC;
 };
 
 // The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
@@ -277,7 +287,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
   constexpr bool A_T = (MODE == MODE_WGRAD);   // A global vectors along rows -> register transpose
-  constexpr bool B_T = (MODE != MODE_DGRAD);   // B global vectors along rows (n) -> transpose
+  constexpr bool B_T = (MODE != MODE_DGRAD && MODE != MODE_PS);   // B global vectors along rows (n) -> transpose
+  constexpr bool FWDLIKE = (MODE == MODE_FWD || MODE == MODE_PS);  // A = the forward im2col gather of x
   using IA = typename ImgSel<MATH, BM>::type;
   using IB = typename ImgSel<MATH, BN>::type;
   using ET = typename ImgSel<MATH, BM>::T;
@@ -303,7 +314,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     zsplit = bz / ncls;
     g = dg_class(p, cls);
     M = g.M; Nn = p.C; Kd = g.Kd;
-  } else if constexpr (MODE == MODE_FWD) {
+  } else if constexpr (FWDLIKE) {
     zsplit = bz;
     M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
   } else {
@@ -328,7 +339,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   // tail) gets offset OOB >= num_records and loads as zero -- no branches, no zero-fill moves.
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, (long)p.N * p.OH * p.OW * p.ycs);
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, (long)p.KH * p.KW * p.wcin * p.K);
+  const __amdgpu_buffer_rsrc_t rw =
+      make_rsrc(p.w, MODE == MODE_PS ? 9L * p.ps_C * p.ps_K : (long)p.KH * p.KW * p.wcin * p.K);
 
   // per-slot row geometry (float offsets; `pb` = element offset of the row at tap/k origin)
   int a_pb[A_PER], a_i1[A_PER], a_i2[A_PER];
@@ -336,7 +348,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   for (int i = 0; i < A_PER; ++i) {
     const int s = tid + i * NT;
     a_pb[i] = 0; a_i1[i] = -(1 << 28); a_i2[i] = -(1 << 28);   // invalid row -> every tap out of range
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (FWDLIKE) {
       const int m = m0 + (s >> 3);
       if (s < A_SLOTS && m < M) {
         const int ohw = p.OH * p.OW;
@@ -383,7 +395,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     // k decode shared by every A slot (and the DGRAD B slots): s & 7 == tid & 7 for all slots
     const int kq = kbase + 4 * (tid & 7);
     int t_h = 0, t_w = 0, koff = 0, kx = 0, dg_wtap = 0;
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (FWDLIKE) {
       const int tap = fdiv(kq, p.fC), c = kq - tap * p.C;
       t_h = fdiv(tap, p.fKW); t_w = tap - t_h * p.KW;
       koff = (t_h * p.W + t_w) * p.xcs + c;
@@ -397,7 +409,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     }
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-      if constexpr (MODE == MODE_FWD) {
+      if constexpr (FWDLIKE) {
         const bool ok = kq < Kd && (unsigned)(a_i1[i] + t_h) < (unsigned)p.H &&
                         (unsigned)(a_i2[i] + t_w) < (unsigned)p.W;
         ra[i][0] = bload(rx, ok ? 4 * (a_pb[i] + koff) : OOB);
@@ -452,6 +464,14 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const int ci = n0 + (s >> 3);
         const bool ok = slot && kq < Kd && ci < p.wcin;
         rb[i][0] = bload(rw, ok ? 4 * (dg_wtap + ci * p.K) : OOB);
+      } else if constexpr (MODE == MODE_PS) {
+        // column n = (py, px, c), k quad kq = (th, tw, kin..kin+3): w[2 (1 - th) + py][2 (1 - tw) + px][c][kin..]
+        const int n = n0 + (s >> 3);
+        const int gq = fdiv(n, p.fpsC), c = n - gq * p.ps_C;
+        const int tap = fdiv(kq, p.fC), kin = kq - tap * p.C;
+        const int kh = 2 - 2 * (tap >> 1) + (gq >> 1), kw = 2 - 2 * (tap & 1) + (gq & 1);
+        const bool ok = slot && n < Nn && kq < Kd && kh < 3 && kw < 3;
+        rb[i][0] = bload(rw, ok ? 4 * (((kh * 3 + kw) * p.ps_C + c) * p.ps_K + kin) : OOB);
       } else {
         const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
         const bool ok = slot && n < Nn;
@@ -726,7 +746,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   // sum and sum of squares over the tile's rows (rows past M hold exact zeros: their operand rows loaded
   // as zero), lanes -> waves in a fixed order, one fp64 partial per row tile.  Workgroup-local: the
   // cross-tile reduction is the next kernel's (a launch costs what an in-kernel hand-off costs).
-  if constexpr (MODE != MODE_WGRAD) {
+  if constexpr (MODE != MODE_WGRAD && MODE != MODE_PS) {
     if (p.bnp != nullptr) {
       float cs[TN], cq[TN];
 #pragma unroll
@@ -767,7 +787,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   // later load, so an interleaved read-modify-write would serialise one memory latency per element).
   const bool direct = (p.splits == 1);
   float* base;
-  if constexpr (MODE == MODE_FWD) base = direct ? p.y : p.ws;
+  if constexpr (FWDLIKE) base = direct ? p.y : p.ws;
   else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
   else base = direct ? p.dw : p.ws;
   long rowaddr[TM][4];
@@ -780,6 +800,11 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       if (m < M) {
         if constexpr (MODE == MODE_FWD) {
           ra_ = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
+        } else if constexpr (MODE == MODE_PS) {
+          // output pixel (2a, 2b) of row (n, a, b); split-K never runs in this mode (the host keeps splits 1)
+          const int ohw = p.OH * p.OW;
+          const int ni = m / ohw, rr = m - ni * ohw, aa = rr / p.OW, bb = rr - aa * p.OW;
+          ra_ = ((long)(ni * p.ps_H + 2 * aa) * p.ps_W + 2 * bb) * p.ycs + p.yco;
         } else if constexpr (MODE == MODE_DGRAD) {
           const int hw = g.HH * g.WW;
           const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
@@ -797,6 +822,20 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       rowaddr[a][r] = ra_;
     }
   }
+  // element offset of column n from its row address, and the channel of n (bias index): n itself, except MODE_PS
+  // (column (py, px, c) -> pixel (2a + py, 2b + px), channel c)
+  long coff[TN];
+  int ccol[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wcol0 + b * 16 + r16;
+    coff[b] = n; ccol[b] = n;
+    if constexpr (MODE == MODE_PS) {
+      const int gq = fdiv(n, p.fpsC);
+      ccol[b] = n - gq * p.ps_C;
+      coff[b] = (long)((gq >> 1) * p.ps_W + (gq & 1)) * p.ycs + ccol[b];
+    }
+  }
   if (direct && p.accumulate) {
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -805,7 +844,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           const int n = n0 + wcol0 + b * 16 + r16;
-          if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + n];
+          if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + coff[b]];
         }
   }
   if constexpr (MODE != MODE_WGRAD) {
@@ -813,7 +852,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wcol0 + b * 16 + r16;
-        const int nb = n < Nn ? n : 0;
+        const int nb = n < Nn ? ccol[b] : 0;
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -832,8 +871,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         for (int b = 0; b < TN; ++b) {
           const int n = n0 + wcol0 + b * 16 + r16;
           if (rowaddr[a][r] >= 0 && n < Nn)
-            asm volatile("global_store_dword %0, %1, off sc1" : : "v"(base + rowaddr[a][r] + n), "v"(acc[a][b][r])
-                         : "memory");
+            asm volatile("global_store_dword %0, %1, off sc1" : : "v"(base + rowaddr[a][r] + coff[b]),
+                         "v"(acc[a][b][r]) : "memory");
         }
     return;
   }
@@ -844,7 +883,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wcol0 + b * 16 + r16;
-        if (rowaddr[a][r] >= 0 && n < Nn) base[rowaddr[a][r] + n] = acc[a][b][r];
+        if (rowaddr[a][r] >= 0 && n < Nn) base[rowaddr[a][r] + coff[b]] = acc[a][b][r];
       }
 }
 
@@ -1509,9 +1548,73 @@ static void launch_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3((int)blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
 }
 
+// Pixel-shuffle path of the stride-2 3x3 virtual DGRAD (deconv forward; MODE_PS above).  TDE_DECONV_PS_MINM:
+// input pixels (N x OH x OW) from which it replaces the four parity-class GEMMs (0: never).  Split-K never runs
+// here (below that size the class GEMMs and their split-K remain).
+static const long g_ps_minm = env_long("TDE_DECONV_PS_MINM", 8192);
+// ... and only with enough tiles to fill the chip (the class GEMMs have 4x the tiles and split K): >= 512 blocks of
+// 128 rows, else >= 512 of 64 rows (measured, batch 8, us: upcnv1 48.2 -> 35.5 with 768 blocks of 128 rows;
+// upcnv2 28.7 -> 29.7 with 192, upcnv3 32.8 -> 37.7 with 96, upcnv4 29.5 -> 57.3 with 24: r03x)
+static const long g_ps_minblocks = env_long("TDE_DECONV_PS_MINBLOCKS", 512);
+static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr) {
+  if (!(g_ps_minm > 0 && g_conv_math == 4 && d.stride == 2 && d.KH == 3 && d.KW == 3 && d.pad_top == 0 &&
+        d.pad_left == 0 && d.H == 2 * d.OH && d.W == 2 * d.OW && d.w_cin == d.C && d.C % 16 == 0 && d.K % 4 == 0 &&
+        (long)d.N * d.OH * d.OW >= g_ps_minm))
+    return false;
+  const long M = (long)d.N * d.OH * d.OW;
+  const int Nn = 4 * d.C, BN = Nn % 128 == 0 ? 128 : 64;
+  int BM = 0;
+  if ((long)tde_cdiv(M, 128) * (Nn / BN) >= g_ps_minblocks) BM = 128;
+  else if ((long)tde_cdiv(M, 64) * (Nn / BN) >= g_ps_minblocks) BM = 64;
+  if (!BM) return false;
+  if (bm) *bm = BM;
+  if (bn) *bn = BN;
+  return true;
+}
+
+static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, const tde_bn_train_t* bn, void* ws,
+                  size_t ws_bytes, void* stream) {
+  // the virtual DGRAD's operands: input = a0.dy (view y of d, K channels), output = a0.dx (view x of d, C channels)
+  ConvArgs a{};
+  a.wt = a0.wt;
+  a.N = d->N; a.H = d->OH; a.W = d->OW; a.C = d->K; a.OH = d->OH; a.OW = d->OW; a.K = 4 * d->C;
+  a.KH = 2; a.KW = 2; a.S = 1; a.PT = 1; a.PL = 1; a.wcin = d->K;
+  a.xcs = d->y_cstride; a.xco = d->y_coff; a.ycs = d->x_cstride; a.yco = d->x_coff;
+  a.fC = make_fdiv(d->K); a.fK = make_fdiv(4 * d->C); a.fKW = make_fdiv(2); a.fOW = make_fdiv(d->OW);
+  a.fOHW = make_fdiv(d->OH * d->OW);
+  a.xmax = a0.ymax; a.wmax = a0.wmax;
+  a.x = a0.dy; a.w = a0.w; a.y = a0.dx; a.bias = a0.bias; a.relu = a0.relu;
+  a.ps_C = d->C; a.ps_H = d->H; a.ps_W = d->W; a.ps_K = d->K; a.fpsC = make_fdiv(d->C);
+  a.splits = 1; a.kt_per = tde_cdiv(4L * d->K, BK3); a.accumulate = accumulate;
+  const long M = (long)d->N * d->OH * d->OW, rows = (long)d->N * d->H * d->W;
+  const int Nn = 4 * d->C;
+  const int G = bn && bn->groups > 1 ? bn->groups : 1;
+  if (rows % G != 0) return TDE_ERR_ARG;
+  if (bn && (!ws || !tde_aligned16(ws) || bn_part_bytes(rows, d->C) > ws_bytes)) return TDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int BM = 0, BN = 0;
+  ps_ok(*d, &BM, &BN);
+  const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
+  if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  if (bn) {
+    // statistics from a grouped partial pass over z (the parity classes of a row tile are not one row range)
+    const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
+    if (rows / G <= BN_SMALL_M) bn_fwd_small_launch((int)rows, d->C, a.y, o, st);
+    else bn_fwd_standalone_launch((int)rows, d->C, a.y, o, reinterpret_cast<double*>(tde_ws_body(ws)), st);
+  }
+  return tde_launch_status();
+}
+
 template <int MODE>
 static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
                size_t ws_bytes, void* stream) {
+  if constexpr (MODE == MODE_DGRAD) {
+    if (ps_ok(*d) && !skip_conv(d)) return run_ps(d, a, accumulate, bn, ws, ws_bytes, stream);
+  }
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   HwgPlan wp;
