@@ -7,6 +7,11 @@ ParamChunk, and asserts on every rank; a non-zero exit fails the test.
   mean        : rank-dependent gradients -> every rank ends with the exact fp32 mean, buckets fire
                 during the schedule (not all at the end), each exactly once.
   uses2       : shared-variable net reported twice per step (config 4): nothing fires on pass 1.
+  two_programs: config 4 with the net overlap: disp_net's and depth_net's chunks in ONE GradSync, one backward
+                call each (twin batching, uses 1), their reports interleaved as two streams would issue them,
+                with the pre_launch / side_streams callbacks of Trainer.enable_ddp; each bucket fires once
+                during its own program's schedule, the launch callbacks see the reporting chunk, and both
+                chunks end with the exact mean.
   oracle_step : one data-parallel config-2 step: each rank takes its shard of the global batch,
                 computes the oracle gradient, writes it op by op with hooks; after the exchange and
                 the oracle Adam, parameters are bit-identical across ranks and equal to Adam applied
@@ -97,6 +102,46 @@ def case_uses2(rank, world):
     assert torch.all(chunk.grad == sum(range(1, world + 1)) / world)
 
 
+def case_two_programs(rank, world):
+    spec_s, chunk_s = build()
+    spec_p = _netlib.depth_net_spec(128, 128, 6, levels=4)
+    specs, bn = spec_p.param_specs()
+    pre_p = "model/depth_cam_net"
+    chunk_p = ParamChunk([(f"{pre_p}/{n}", s, i) for n, s, i in specs], [(f"{pre_p}/{n}", c) for n, c in bn],
+                         device="cpu", seed=2)
+    seen = []
+    gs = ddp.GradSync([chunk_s, chunk_p], world, bucket_mb=1.0, pre_launch=lambda c: seen.append(("pre", id(c))),
+                      side_streams=lambda c: (seen.append(("side", id(c))), ())[1])
+    gs.begin_step()
+    hooks = {id(chunk_s): gs.hook(chunk_s), id(chunk_p): gs.hook(chunk_p)}
+    chunk_s.grad.fill_(float(rank + 1))
+    chunk_p.grad.fill_(float(10 * (rank + 1)))
+    sched_s = schedule(spec_s)
+    sched_p = [[f"{pre_p}/{n}" for n, _, _ in op.params] for op in reversed(spec_p.ops) if op.params]
+    # interleave: depth_net's backward (the second stream) and disp_net's alternate op by op
+    order = []
+    for i in range(max(len(sched_s), len(sched_p))):
+        if i < len(sched_p):
+            order.append((chunk_p, sched_p[i]))
+        if i < len(sched_s):
+            order.append((chunk_s, sched_s[i]))
+    fired = {id(chunk_s): 0, id(chunk_p): 0}
+    for ch, names in order:
+        before = len(gs.log)
+        hooks[id(ch)](names)
+        new = gs.log[before:]
+        for nm in new:                  # every bucket that fired now belongs to the reporting chunk
+            assert all(n.startswith(pre_p if ch is chunk_p else PREFIX + "/") for n in nm), (nm[:2], id(ch))
+        fired[id(ch)] += len(new)
+    assert fired[id(chunk_s)] > 0 and fired[id(chunk_p)] > 0, fired
+    assert all(b.launched for b in gs.buckets) and not gs.leftovers(), "a bucket never reached its last report"
+    assert all(kind == "side" for kind, _ in seen), "eager launches use side_streams, never pre_launch"
+    assert {c for _, c in seen} == {id(chunk_s), id(chunk_p)}
+    gs.finish()
+    n = sum(range(1, world + 1)) / world
+    assert torch.all(chunk_s.grad == n) and torch.all(chunk_p.grad == 10 * n)
+
+
 def case_oracle_step(rank, world):
     from oracle import losses as OL
     from oracle import nets as ON
@@ -146,7 +191,8 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     try:
-        {"mean": case_mean, "uses2": case_uses2, "oracle_step": case_oracle_step}[case](rank, world)
+        {"mean": case_mean, "uses2": case_uses2, "two_programs": case_two_programs,
+         "oracle_step": case_oracle_step}[case](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

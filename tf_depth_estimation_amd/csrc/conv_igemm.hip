@@ -27,6 +27,8 @@
 #include <vector>
 #include "bn_internal.h"
 #include "split_math.h"
+
+#include <utility>
 #include "halo_conv.h"
 
 #include <cstdlib>
@@ -44,9 +46,14 @@ constexpr int MODE_PS = 3;
 // WGRAD pixel decode fast path for OW % 4 == 0 (conv_tile R4), off: ~60 VALU less per k-tile, but measured
 // neutral (big3x3 WGRAD 640 vs 649 us, config 4 8.19 vs 8.22 ms; scripts/sessions/r03n.sh) -- the loop waits
 // on its loads, not on address arithmetic -- so it is not worth the second set of WGRAD instantiations
-// TDE_DBG_PHASE (timing diagnostics only, wrong results): 1 no k-loop global loads, 2 no MFMAs, 3 no staging
+// TDE_DBG_PHASE (timing diagnostics only, wrong results), a bit mask: 1 no k-loop global loads, 2 no MFMAs,
+// 4 no staging (split + LDS stores)
 #ifndef TDE_DBG_PHASE
 #define TDE_DBG_PHASE 0
+#endif
+// TDE_PIPE: the PF 2 k-loop of the staged fp16x3 image interleaves the next tile's staging with the MFMAs
+#ifndef TDE_PIPE
+#define TDE_PIPE 1
 #endif
 #ifndef TDE_WGRAD_ROW4
 #define TDE_WGRAD_ROW4 0
@@ -379,7 +386,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   f4 ra1[PF == 2 ? A_PER : 1][A_V], rb1[PF == 2 ? B_PER : 1][B_V];
 
   auto load_tiles = [&](int kt, auto& ra, auto& rb) {
-#if TDE_DBG_PHASE == 1
+#if TDE_DBG_PHASE & 1
     // timing diagnostic (not a result): no global loads in the k-loop
 #pragma unroll
     for (int i = 0; i < A_PER; ++i)
@@ -492,7 +499,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     else IB::put(Bm, row, k, v);
   };
   auto store_tiles = [&](int buf, auto& ra, auto& rb) {
-#if TDE_DBG_PHASE == 3
+#if TDE_DBG_PHASE & 4
     // timing diagnostic (not a result): no split / LDS staging stores (loads kept alive by one cheap use)
     if (ra[0][0][0] == 12345.f && rb[0][0][0] == 54321.f) As0[tid] = 0;
     return;
@@ -523,6 +530,45 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           putB(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
       } else {
         putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
+      }
+    }
+  };
+
+  // store_tiles cut into PARTS slices (a slice = every put whose index u has u * PARTS / NPUT == part), so the
+  // staging of the next tile can be interleaved with the MFMAs of the current one (TDE_PIPE loop below)
+  constexpr int NPUT = A_PER * (A_T ? 4 : 1) + B_PER * (B_T ? 4 : 1);
+  auto store_part = [&](int buf, auto& ra, auto& rb, auto part_c, auto parts_c) {
+    constexpr int PART = decltype(part_c)::value, PARTS = decltype(parts_c)::value;
+    ET* A = As0 + buf * IA::SIZE;
+    ET* Bm = Bs0 + buf * IB::SIZE;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int s = tid + i * NT;
+#pragma unroll
+      for (int rr = 0; rr < (A_T ? 4 : 1); ++rr) {
+        const int u = i * (A_T ? 4 : 1) + rr;
+        if (u * PARTS / NPUT != PART || s >= A_SLOTS) continue;
+        if constexpr (A_T) {
+          const int r0 = 4 * (s % (BM / 4)), k0 = 4 * (s / (BM / 4));
+          putA(A, r0 + rr, k0, f4{ra[i][0][rr], ra[i][1][rr], ra[i][2][rr], ra[i][3][rr]});
+        } else {
+          putA(A, s >> 3, 4 * (s & 7), ra[i][0]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int s = tid + i * NT;
+#pragma unroll
+      for (int rr = 0; rr < (B_T ? 4 : 1); ++rr) {
+        const int u = A_PER * (A_T ? 4 : 1) + i * (B_T ? 4 : 1) + rr;
+        if (u * PARTS / NPUT != PART || s >= B_SLOTS) continue;
+        if constexpr (B_T) {
+          const int r0 = 4 * (s % (BN / 4)), k0 = 4 * (s / (BN / 4));
+          putB(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
+        } else {
+          putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
+        }
       }
     }
   };
@@ -562,7 +608,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
-    } else if constexpr (MATH == 4 && TDE_F16_STAGE && TDE_DBG_PHASE == 2) {
+    } else if constexpr (MATH == 4 && TDE_F16_STAGE && (TDE_DBG_PHASE & 2)) {
       // timing diagnostic (not a result): fragment reads, no MFMAs
       h8 ah[TM], bh[TN];
 #pragma unroll
@@ -694,12 +740,69 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     }
   };
 
+  // TDE_PIPE (PF 2, staged fp16x3): one k-tile = fragment reads of tile k, global loads of tile k+2, then the MFMAs
+  // of tile k with the split + LDS stores of tile k+1 (loaded one iteration earlier) between their rows -- the
+  // staging's VALU and LDS stores issue while the matrix pipe runs, instead of after it (sched_barrier keeps
+  // hipcc from clustering them again)
+  auto compute_pipe = [&](int cur, auto&& issue, int buf, auto& ra, auto& rb) {
+   if constexpr (MATH == 4 && TDE_F16_STAGE) {
+    const ET* A = As0 + cur * IA::SIZE;
+    const ET* Bm = Bs0 + cur * IB::SIZE;
+    h8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
+      al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
+    }
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
+      bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
+    }
+    issue();
+    auto row = [&](auto a_c) {
+      constexpr int a = decltype(a_c)::value;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+      }
+      store_part(buf, ra, rb, a_c, std::integral_constant<int, TM>{});
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(TM <= 8, "rows");
+    row(std::integral_constant<int, 0>{});
+    if constexpr (TM > 1) row(std::integral_constant<int, 1>{});
+    if constexpr (TM > 2) row(std::integral_constant<int, 2>{});
+    if constexpr (TM > 3) row(std::integral_constant<int, 3>{});
+    if constexpr (TM > 4) row(std::integral_constant<int, 4>{});
+    if constexpr (TM > 5) row(std::integral_constant<int, 5>{});
+    if constexpr (TM > 6) row(std::integral_constant<int, 6>{});
+    if constexpr (TM > 7) row(std::integral_constant<int, 7>{});
+   }
+  };
+
   if (kt0 < kt1) {
     load_tiles(kt0, ra0, rb0);
     store_tiles(0, ra0, rb0);
     __syncthreads();
     int cur = 0;
-    if constexpr (PF == 1) {
+    if constexpr (PF == 2 && MATH == 4 && TDE_F16_STAGE && TDE_PIPE && !(TDE_DBG_PHASE & 6)) {
+      const int klast = kt1 - 1;
+      load_tiles(min(kt0 + 1, klast), ra1, rb1);
+      int kt = kt0;
+      while (true) {
+        compute_pipe(cur, [&] { load_tiles(min(kt + 2, klast), ra0, rb0); }, cur ^ 1, ra1, rb1);
+        __syncthreads();
+        cur ^= 1;
+        if (++kt >= kt1) break;
+        compute_pipe(cur, [&] { load_tiles(min(kt + 2, klast), ra1, rb1); }, cur ^ 1, ra0, rb0);
+        __syncthreads();
+        cur ^= 1;
+        if (++kt >= kt1) break;
+      }
+    } else if constexpr (PF == 1) {
       // one tile in flight: the load of tile kt+1 overlaps the MFMAs of tile kt
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = (kt + 1 < kt1);
@@ -1410,6 +1513,8 @@ static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
 // TDE_PF128: prefetch depth of the 128-row tiles (2: two k-tiles in flight, capped at 256 VGPRs = 2 waves per
 // SIMD by TDE_PF2_WAVES -- the occupancy the 128-row tiles have anyway, 64 KiB of LDS per workgroup)
 static const long g_pf128 = env_long("TDE_PF128", 1);
+// TDE_PF64: the same for the 64-row tiles in fp16x3 (2: 153 VGPRs, still 3 waves per SIMD, with the pipelined loop)
+static const long g_pf64 = env_long("TDE_PF64", 1);
 // wave layout of a tile: 2 x 2 waves when BN is a multiple of TDE_WN_DIV, else 4 x 1 (all rows split)
 #ifndef TDE_WN_DIV
 #define TDE_WN_DIV 32
@@ -1438,7 +1543,7 @@ static void launch_cfg(const ConvArgs& a0, dim3 grid, hipStream_t st) {
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int math = tile_math(BN, MODE);
-  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? (math != 4 ? 2 : 1) : (int)g_pf128);
+  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? (math != 4 ? 2 : (int)g_pf64) : (int)g_pf128);
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 4 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
