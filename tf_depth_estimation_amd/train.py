@@ -871,6 +871,8 @@ class DepthThenCamTrainer(Trainer):
         if self.graphs is None or getattr(self, "ov_seq", None) is None:
             return super().step()
         cur, ov = torch.cuda.current_stream(), self.net_stream
+        if os.environ.get("TDE_C4_OV_SERIAL") == "1":
+            ov = cur        # diagnostic: the same piece graphs replayed one after another on one stream
         gs = self.grad_sync
         seg = gs is not None and hasattr(gs, "begin_step")
         if seg:
