@@ -340,6 +340,8 @@ class NetProgram:
         # filter-gradient blocks ride along, instead of queueing on the side stream behind the high-resolution
         # layers' filter gradients (0: every layer but the tail goes to the side stream)
         self.wgrad_inline_m = _env_nonneg("TDE_WGRAD_INLINE_M", 0)
+        # the heads' filter gradients join the side stream too (their data gradient stays on the compute stream)
+        self.head_wgrad_side = _env_nonneg("TDE_HEAD_WGRAD_SIDE", 1) > 0
         self._ws2 = {}
         self._dzl = {}
         self._wsplit = {}       # (N, conv math) -> pre-split weight images (_split_plan)
@@ -829,12 +831,38 @@ class NetProgram:
             elif isinstance(op, Head):
                 d = op.desc(N)
                 acc = mark(op.src) if src_needs else 0
+                hw, hgw, hgb = (ptr(self.P(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/weights")),
+                                ptr(self.G(f"{op.layer}/biases")))
+                if side is not None and self.head_wgrad_side:
+                    # the head's filter gradient joins the deferred group on the side stream (it reads x, y and
+                    # dy, none of which the rest of backward rewrites); the data gradient stays on this stream
+                    def head_wgrad_call(wsp, wsb2, d=d, x=run.vptr(op.src), y=run.vptr(op.dst),
+                                        dy=run.vptr(op.dst, True), op=op, hw=hw, hgw=hgw, hgb=hgb):
+                        _lib.check(lib.tde_head_bwd(ctypes_ref(d), x, hw, y, dy, None, 0, hgw, hgb, pacc, op.act,
+                                                    op.scale, op.offset, wsp, wsb2, _lib.stream_ptr()),
+                                   op.layer + " head wgrad")
+                    self._wg_pending.append((head_wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
+                    ev = None
+                    if len(self._wg_pending) >= self.wgrad_group:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    if src_needs:
+                        _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), hw, run.vptr(op.dst),
+                                                    run.vptr(op.dst, True), run.vptr(op.src, True), acc, None, None,
+                                                    0, op.act, op.scale, op.offset, ptr(ws), wsb, st),
+                                   op.layer + " head dgrad")
+                    if ev is not None:
+                        self._flush_wgrad(ev)
+                    names, self._wg_issued = self._wg_issued, []
+                    if on_grads is not None and names:
+                        on_grads(names)
+                    continue
                 with self._span("head_bwd", 2 * conv_flops(op, N)):
-                    _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), ptr(self.P(f"{op.layer}/weights")),
+                    _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), hw,
                                                 run.vptr(op.dst), run.vptr(op.dst, True),
                                                 run.vptr(op.src, True) if src_needs else None, acc,
-                                                ptr(self.G(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/biases")),
-                                                pacc, op.act, op.scale, op.offset, ptr(ws), wsb, st), op.layer + " bwd")
+                                                hgw, hgb, pacc, op.act, op.scale, op.offset, ptr(ws), wsb, st),
+                               op.layer + " bwd")
                 if on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Resize):
