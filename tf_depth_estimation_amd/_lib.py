@@ -192,18 +192,25 @@ _hip = None
 _own_streams = []
 
 
-def dedicated_stream():
-    """A HIP stream of its own (hipStreamCreateWithFlags, non-blocking) wrapped as a torch ExternalStream, kept for
-    the life of the process.  torch.cuda.Stream() hands out streams from a fixed round-robin pool, so after enough
-    of them a "new" stream can be the very HIP stream a graph is being captured on or another side stream: a
-    cross-stream wait between the two is then a self-wait, and one such capture crashed in capture_end."""
+def dedicated_stream(priority=None):
+    """A HIP stream of its own (non-blocking) wrapped as a torch ExternalStream, kept for the life of the process.
+    torch.cuda.Stream() hands out streams from a fixed round-robin pool, so after enough of them a "new" stream can
+    be the very HIP stream a graph is being captured on or another side stream: a cross-stream wait between the two
+    is then a self-wait.  priority: None (default), "high" or "low" (hipStreamCreateWithPriority over the device's
+    range; the hardware queue's priority orders the dispatch of workgroups from concurrently runnable kernels)."""
     global _hip
     if _hip is None:
         _hip = ctypes.CDLL("libamdhip64.so")
     s = ctypes.c_void_p()
-    rc = _hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
+    if priority in ("high", "low"):
+        least, greatest = ctypes.c_int(), ctypes.c_int()
+        _hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
+        pv = greatest.value if priority == "high" else least.value
+        rc = _hip.hipStreamCreateWithPriority(ctypes.byref(s), ctypes.c_uint(1), ctypes.c_int(pv))
+    else:
+        rc = _hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
     if rc != 0 or not s.value:
-        raise TdeError(f"hipStreamCreateWithFlags failed ({rc})")
+        raise TdeError(f"hip stream creation failed ({rc})")
     _own_streams.append(s)
     return torch.cuda.ExternalStream(s.value)
 
@@ -250,14 +257,14 @@ def wait_event(stream, ev):
     _keep(ev)
 
 
-def owned_stream(owner, name):
+def owned_stream(owner, name, priority=None):
     """A dedicated stream (dedicated_stream) cached on `owner` under `name`: created once per owner and role, so
     re-enabling an overlap or re-capturing a step never allocates another HIP stream, and no two roles ever share
-    one (the pool aliasing dedicated_stream avoids)."""
+    one (the pool aliasing dedicated_stream avoids).  The priority applies when the stream is first created."""
     cache = owner.__dict__.setdefault("_tde_streams", {})
     st = cache.get(name)
     if st is None:
-        st = cache[name] = dedicated_stream()
+        st = cache[name] = dedicated_stream(priority)
     return st
 
 

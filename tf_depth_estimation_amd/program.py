@@ -467,7 +467,8 @@ class NetProgram:
         serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
         # dedicated HIP streams, one per role and program (torch.cuda.Stream() recycles a fixed pool: a pooled
         # side stream can alias a capture stream or another program's side stream, _lib.dedicated_stream)
-        self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0")) if on else None
+        prio = os.environ.get("TDE_WGRAD_PRIO") or None     # filter-gradient stream priority ("low" / "high")
+        self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0", prio)) if on else None
         # TDE_WGRAD_STREAMS > 1: the filter-gradient groups alternate over that many side streams (each with its
         # own workspace), so independent filter gradients may run concurrently with each other
         n = 1 if (serial or not on) else _env_pos("TDE_WGRAD_STREAMS", 1)

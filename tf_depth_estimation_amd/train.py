@@ -261,7 +261,8 @@ class Trainer:
         (enable_ddp).  Not combinable with the Adam overlaps or SyncBN."""
         if on and (self.adam_ov is not None or self.dadam is not None or getattr(self, "sync_bn", False)):
             raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / SyncBN")
-        self.net_stream = _lib.owned_stream(self, "net") if on else None
+        # TDE_NET_PRIO: priority of the second stream ("high": its network is the longer chain of config 4)
+        self.net_stream = _lib.owned_stream(self, "net", os.environ.get("TDE_NET_PRIO") or None) if on else None
         return self
 
     def _overlap_stream(self):
