@@ -342,6 +342,10 @@ typedef struct {
   int grad_accumulate;
 } tde_depth_loss_t;
 int tde_loss_depth_pyramid(const tde_depth_loss_t* args, void* stream);
+/* n <= TDE_PYR_MULTI_MAX independent tde_loss_depth_pyramid calls (config 4's four disparity maps) in ONE launch:
+ * same results as n calls when their grad views are disjoint (the loss sums are fp64 atomics either way). */
+#define TDE_PYR_MULTI_MAX 4
+int tde_loss_depth_pyramid_multi(const tde_depth_loss_t* args, int n, void* stream);
 
 /* ---------------------------------------------------------------- projective warp loss head
  * Fused forward + hand-derived backward of the per-scale self-supervised terms of
@@ -382,6 +386,13 @@ typedef struct {
 } tde_warp_loss_t;
 int tde_warp_loss(const tde_warp_loss_t* args, void* stream);
 size_t tde_warp_loss_det_workspace_size(int B, int H, int W);
+/* n <= TDE_WARP_MULTI_MAX tde_warp_loss calls in ONE launch (the per-scale calls of one direction of
+ * train_depth_then_cam_lr.py:253-340: 8 launches per step become 2).  The calls must write disjoint
+ * g_disp / g_logits views (those are plain +=; the g_other / loss / g_P sums are atomics as in tde_warp_loss),
+ * must all have det_ws == NULL and either all or none compute g_P.  Results equal n tde_warp_loss calls up to
+ * the float-atomic order. */
+#define TDE_WARP_MULTI_MAX 8
+int tde_warp_loss_multi(const tde_warp_loss_t* args, int n, void* stream);
 
 /* Forward-only projective_inverse_warp (utils_lr.py:222-256) / bilinear_sampler (:276-366): coords from
  * depth (or 1/disp when depth_is_disp) through P and Kinv, or given coords_in [B,H,W,2] when depth is
@@ -396,6 +407,14 @@ int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_di
  * T may be NULL.  K is [B][9]. */
 int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const float* K, float* T,
                   float* P, float* Kinv, void* stream);
+/* n <= TDE_WARP_MULTI_MAX independent tde_pose_prep calls (every scale and direction of the config-4 loss) in
+ * ONE launch; same arguments per job, same results. */
+typedef struct {
+  int B;
+  const float* pose_vec; const float* pose_mat; const float* K;
+  float* T; float* P; float* Kinv;
+} tde_pose_prep_t;
+int tde_pose_prep_multi(const tde_pose_prep_t* jobs, int n, void* stream);
 /* ---- reference-named geometry ops with their backward (the un-fused utils_lr.py path; the host layer
  * tf_depth_estimation_amd/utils_lr.py wraps them as autograd functions).
  * pose_vec2mat(vec, format) (utils_lr.py:106-149): vec [B][6] (tx,ty,tz,rx,ry,rz) -> T [B][16];

@@ -52,6 +52,15 @@ class WarpLossArgs(ctypes.Structure):
                 ("det_ws", P), ("det_ws_bytes", c_size_t)]
 
 
+class PosePrepArgs(ctypes.Structure):
+    """Mirror of tde_pose_prep_t (include/tde.h): one job of tde_pose_prep_multi."""
+    _fields_ = [("B", c_int), ("pose_vec", P), ("pose_mat", P), ("K", P), ("T", P), ("P", P), ("Kinv", P)]
+
+
+WARP_MULTI_MAX = 8      # TDE_WARP_MULTI_MAX
+PYR_MULTI_MAX = 4       # TDE_PYR_MULTI_MAX
+
+
 class DepthLoss(ctypes.Structure):
     """Mirror of tde_depth_loss_t (include/tde.h): the multi-scale smooth + depth-L1 loss head."""
     _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("nscales", c_int),
@@ -73,6 +82,9 @@ _SIGS = {
     "tde_conv2d_split_weights": (c_int, [c_int, P, P, P, P, P]),
     "tde_image_resize_unpack": (c_int, [P, P]),
     "tde_loss_depth_pyramid": (c_int, [P, P]),
+    "tde_warp_loss_multi": (c_int, [P, c_int, P]),
+    "tde_loss_depth_pyramid_multi": (c_int, [P, c_int, P]),
+    "tde_pose_prep_multi": (c_int, [P, c_int, P]),
     "tde_warp_loss": (c_int, [P, P]),
     "tde_warp_loss_det_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),

@@ -220,12 +220,12 @@ struct PyrArgs {
 // terms exist) and every second difference is formed from them in the same fp32 order as t_dx2 / t_dxdy /
 // t_dydx / t_dy2 (the same fp32 expressions as the per-term evaluation).  32-bit index math; the
 // per-scale weights are precomputed on the host exactly as before (double, then rounded to float).
-__global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
+__device__ __forceinline__ void depth_pyramid_block(const PyrArgs& P, const int bid) {
   __shared__ double sh[4];
   const tde_depth_loss_t& a = P.a;
   double ls = 0.0, ll = 0.0;
   int s = 0;
-  while ((int)blockIdx.x >= P.bstart[s + 1]) ++s;
+  while (bid >= P.bstart[s + 1]) ++s;
   s = __builtin_amdgcn_readfirstlane(s);
   const int H = a.H >> s, W = a.W >> s;
   const int total = a.N * H * W;
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
   const int pcs = a.pred_cs[s], pco = a.pred_co[s];
   const bool smooth = a.smooth_w[s] != 0.f && H >= 3 && W >= 3;
   const float w1 = P.w1[s], w23 = P.w23[s], w4 = P.w4[s];
-  for (int loc = (blockIdx.x - P.bstart[s]) * 256 + threadIdx.x; loc < total; loc += nb * 256) {
+  for (int loc = (bid - P.bstart[s]) * 256 + threadIdx.x; loc < total; loc += nb * 256) {
     const int t = loc / W;
     const int j = loc - t * W;
     const int n = t / H, i = t - n * H;
@@ -328,6 +328,21 @@ __global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) {
   }
 }
 
+__global__ void __launch_bounds__(256) depth_pyramid_kernel(const PyrArgs P) { depth_pyramid_block(P, blockIdx.x); }
+
+// tde_loss_depth_pyramid_multi: map m owns blocks [mstart[m], mstart[m+1]) of the grid
+struct PyrMulti {
+  PyrArgs p[TDE_PYR_MULTI_MAX];
+  int mstart[TDE_PYR_MULTI_MAX + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) depth_pyramid_multi_kernel(const PyrMulti M) {
+  int m = 0;
+  while (m + 1 < M.n && (int)blockIdx.x >= M.mstart[m + 1]) ++m;
+  depth_pyramid_block(M.p[m], (int)blockIdx.x - M.mstart[m]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -376,9 +391,9 @@ int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int cof
 // (TDE_PYR_MAXB tuning knob; a missing, non-numeric or non-positive value means the default)
 static const long g_pyr_maxb = tde_env_pos("TDE_PYR_MAXB", 192);
 
-int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
+// host-side setup of one map's launch arguments (argument checks, per-scale block ranges and weights)
+static int pyr_setup(const tde_depth_loss_t* a, PyrArgs& P) {
   TDE_CHECK_ARG(a && a->N > 0 && a->H > 0 && a->W > 0 && a->nscales >= 1 && a->nscales <= TDE_MAX_SCALES);
-  PyrArgs P;
   P.a = *a;
   P.bstart[0] = 0;
   for (int s = 0; s < a->nscales; ++s) {
@@ -409,8 +424,30 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
     P.l1d[s] = on ? (double)a->l1_w[s] / tot : 0.0;
     P.l1f[s] = on ? (float)(a->l1_w[s] / tot) : 0.f;
   }
+  return TDE_OK;
+}
+
+int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
+  PyrArgs P;
+  const int rc = pyr_setup(a, P);
+  if (rc != TDE_OK) return rc;
   hipLaunchKernelGGL(depth_pyramid_kernel, dim3(P.bstart[a->nscales]), dim3(256), 0,
                      static_cast<hipStream_t>(stream), P);
+  return tde_launch_status();
+}
+
+int tde_loss_depth_pyramid_multi(const tde_depth_loss_t* args, int n, void* stream) {
+  TDE_CHECK_ARG(args && n > 0 && n <= TDE_PYR_MULTI_MAX);
+  PyrMulti M;
+  M.n = n;
+  M.mstart[0] = 0;
+  for (int m = 0; m < n; ++m) {
+    const int rc = pyr_setup(args + m, M.p[m]);
+    if (rc != TDE_OK) return rc;
+    M.mstart[m + 1] = M.mstart[m] + M.p[m].bstart[args[m].nscales];
+  }
+  hipLaunchKernelGGL(depth_pyramid_multi_kernel, dim3(M.mstart[n]), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     M);
   return tde_launch_status();
 }
 

@@ -63,10 +63,11 @@ __device__ __forceinline__ double det_scale(const tde_warp_loss_t& a, const Warp
   return ldexp(1.0, 62 - e);
 }
 
+// One block of one call: block bx of gdx along the pixels of batch element b.
 template <bool NEED_G_P, bool DET>
-__global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a, const WarpDet det) {
+__device__ __forceinline__ void warp_loss_block(const tde_warp_loss_t& a, const WarpDet& det, const int bx,
+                                                const int b, const int gdx) {
   __shared__ double sh[16][4];
-  const int b = blockIdx.y;
   const int HW = a.H * a.W;
   // per-thread fp64 accumulators over a grid-stride loop: a capped grid (tde_warp_loss) keeps the
   // block-end fp64 atomics on the shared loss / dL/dP words few
@@ -76,7 +77,7 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a,
   for (int i = 0; i < 12; ++i) gp[i] = 0.0;
   const double inv_n3 = 1.0 / (3.0 * a.B * HW), inv_n = 1.0 / ((double)a.B * HW);
   const double dscale = DET ? det_scale(a, det) : 0.0;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < HW; idx += gridDim.x * blockDim.x) {
+  for (int idx = bx * blockDim.x + threadIdx.x; idx < HW; idx += gdx * blockDim.x) {
     const int y = idx / a.W, x = idx - y * a.W;
     const long pix = (long)b * HW + idx;
     // ---- coordinates (cam2pixel of pixel2cam) or grid + flow
@@ -239,13 +240,37 @@ __global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a,
     const int i = threadIdx.x;
     const double s = sh[i][0] + sh[i][1] + sh[i][2] + sh[i][3];
     if (DET) {
-      det.part[((long)b * gridDim.x + blockIdx.x) * 15 + i] = s;
+      det.part[((long)b * gdx + bx) * 15 + i] = s;
     } else if (i < 3) {
       if (s != 0.0) atomicAdd(a.loss + i, s);
     } else {
       atomicAdd(a.g_P + 12 * b + (i - 3), s);
     }
   }
+}
+
+template <bool NEED_G_P, bool DET>
+__global__ void __launch_bounds__(256) warp_loss_kernel(const tde_warp_loss_t a, const WarpDet det) {
+  warp_loss_block<NEED_G_P, DET>(a, det, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// Several calls in ONE launch (tde_warp_loss_multi): call c owns blocks [start[c], start[c+1]) of a 1-D grid, gx[c]
+// per batch element.  The calls' gradient outputs must be disjoint (float += without atomics on g_disp / g_logits).
+struct WarpMulti {
+  tde_warp_loss_t a[TDE_WARP_MULTI_MAX];
+  int start[TDE_WARP_MULTI_MAX + 1];
+  int gx[TDE_WARP_MULTI_MAX];
+  int n;
+};
+
+template <bool NEED_G_P>
+__global__ void __launch_bounds__(256) warp_loss_multi_kernel(const WarpMulti m) {
+  const int id = blockIdx.x;
+  int c = 0;
+  while (c + 1 < m.n && id >= m.start[c + 1]) ++c;
+  const int local = id - m.start[c], gx = m.gx[c];
+  const WarpDet none{nullptr, nullptr, nullptr};
+  warp_loss_block<NEED_G_P, false>(m.a[c], none, local % gx, local / gx, gx);
 }
 
 // Deterministic mode, before the loss kernel: zero the fixed-point sums and raise the bound slot to
@@ -320,10 +345,8 @@ __device__ void inv3(const float* K, float* Ki) {
   Ki[6] = C * id; Ki[7] = -(a * h - b * g) * id; Ki[8] = (a * e - b * d) * id;
 }
 
-__global__ void pose_prep_kernel(int B, const float* vec, const float* mat, const float* K, float* T, float* P,
-                                 float* Kinv) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+__device__ __forceinline__ void pose_prep_one(int b, const float* vec, const float* mat, const float* K, float* T,
+                                              float* P, float* Kinv) {
   float Tm[16];
   if (vec) {
     float R[9];
@@ -342,6 +365,23 @@ __global__ void pose_prep_kernel(int B, const float* vec, const float* mat, cons
     for (int j = 0; j < 4; ++j)
       P[12 * b + 4 * i + j] = Kb[3 * i] * Tm[j] + Kb[3 * i + 1] * Tm[4 + j] + Kb[3 * i + 2] * Tm[8 + j];
   inv3(Kb, Kinv + 9 * b);
+}
+
+__global__ void pose_prep_kernel(int B, const float* vec, const float* mat, const float* K, float* T, float* P,
+                                 float* Kinv) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) pose_prep_one(b, vec, mat, K, T, P, Kinv);
+}
+
+// tde_pose_prep_multi: job blockIdx.y of up to TDE_WARP_MULTI_MAX independent tde_pose_prep calls
+struct PoseMulti {
+  tde_pose_prep_t j[TDE_WARP_MULTI_MAX];
+};
+
+__global__ void pose_prep_multi_kernel(const PoseMulti m) {
+  const tde_pose_prep_t& j = m.j[blockIdx.y];
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < j.B) pose_prep_one(b, j.pose_vec, j.pose_mat, j.K, j.T, j.P, j.Kinv);
 }
 
 // dL/dvec from dL/dP (all scales summed: gP[s][b][12], K_s at Ks + b*k_stride_b + 9*s) and an
@@ -765,6 +805,34 @@ int tde_warp_loss(const tde_warp_loss_t* a, void* stream) {
   return tde_launch_status();
 }
 
+int tde_warp_loss_multi(const tde_warp_loss_t* args, int n, void* stream) {
+  TDE_CHECK_ARG(args && n > 0 && n <= TDE_WARP_MULTI_MAX);
+  static const long maxb = tde_env_pos("TDE_WARP_MAXB", 512);
+  WarpMulti m;
+  m.n = n;
+  m.start[0] = 0;
+  const bool gp = args[0].g_P && args[0].disp;
+  for (int c = 0; c < n; ++c) {
+    const tde_warp_loss_t* a = args + c;
+    TDE_CHECK_ARG(a->B > 0 && a->H > 0 && a->W > 0 && a->img_src && a->img_tgt && a->loss);
+    TDE_CHECK_ARG((a->disp != nullptr) != (a->flow != nullptr));
+    TDE_CHECK_ARG(!a->disp || (a->P && a->Kinv));
+    TDE_CHECK_ARG(!a->disp_other || a->disp);
+    TDE_CHECK_ARG(a->det_ws == nullptr);                   // the deterministic scatter runs per call (tde_warp_loss)
+    TDE_CHECK_ARG((a->g_P && a->disp) == gp);               // one kernel variant for all calls
+    int gx = (a->H * a->W + 255) / 256;
+    const int cap = (int)std::max(1L, maxb / a->B);
+    if (gx > cap) gx = cap;
+    m.a[c] = *a;
+    m.gx[c] = gx;
+    m.start[c + 1] = m.start[c] + gx * a->B;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (gp) hipLaunchKernelGGL(warp_loss_multi_kernel<true>, dim3(m.start[n]), dim3(256), 0, st, m);
+  else hipLaunchKernelGGL(warp_loss_multi_kernel<false>, dim3(m.start[n]), dim3(256), 0, st, m);
+  return tde_launch_status();
+}
+
 size_t tde_warp_loss_det_workspace_size(int B, int H, int W) {
   if (B <= 0 || H <= 0 || W <= 0) return 0;
   static const long maxb = tde_env_pos("TDE_WARP_MAXB", 512);
@@ -779,6 +847,21 @@ int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const flo
   TDE_CHECK_ARG(B > 0 && (pose_vec || pose_mat) && K && P && Kinv);
   hipLaunchKernelGGL(pose_prep_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B,
                      pose_vec, pose_mat, K, T, P, Kinv);
+  return tde_launch_status();
+}
+
+int tde_pose_prep_multi(const tde_pose_prep_t* jobs, int n, void* stream) {
+  TDE_CHECK_ARG(jobs && n > 0 && n <= TDE_WARP_MULTI_MAX);
+  PoseMulti m;
+  int bmax = 0;
+  for (int c = 0; c < n; ++c) {
+    const tde_pose_prep_t& j = jobs[c];
+    TDE_CHECK_ARG(j.B > 0 && (j.pose_vec || j.pose_mat) && j.K && j.P && j.Kinv);
+    m.j[c] = j;
+    bmax = std::max(bmax, j.B);
+  }
+  hipLaunchKernelGGL(pose_prep_multi_kernel, dim3((bmax + 63) / 64, n), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     m);
   return tde_launch_status();
 }
 

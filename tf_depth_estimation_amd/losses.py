@@ -74,6 +74,25 @@ def pyramid(preds, grads, acc, smooth_w, slot_smooth, recip=False, coff=0, label
     label, mean|nf(resize_area(label, s) - pred_s)| in ONE launch (tde_loss_depth_pyramid): the same
     fp32 expressions as smooth() + area() + l1() per scale.  preds[s] / grads[s]: NHWC [N,H>>s,W>>s,C]
     dense tensors (same C); label: full-resolution [N,H,W] / [N,H,W,1]; smooth_w / l1_w: per-scale weights."""
+    a = _pyramid_args(preds, grads, acc, smooth_w, slot_smooth, recip, coff, label, l1_w, slot_l1, nonfinite,
+                      accumulate)
+    _lib.call("tde_loss_depth_pyramid", ctypes.byref(a), _lib.stream_ptr())
+
+
+def pyramid_multi(maps):
+    """Several pyramid() calls (keyword dicts of its arguments) in ONE launch (tde_loss_depth_pyramid_multi); their
+    grads must be disjoint views."""
+    n = len(maps)
+    if not 0 < n <= _lib.PYR_MULTI_MAX:
+        raise ValueError(f"1..{_lib.PYR_MULTI_MAX} maps per launch")
+    arr = (_lib.DepthLoss * n)()
+    for i, kw in enumerate(maps):
+        arr[i] = _pyramid_args(**kw)
+    _lib.call("tde_loss_depth_pyramid_multi", arr, n, _lib.stream_ptr())
+
+
+def _pyramid_args(preds, grads, acc, smooth_w, slot_smooth, recip=False, coff=0, label=None, l1_w=None, slot_l1=None,
+                  nonfinite=False, accumulate=True):
     n = len(preds)
     N, H, W, C = preds[0].shape
     a = _lib.DepthLoss()
@@ -89,7 +108,7 @@ def pyramid(preds, grads, acc, smooth_w, slot_smooth, recip=False, coff=0, label
     a.label = ptr(label) if label is not None else None
     a.loss_smooth = dptr(acc, slot_smooth)
     a.loss_l1 = dptr(acc, slot_l1) if slot_l1 is not None else None
-    _lib.call("tde_loss_depth_pyramid", ctypes.byref(a), _lib.stream_ptr())
+    return a
 
 
 def smooth(pred, g, weight, acc, slot, recip=False, coff=0):
@@ -131,6 +150,31 @@ def warp_loss(acc, slot0, img_src, img_tgt, P=None, Kinv=None, disp=None, flow=N
     """One direction of the fused projective-warp loss head (include/tde.h tde_warp_loss).  All NHWC
     tensors are dense; acc[slot0 .. slot0+2] += (photo, exp, consist).  det_ws: a device buffer of at least
     tde_warp_loss_det_workspace_size bytes selects the deterministic (run-to-run bit-identical) scatter."""
+    a = _warp_args(img_src, img_tgt, P, Kinv, disp, flow, wmask, logits, disp_other, photo_w, exp_w, consist_w,
+                   g_disp, g_flow, g_logits, g_other, g_P, det_ws)
+    a.loss = dptr(acc, slot0)
+    _lib.call("tde_warp_loss", ctypes.byref(a), _lib.stream_ptr())
+
+
+def warp_loss_multi(acc, slot0, calls):
+    """Several warp_loss calls (keyword dicts of warp_loss's arguments after slot0) in ONE launch
+    (tde_warp_loss_multi).  The calls must write disjoint g_disp / g_logits views, e.g. the four scales of one
+    direction; each call's deterministic scatter needs its own launch, so det_ws must be absent."""
+    n = len(calls)
+    if not 0 < n <= _lib.WARP_MULTI_MAX:
+        raise ValueError(f"1..{_lib.WARP_MULTI_MAX} calls per launch")
+    arr = (WarpLossArgs * n)()
+    for i, kw in enumerate(calls):
+        if kw.get("det_ws") is not None:
+            raise ValueError("the deterministic scatter runs per call: use warp_loss")
+        arr[i] = _warp_args(**kw)
+        arr[i].loss = dptr(acc, slot0)
+    _lib.call("tde_warp_loss_multi", arr, n, _lib.stream_ptr())
+
+
+def _warp_args(img_src, img_tgt, P=None, Kinv=None, disp=None, flow=None, wmask=None, logits=None, disp_other=None,
+               photo_w=0.0, exp_w=0.0, consist_w=0.0, g_disp=None, g_flow=None, g_logits=None, g_other=None, g_P=None,
+               det_ws=None):
     B, H, W, _ = img_tgt.shape
     a = WarpLossArgs()
     a.B, a.H, a.W = B, H, W
@@ -145,11 +189,10 @@ def warp_loss(acc, slot0, img_src, img_tgt, P=None, Kinv=None, disp=None, flow=N
     if disp_other is not None:
         a.disp_other, a.other_cs, a.other_co = ptr(disp_other), disp_other.shape[-1], 0
     a.photo_w, a.exp_w, a.consist_w = photo_w, exp_w, consist_w
-    a.loss = dptr(acc, slot0)
     a.g_disp, a.g_flow, a.g_logits, a.g_other, a.g_P = ptr(g_disp), ptr(g_flow), ptr(g_logits), ptr(g_other), ptr(g_P)
     if det_ws is not None:
         a.det_ws, a.det_ws_bytes = ptr(det_ws), det_ws.numel() * det_ws.element_size()
-    _lib.call("tde_warp_loss", ctypes.byref(a), _lib.stream_ptr())
+    return a
 
 
 def det_workspace(B, H, W):
@@ -162,6 +205,19 @@ def det_workspace(B, H, W):
 def pose_prep(K, T=None, P=None, Kinv=None, vec=None, mat=None):
     B = K.shape[0]
     _lib.call("tde_pose_prep", B, ptr(vec), ptr(mat), ptr(K), ptr(T), ptr(P), ptr(Kinv), _lib.stream_ptr())
+
+
+def pose_prep_multi(jobs):
+    """Several pose_prep calls (keyword dicts: K, T, P, Kinv, vec, mat) in ONE launch (tde_pose_prep_multi)."""
+    n = len(jobs)
+    if not 0 < n <= _lib.WARP_MULTI_MAX:
+        raise ValueError(f"1..{_lib.WARP_MULTI_MAX} jobs per launch")
+    arr = (_lib.PosePrepArgs * n)()
+    for i, j in enumerate(jobs):
+        arr[i].B = j["K"].shape[0]
+        arr[i].pose_vec, arr[i].pose_mat = ptr(j.get("vec")), ptr(j.get("mat"))
+        arr[i].K, arr[i].T, arr[i].P, arr[i].Kinv = ptr(j["K"]), ptr(j.get("T")), ptr(j["P"]), ptr(j["Kinv"])
+    _lib.call("tde_pose_prep_multi", arr, n, _lib.stream_ptr())
 
 
 def new(shape, dtype=torch.float32):

@@ -7,6 +7,7 @@ into a hipGraph (torch.cuda.CUDAGraph) and replay it with zero host work per ste
   DepthOnlyTrainer   config 2 -- train_depth_only.py:108-219 (disp_net, smooth + depth L1, Adam)
 """
 import os
+import warnings
 
 import torch
 
@@ -20,6 +21,24 @@ W_CONFIG2 = dict(smooth=1.0, depth=1.0)     # train_depth_only.py:33-37
 # being recorded; under the default "global" mode that poll is an illegal call during capture and
 # aborts the process (hipErrorStreamCaptureUnsupported).
 CAPTURE_MODE = "thread_local"
+# config 4's per-scale pose and warp-loss calls as multi-call launches (TDE_LOSS_MULTI=0: one launch per call, A/B)
+LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
+
+
+def _end_segment(g):
+    """capture_end() of one graph segment; None when nothing was recorded into it (a bucket launch point right
+    at a piece boundary).  An empty segment is dropped instead of replayed: its buckets launch after the
+    previous segment, which is where the stream's tail already is."""
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        g.capture_end()
+    empty = False
+    for w in caught:
+        if "CUDA Graph is empty" in str(w.message):
+            empty = True
+        else:
+            warnings.warn_explicit(w.message, w.category, w.filename, w.lineno)
+    return None if empty else g
 
 
 class Adam:
@@ -459,8 +478,7 @@ class Trainer:
         state = {"g": torch.cuda.CUDAGraph()}
 
         def cut(buckets):
-            state["g"].capture_end()
-            segs.append((state["g"], list(buckets)))
+            segs.append((_end_segment(state["g"]), list(buckets)))
             state["g"] = torch.cuda.CUDAGraph()
             state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
 
@@ -470,8 +488,7 @@ class Trainer:
             with torch.cuda.stream(cs):
                 state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                 self.phase_compute()
-                state["g"].capture_end()
-                segs.append((state["g"], gs.leftovers()))
+                segs.append((_end_segment(state["g"]), gs.leftovers()))
                 upd = torch.cuda.CUDAGraph()
                 upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                 self.phase_update()
@@ -480,7 +497,7 @@ class Trainer:
             gs.capturing = None
         torch.cuda.synchronize()
         self.segments = segs
-        self.graphs = [g for g, _ in segs] + [upd]
+        self.graphs = [g for g, _ in segs if g is not None] + [upd]
         return self.graphs
 
     def step(self):
@@ -490,7 +507,8 @@ class Trainer:
             gs = self.grad_sync
             gs.begin_step()
             for g, buckets in self.segments:
-                g.replay()
+                if g is not None:
+                    g.replay()
                 if buckets:
                     for b in buckets:
                         b.launched = True
@@ -836,8 +854,7 @@ class DepthThenCamTrainer(Trainer):
                 state = {"g": torch.cuda.CUDAGraph()}
 
                 def cut(buckets, state=state, segs=segs, stream=stream):
-                    state["g"].capture_end()
-                    segs.append((state["g"], list(buckets)))
+                    segs.append((_end_segment(state["g"]), list(buckets)))
                     state["g"] = torch.cuda.CUDAGraph()
                     state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
 
@@ -846,8 +863,7 @@ class DepthThenCamTrainer(Trainer):
                         gs.capturing = cut
                     state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                     fn()
-                    state["g"].capture_end()
-                    segs.append((state["g"], []))
+                    segs.append((_end_segment(state["g"]), []))
                 seq.append((where, segs))
             if seg:
                 gs.capturing = None
@@ -863,7 +879,7 @@ class DepthThenCamTrainer(Trainer):
                 gs.capturing = None
         torch.cuda.synchronize()
         self.ov_seq = seq
-        self.graphs = [g for _, segs in seq if segs is not None for g, _ in segs]
+        self.graphs = [g for _, segs in seq if segs is not None for g, _ in segs if g is not None]
         if seg:
             self.graphs.append(self.ov_upd[1])
         return self.graphs
@@ -886,7 +902,8 @@ class DepthThenCamTrainer(Trainer):
                 ov.wait_stream(cur)
             with torch.cuda.stream(ov if where == "ov" else cur):
                 for g, buckets in segs:
-                    g.replay()
+                    if g is not None:
+                        g.replay()
                     if buckets:
                         for b in buckets:
                             b.launched = True
@@ -910,27 +927,45 @@ class DepthThenCamTrainer(Trainer):
             else:
                 Ls.area(self.img["l"], self.pyr["l"][s])
                 Ls.area(self.img["r"], self.pyr["r"][s])
-        for s in range(4):
-            for d in ("lr", "rl"):
-                Ls.pose_prep(self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
-                             vec=self.pose[d])
+        jobs = [dict(K=self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
+                     vec=self.pose[d]) for s in range(4) for d in ("lr", "rl")]
+        if LOSS_MULTI:
+            Ls.pose_prep_multi(jobs)
+        else:
+            for j in jobs:
+                Ls.pose_prep(j["K"], T=j["T"], P=j["P"], Kinv=j["Kinv"], vec=j["vec"])
         S = self.SLOTS
         _lib.check(lib.tde_cam_loss(B, ptr(self.gt_cam), ptr(self.T["lr"]), ptr(self.T["rl"]), w["cam"],
                                     Ls.dptr(self.acc, S["cam"]), ptr(self.gT["lr"]), ptr(self.gT["rl"]), st), "cam")
         # smoothness of 1/disp on the 4 maps at every scale (:216-225) and, on the single left net, the depth L1
         # to the area-downsampled label with replace_nonfinite (:227-232,241-243): one multi-scale launch per map
         sw = [w["smooth"] / 2 ** s for s in range(4)]
-        for k in ("pl", "pr", "sr"):
-            Ls.pyramid(out[k][:4], self.d_out[k][:4], self.acc, sw, S["smooth"], recip=True)
-        Ls.pyramid(out["sl"][:4], self.d_out["sl"][:4], self.acc, sw, S["smooth"], recip=True, label=self.label,
-                   l1_w=[w["depth"]] * 4, slot_l1=S["depth"], nonfinite=True)
-        for s in range(4):
-            for tgt, src, run, oth, d in (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl")):
-                Ls.warp_loss(self.acc, S["photo"], self.pyr[src][s], self.pyr[tgt][s], P=self.P[d][s],
-                             Kinv=self.Kinv[s], disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s],
-                             photo_w=w["data"], exp_w=w["exp"], consist_w=w["depth"], g_disp=self.d_out[run][s],
-                             g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s],
-                             det_ws=self.det_ws)
+        maps = [dict(preds=out[k][:4], grads=self.d_out[k][:4], acc=self.acc, smooth_w=sw, slot_smooth=S["smooth"],
+                     recip=True) for k in ("pl", "pr", "sr")]
+        maps.append(dict(preds=out["sl"][:4], grads=self.d_out["sl"][:4], acc=self.acc, smooth_w=sw,
+                         slot_smooth=S["smooth"], recip=True, label=self.label, l1_w=[w["depth"]] * 4,
+                         slot_l1=S["depth"], nonfinite=True))
+        if LOSS_MULTI:
+            Ls.pyramid_multi(maps)        # the four maps' gradients are disjoint buffers
+        else:
+            for m in maps:
+                Ls.pyramid(**m)
+        dirs = (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl"))
+        calls = {d: [dict(img_src=self.pyr[src][s], img_tgt=self.pyr[tgt][s], P=self.P[d][s], Kinv=self.Kinv[s],
+                          disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s], photo_w=w["data"],
+                          exp_w=w["exp"], consist_w=w["depth"], g_disp=self.d_out[run][s],
+                          g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s],
+                          det_ws=self.det_ws) for s in range(4)]
+                 for tgt, src, run, oth, d in dirs}
+        if LOSS_MULTI and self.det_ws is None:
+            # one launch per direction over the 4 scales (a direction's calls write disjoint g_disp / g_logits;
+            # the two directions of one scale do not: g_disp of one is g_other of the other)
+            for d in ("lr", "rl"):
+                Ls.warp_loss_multi(self.acc, S["photo"], calls[d])
+        else:
+            for s in range(4):
+                for d in ("lr", "rl"):
+                    Ls.warp_loss(self.acc, S["photo"], **calls[d][s])
         # pose gradients -> pose_pred (spatial mean backward)
         for run_key, d in (("pl", "lr"), ("pr", "rl")):
             _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
