@@ -235,7 +235,8 @@ class DataLoader(object):
         # (with worker processes the thread pool only serves the rare re-stage: keep it small, fewer threads
         # competing for the GIL with the consumer)
         self._pool = ThreadPoolExecutor(self._workers if self._procs == 0 else 1)
-        self._copy = torch.cuda.Stream()
+        # a dedicated HIP stream: a pooled torch.cuda.Stream() can alias a trainer's capture or side stream
+        self._copy = _lib.dedicated_stream()
         self._dev = torch.cuda.current_device()
         self._thread = threading.Thread(target=self._produce, daemon=True)
         self._started = True
