@@ -6,6 +6,7 @@ already loaded (one runtime per process: torch's streams and allocations are val
 There is no fallback: if the library is missing, `load()` raises.
 """
 import ctypes
+import gc
 import os
 
 import torch  # noqa: F401  (must be imported first, see module docstring)
@@ -238,15 +239,30 @@ _CAPTURE_DEPTH = [0]
 _CAPTURE_EVENTS = []
 
 
+_GC_WAS_ON = [False]
+
+
 class capture_scope:
-    """Context manager around every stream-capture region: events used for cross-stream waits inside it are kept."""
+    """Context manager around every stream-capture region: events used for cross-stream waits inside it are kept,
+    and Python's cyclic garbage collector is run once before the region and held off inside it.  A collection
+    inside a capture can destroy an unreachable older trainer's graphs (hipGraphExecDestroy and the release of
+    their memory pool, which frees device memory) while the capture is open: the process aborted that way in
+    test_net_overlap_matches_serial (r03s2c, "Fatal Python error: Aborted" while "Garbage-collecting" under
+    Trainer.capture).  torch.cuda.graph() collects before its own capture_begin but not inside; the piece and
+    segmented captures call capture_begin directly."""
 
     def __enter__(self):
+        if _CAPTURE_DEPTH[0] == 0:
+            _GC_WAS_ON[0] = gc.isenabled()
+            gc.collect()
+            gc.disable()
         _CAPTURE_DEPTH[0] += 1
         return self
 
     def __exit__(self, *exc):
         _CAPTURE_DEPTH[0] -= 1
+        if _CAPTURE_DEPTH[0] == 0 and _GC_WAS_ON[0]:
+            gc.enable()
         return False
 
 

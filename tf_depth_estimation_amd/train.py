@@ -25,6 +25,12 @@ CAPTURE_MODE = "thread_local"
 LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
 
 
+def _halves(a, b):
+    """True when dense tensors a and b are the two consecutive halves of one buffer (b starts where a ends)."""
+    return (a.is_contiguous() and b.is_contiguous() and a.shape == b.shape and
+            b.data_ptr() == a.data_ptr() + a.numel() * a.element_size())
+
+
 def _end_segment(g):
     """capture_end() of one graph segment; None when nothing was recorded into it (a bucket launch point right
     at a piece boundary).  An empty segment is dropped instead of replayed: its buckets launch after the
@@ -676,8 +682,11 @@ class DepthThenCamTrainer(Trainer):
         else:
             self.pyr = {k: [self.img[k]] + [new(s) for s in _scale_shapes(B, H, W, 3)[1:]] for k in ("l", "r")}
         self.Ks = [new((B, 9)) for _ in range(4)]
-        self.pose = {"lr": new((B, 6)), "rl": new((B, 6))}
-        self.g_pose = {"lr": new((B, 6)), "rl": new((B, 6))}
+        # the two directions' pose vectors (and gradients) as halves of one [2B, 6] tensor: with twin batching the
+        # pose maps of the pair net's two calls are the halves of one output, so one spatial-mean launch serves both
+        self.pose2, self.g_pose2 = new((2 * B, 6)), new((2 * B, 6))
+        self.pose = {"lr": self.pose2[:B], "rl": self.pose2[B:]}
+        self.g_pose = {"lr": self.g_pose2[:B], "rl": self.g_pose2[B:]}
         self.T = {"lr": new((B, 16)), "rl": new((B, 16))}
         self.P = {d: [new((B, 12)) for _ in range(4)] for d in ("lr", "rl")}
         self.Kinv = [new((B, 9)) for _ in range(4)]
@@ -917,10 +926,13 @@ class DepthThenCamTrainer(Trainer):
         lib, st = _lib.load(), _lib.stream_ptr()
         B, w, out = self.N, self.w, self._out
         # pose_final = reduce_mean(pose_pred, [1,2]) (nets_optflow_depth.py:183-186)
-        for run_key, d in (("pl", "lr"), ("pr", "rl")):
-            pp = out[run_key][4]
-            _lib.check(lib.tde_spatial_mean_fwd(B, pp.shape[1] * pp.shape[2], 6, ptr(pp), 6, ptr(self.pose[d]), st),
-                       "pose mean")
+        pl, pr = out["pl"][4], out["pr"][4]
+        hw = pl.shape[1] * pl.shape[2]
+        if LOSS_MULTI and _halves(pl, pr):
+            _lib.check(lib.tde_spatial_mean_fwd(2 * B, hw, 6, ptr(pl), 6, ptr(self.pose2), st), "pose mean")
+        else:
+            for pp, d in ((pl, "lr"), (pr, "rl")):
+                _lib.check(lib.tde_spatial_mean_fwd(B, hw, 6, ptr(pp), 6, ptr(self.pose[d]), st), "pose mean")
         for s in range(1, 4):
             if self.twin:
                 Ls.area(self.img_lr, self.pyr_lr[s])
@@ -967,12 +979,15 @@ class DepthThenCamTrainer(Trainer):
                 for d in ("lr", "rl"):
                     Ls.warp_loss(self.acc, S["photo"], **calls[d][s])
         # pose gradients -> pose_pred (spatial mean backward)
-        for run_key, d in (("pl", "lr"), ("pr", "rl")):
+        for d in ("lr", "rl"):
             _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
                                          ptr(self.g_pose[d]), 0, st), "pose grad")
-            gpp = self.d_out[run_key][4]
-            _lib.check(lib.tde_spatial_mean_bwd(B, gpp.shape[1] * gpp.shape[2], 6, ptr(gpp), 6, 0,
-                                                ptr(self.g_pose[d]), st), "pose mean bwd")
+        gl, gr = self.d_out["pl"][4], self.d_out["pr"][4]
+        if LOSS_MULTI and _halves(gl, gr):
+            _lib.check(lib.tde_spatial_mean_bwd(2 * B, hw, 6, ptr(gl), 6, 0, ptr(self.g_pose2), st), "pose mean bwd")
+        else:
+            for gpp, d in ((gl, "lr"), (gr, "rl")):
+                _lib.check(lib.tde_spatial_mean_bwd(B, hw, 6, ptr(gpp), 6, 0, ptr(self.g_pose[d]), st), "pose mean bwd")
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
