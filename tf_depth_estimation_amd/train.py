@@ -750,6 +750,14 @@ class DepthThenCamTrainer(Trainer):
         M = self.N * self.H * self.W
         self.arena.zero()
         # pair inputs: tf.concat([L, R], axis=3) and [R, L] (:146,152)
+        if self.twin:
+            # channels 0-2 of [concat(L,R); concat(R,L)] are [L; R] = img_lr: one copy for both halves
+            _lib.check(lib.tde_copy_view(2 * M, 3, ptr(self.img_lr), 3, 0, ptr(self.pair_in), 6, 0, 0, st), "concat")
+            _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["r"]), 3, 0, ptr(self.pair_in[:self.N]), 6, 3, 0, st),
+                       "concat")
+            _lib.check(lib.tde_copy_view(M, 3, ptr(self.img["l"]), 3, 0, ptr(self.pair_in[self.N:]), 6, 3, 0, st),
+                       "concat")
+            return
         for key, (a, b) in (("lr", ("l", "r")), ("rl", ("r", "l"))):
             if self.twin:
                 dst = self.pair_in[:self.N] if key == "lr" else self.pair_in[self.N:]
