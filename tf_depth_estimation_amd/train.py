@@ -23,6 +23,8 @@ W_CONFIG2 = dict(smooth=1.0, depth=1.0)     # train_depth_only.py:33-37
 CAPTURE_MODE = "thread_local"
 # config 4's per-scale pose and warp-loss calls as multi-call launches (TDE_LOSS_MULTI=0: one launch per call, A/B)
 LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
+# config 4 as two independent per-network chains with one join (TDE_C4_CHAINS=0: the two-join schedule, A/B)
+C4_CHAINS = os.environ.get("TDE_C4_CHAINS", "1") != "0"
 
 
 def _halves(a, b):
@@ -742,10 +744,32 @@ class DepthThenCamTrainer(Trainer):
         bwd = {"pair": self._p_bwd_pair, "single": self._p_bwd_single}
         o = self.ov_net if self.ov_net in fwd else "pair"
         m = "single" if o == "pair" else "pair"
+        if C4_CHAINS:
+            # disp_net's outputs enter only its own loss terms (smoothness of both maps, the depth L1 of the left;
+            # train_depth_then_cam_lr.py:211-355, oracle.losses.loss_depth_then_cam_lr), so each network's
+            # forward -> loss -> backward -> Adam is an independent chain: ONE join at the end of the step instead
+            # of a join before the loss, and the depth_net-dependent loss runs beside disp_net's backward.  The
+            # second stream waits only for the inputs (concat + image area pyramids)
+            chain = {"pair": self._chain_pair, "single": self._chain_single}
+            return [("main", self._p_inputs), ("ov", chain[o]), ("main", chain[m]), ("join", None)]
         return [("main", self._p_inputs), ("ov", fwd[o]), ("main", fwd[m]), ("join", None),
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
+    def _chain_pair(self):
+        self._p_fwd_pair()
+        self._p_loss()
+        self._p_bwd_pair()
+
+    def _chain_single(self):
+        self._p_fwd_single()
+        self._p_bwd_single()
+
     def _p_inputs(self):
+        self._p_concat()
+        if C4_CHAINS:
+            self._area_pyramids()
+
+    def _p_concat(self):
         lib, st = _lib.load(), _lib.stream_ptr()
         M = self.N * self.H * self.W
         self.arena.zero()
@@ -785,6 +809,38 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._out["sl"] = self.single.forward(self.runs["sl"], self.img["l"])
             self._out["sr"] = self.single.forward(self.runs["sr"], self.img["r"])
+        if LOSS_MULTI:
+            from . import losses as Ls
+            # the loss terms that need only this network's outputs and the inputs run here, on this network's
+            # stream: disp_net's smoothness + depth-L1 pyramids (and, in the two-join schedule, the image area
+            # pyramids, before the join beside the other network's forward); the rest of the loss needs depth_net's
+            # outputs (_p_loss)
+            if not C4_CHAINS:
+                self._area_pyramids()
+            Ls.pyramid_multi([self._pyramid_map(k) for k in ("sr", "sl")])
+        elif C4_CHAINS:
+            from . import losses as Ls
+            for k in ("sr", "sl"):
+                Ls.pyramid(**self._pyramid_map(k))
+
+    def _area_pyramids(self):
+        from . import losses as Ls
+        for s in range(1, 4):
+            if self.twin:
+                Ls.area(self.img_lr, self.pyr_lr[s])
+            else:
+                Ls.area(self.img["l"], self.pyr["l"][s])
+                Ls.area(self.img["r"], self.pyr["r"][s])
+
+    def _pyramid_map(self, k):
+        """Arguments of one map's smoothness of 1/disp at every scale (:216-225); on the single left net also the
+        depth L1 to the area-downsampled label with replace_nonfinite (:227-232,241-243)."""
+        w, S = self.w, self.SLOTS
+        m = dict(preds=self._out[k][:4], grads=self.d_out[k][:4], acc=self.acc,
+                 smooth_w=[w["smooth"] / 2 ** s for s in range(4)], slot_smooth=S["smooth"], recip=True)
+        if k == "sl":
+            m.update(label=self.label, l1_w=[w["depth"]] * 4, slot_l1=S["depth"], nonfinite=True)
+        return m
 
     # each net runs twice (shared variables): the first backward call overwrites its gradients, the second
     # accumulates -- no zeroed gradient buffer needed.  Twin: one call per net overwrites them.
@@ -941,12 +997,8 @@ class DepthThenCamTrainer(Trainer):
         else:
             for pp, d in ((pl, "lr"), (pr, "rl")):
                 _lib.check(lib.tde_spatial_mean_fwd(B, hw, 6, ptr(pp), 6, ptr(self.pose[d]), st), "pose mean")
-        for s in range(1, 4):
-            if self.twin:
-                Ls.area(self.img_lr, self.pyr_lr[s])
-            else:
-                Ls.area(self.img["l"], self.pyr["l"][s])
-                Ls.area(self.img["r"], self.pyr["r"][s])
+        if not LOSS_MULTI and not C4_CHAINS:
+            self._area_pyramids()
         jobs = [dict(K=self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
                      vec=self.pose[d]) for s in range(4) for d in ("lr", "rl")]
         if LOSS_MULTI:
@@ -958,18 +1010,13 @@ class DepthThenCamTrainer(Trainer):
         _lib.check(lib.tde_cam_loss(B, ptr(self.gt_cam), ptr(self.T["lr"]), ptr(self.T["rl"]), w["cam"],
                                     Ls.dptr(self.acc, S["cam"]), ptr(self.gT["lr"]), ptr(self.gT["rl"]), st), "cam")
         # smoothness of 1/disp on the 4 maps at every scale (:216-225) and, on the single left net, the depth L1
-        # to the area-downsampled label with replace_nonfinite (:227-232,241-243): one multi-scale launch per map
-        sw = [w["smooth"] / 2 ** s for s in range(4)]
-        maps = [dict(preds=out[k][:4], grads=self.d_out[k][:4], acc=self.acc, smooth_w=sw, slot_smooth=S["smooth"],
-                     recip=True) for k in ("pl", "pr", "sr")]
-        maps.append(dict(preds=out["sl"][:4], grads=self.d_out["sl"][:4], acc=self.acc, smooth_w=sw,
-                         slot_smooth=S["smooth"], recip=True, label=self.label, l1_w=[w["depth"]] * 4,
-                         slot_l1=S["depth"], nonfinite=True))
+        # to the area-downsampled label with replace_nonfinite (:227-232,241-243): one multi-scale launch per map,
+        # or (LOSS_MULTI) depth_net's two maps in one launch here, disp_net's two before the join (_p_fwd_single)
         if LOSS_MULTI:
-            Ls.pyramid_multi(maps)        # the four maps' gradients are disjoint buffers
+            Ls.pyramid_multi([self._pyramid_map(k) for k in ("pl", "pr")])   # disjoint gradient buffers
         else:
-            for m in maps:
-                Ls.pyramid(**m)
+            for k in ("pl", "pr") if C4_CHAINS else ("pl", "pr", "sr", "sl"):
+                Ls.pyramid(**self._pyramid_map(k))
         dirs = (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl"))
         calls = {d: [dict(img_src=self.pyr[src][s], img_tgt=self.pyr[tgt][s], P=self.P[d][s], Kinv=self.Kinv[s],
                           disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s], photo_w=w["data"],
