@@ -163,6 +163,21 @@ class AdamOverlap:
             _lib.wait_stream(torch.cuda.current_stream(), st)
 
 
+class ChainAdam(AdamOverlap):
+    """Config 4's overlapped network (depth_net) in the two-chain schedule: its Adam per gradient bucket on that
+    network's filter-gradient stream as soon as backward has finalised the bucket (AdamOverlap with
+    on_wgrad_stream), so the update hides under the rest of its backward instead of ending the step's critical
+    chain.  begin_step() / finish() run on the chain's own stream, inside its captured piece; no other stream is
+    involved (the base class's side stream stays unused and is never waited on)."""
+
+    def finish(self):
+        rest = [b for b in self.buckets if id(b) not in self.done]
+        if rest:
+            self.launch(rest)
+        for st in set(self.streams.values()):
+            _lib.wait_stream(torch.cuda.current_stream(), st)
+
+
 class DeferredAdam:
     """Single-GPU: the optimizer step of step k runs at the START of step k+1 on a side stream, overlapped
     with that step's forward, which waits (per parameter bucket, in forward order) only for the buckets of
@@ -431,6 +446,9 @@ class Trainer:
 
     def hook(self, chunk):
         """on_grads callback for NetProgram.backward (None without an overlapped exchange)."""
+        cadam = getattr(self, "_cadam", None)
+        if cadam is not None and id(chunk) in cadam.streams:
+            return cadam.hook(chunk)
         if self.adam_ov is not None:
             return self.adam_ov.hook(chunk)
         gs = self.grad_sync
@@ -756,13 +774,40 @@ class DepthThenCamTrainer(Trainer):
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
     def _chain_pair(self):
+        cadam = self._chain_adam("pair")
+        if cadam is not None:
+            cadam.begin_step()
         self._p_fwd_pair()
         self._p_loss()
         self._p_bwd_pair()
+        if cadam is not None:
+            cadam.finish()
 
     def _chain_single(self):
+        cadam = self._chain_adam("single")
+        if cadam is not None:
+            cadam.begin_step()
         self._p_fwd_single()
         self._p_bwd_single()
+        if cadam is not None:
+            cadam.finish()
+
+    def _chain_adam(self, net):
+        """ChainAdam of `net` when that network is the overlapped one of the two-chain schedule and runs its
+        filter gradients on ONE side stream, with TDE_C4_CHAIN_ADAM=1 (default off: measured 1043 -> 777 pairs/s,
+        profiles/ab_r03s2e_chain_adam.txt); else None (inline Adam after its backward)."""
+        if not (self._inline_adam() and C4_CHAINS and net == self.ov_net and self._overlap_stream() is not None
+                and os.environ.get("TDE_C4_CHAIN_ADAM", "0") == "1"):
+            return None
+        p = getattr(self, net)
+        if p.wgrad_stream is None or isinstance(p.wgrad_stream, str) or len(p.wgrad_streams) != 1:
+            return None
+        c = getattr(self, "_cadam", None)
+        if c is None or c.streams.get(id(p.chunk)) is not p.wgrad_stream:
+            opt = self.opt.opts[0 if net == "single" else 1]
+            c = self._cadam = ChainAdam([opt], float(os.environ.get("TDE_C4_CHAIN_ADAM_MB", "16")),
+                                        {id(p.chunk): self.BACKWARD_USES}, streams={id(p.chunk): p.wgrad_stream})
+        return c
 
     def _p_inputs(self):
         self._p_concat()
@@ -861,7 +906,7 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("pr", self.pair, True)
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
-        if self._inline_adam():
+        if self._inline_adam() and self._chain_adam("pair") is None:
             self.opt.opts[1].step()
 
     def _p_bwd_single(self):
@@ -870,7 +915,7 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("sr", self.single, True)
             self._bwd("sl", self.single, False)
-        if self._inline_adam():
+        if self._inline_adam() and self._chain_adam("single") is None:
             self.opt.opts[0].step()
 
     def phase_compute(self):
