@@ -442,6 +442,18 @@ int tde_pose_dp_to_dt(int B, const float* K, const double* gP, float* dT, void* 
 int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, long k_stride_b,
                   const double* gP, const float* gT_extra, float* g_pose_vec, int accumulate,
                   void* stream);
+/* n <= TDE_WARP_MULTI_MAX tde_pose_grad jobs in ONE launch, each optionally followed by the backward of
+ * pose_avg = reduce_mean(pose_pred, [1, 2]) (nets_optflow_depth.py:183-186; tde_spatial_mean_bwd with C = 6):
+ * dpose [B][hw] rows of dpose_cstride floats, channels 0..5 (+)= g_pose_vec / hw.  Same results as tde_pose_grad
+ * followed by tde_spatial_mean_bwd per job (config 4's two directions: 4 launches become 1). */
+typedef struct {
+  int B, nscales;
+  const float* pose_vec; const float* K; long k_stride_b;
+  const double* gP; const float* gT_extra;
+  float* g_pose_vec; int accumulate;
+  float* dpose; int hw, dpose_cstride, dpose_accumulate;   /* dpose NULL: no spatial-mean backward */
+} tde_pose_grad_t;
+int tde_pose_grad_spread(const tde_pose_grad_t* jobs, int n, void* stream);
 /* Config 4 cam loss (train_depth_then_cam_lr.py:278-286): w*mean((T_gt-T_lr)^2) +
  * w*mean((inv(T_gt)-T_rl)^2); loss += value, gT_lr/gT_rl += gradients. */
 int tde_cam_loss(int B, const float* gt_vec, const float* T_lr, const float* T_rl, float weight,

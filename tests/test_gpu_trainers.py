@@ -591,3 +591,37 @@ def test_depth_pyramid_multi_matches_per_map():
             assert torch.equal(g0[k][s], g1[k][s])
     assert torch.allclose(a0, a1, rtol=1e-9, atol=1e-12)
     assert a0[1].item() > 0
+
+
+def test_pose_grad_spread_matches_pose_grad_and_spatial_mean_bwd():
+    """tde_pose_grad_spread (config 4's two directions: pose gradient + spatial-mean backward, one launch) equals
+    tde_pose_grad followed by tde_spatial_mean_bwd per direction, bit for bit (accumulating and overwriting)."""
+    from tf_depth_estimation_amd import _lib
+    from tf_depth_estimation_amd._lib import ptr
+    B, hw = 5, 12
+    g = np.random.default_rng(61)
+    K = intrinsics(B, 48, 64).reshape(B, 36).contiguous().cuda()
+    pose = [small_pose(B, 62 + j).cuda() for j in range(2)]
+    gP = [torch.tensor(g.standard_normal((4, B, 12)), dtype=torch.float64).cuda() for _ in range(2)]
+    gT = [torch.tensor(g.standard_normal((B, 16)), dtype=torch.float32).cuda() for _ in range(2)]
+    lib, st = _lib.load(), _lib.stream_ptr()
+    for acc in (0, 1):
+        res = []
+        for fused in (False, True):
+            gv = [torch.full((B, 6), 0.25, device="cuda") for _ in range(2)]
+            dp = [torch.full((B, 3, 4, 6), -0.5, device="cuda") for _ in range(2)]
+            if fused:
+                jobs = (_lib.PoseGradArgs * 2)()
+                for j in range(2):
+                    jobs[j] = _lib.PoseGradArgs(B, 4, ptr(pose[j]), ptr(K), 36, ptr(gP[j]), ptr(gT[j]), ptr(gv[j]), acc,
+                                                ptr(dp[j]), hw, 6, acc)
+                _lib.check(lib.tde_pose_grad_spread(jobs, 2, st))
+            else:
+                for j in range(2):
+                    _lib.check(lib.tde_pose_grad(B, 4, ptr(pose[j]), ptr(K), 36, ptr(gP[j]), ptr(gT[j]), ptr(gv[j]),
+                                                 acc, st))
+                    _lib.check(lib.tde_spatial_mean_bwd(B, hw, 6, ptr(dp[j]), 6, acc, ptr(gv[j]), st))
+            torch.cuda.synchronize()
+            res.append((gv, dp))
+        for j in range(2):
+            assert torch.equal(res[0][0][j], res[1][0][j]) and torch.equal(res[0][1][j], res[1][1][j])

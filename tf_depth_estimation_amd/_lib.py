@@ -58,6 +58,13 @@ class PosePrepArgs(ctypes.Structure):
     _fields_ = [("B", c_int), ("pose_vec", P), ("pose_mat", P), ("K", P), ("T", P), ("P", P), ("Kinv", P)]
 
 
+class PoseGradArgs(ctypes.Structure):
+    """Mirror of tde_pose_grad_t (include/tde.h): one job of tde_pose_grad_spread."""
+    _fields_ = [("B", c_int), ("nscales", c_int), ("pose_vec", P), ("K", P), ("k_stride_b", ctypes.c_long),
+                ("gP", P), ("gT_extra", P), ("g_pose_vec", P), ("accumulate", c_int),
+                ("dpose", P), ("hw", c_int), ("dpose_cstride", c_int), ("dpose_accumulate", c_int)]
+
+
 WARP_MULTI_MAX = 8      # TDE_WARP_MULTI_MAX
 PYR_MULTI_MAX = 4       # TDE_PYR_MULTI_MAX
 
@@ -86,6 +93,7 @@ _SIGS = {
     "tde_warp_loss_multi": (c_int, [P, c_int, P]),
     "tde_loss_depth_pyramid_multi": (c_int, [P, c_int, P]),
     "tde_pose_prep_multi": (c_int, [P, c_int, P]),
+    "tde_pose_grad_spread": (c_int, [P, c_int, P]),
     "tde_warp_loss": (c_int, [P, P]),
     "tde_warp_loss_det_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "tde_warp_fwd": (c_int, [c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, c_int, c_int, P, P, P, P, P, P, P]),

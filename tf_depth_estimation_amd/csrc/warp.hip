@@ -386,10 +386,47 @@ __global__ void pose_prep_multi_kernel(const PoseMulti m) {
 
 // dL/dvec from dL/dP (all scales summed: gP[s][b][12], K_s at Ks + b*k_stride_b + 9*s) and an
 // optional extra dL/dT [B][16] (cam loss).  Rodrigues backward (utils_lr.py:77-103,126-134).
+__device__ void pose_grad_one(int b, int B, int nscales, const float* vec, const float* Ks, long k_stride_b,
+                              const double* gP, const float* gT_extra, float* out);
+
 __global__ void pose_grad_kernel(int B, int nscales, const float* vec, const float* Ks, long k_stride_b,
                                  const double* gP, const float* gT_extra, float* gvec, int accumulate) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  float out[6];
+  pose_grad_one(b, B, nscales, vec, Ks, k_stride_b, gP, gT_extra, out);
+  for (int i = 0; i < 6; ++i) gvec[6 * b + i] = accumulate ? gvec[6 * b + i] + out[i] : out[i];
+}
+
+// tde_pose_grad_spread: job blockIdx.y; the pose gradient, then its spatial-mean backward into the pose map
+struct PoseGradMulti {
+  tde_pose_grad_t j[TDE_WARP_MULTI_MAX];
+};
+
+__global__ void pose_grad_spread_kernel(const PoseGradMulti m) {
+  const tde_pose_grad_t& j = m.j[blockIdx.y];
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= j.B) return;
+  float out[6];
+  pose_grad_one(b, j.B, j.nscales, j.pose_vec, j.K, j.k_stride_b, j.gP, j.gT_extra, out);
+  float g[6];
+  for (int i = 0; i < 6; ++i) {
+    g[i] = j.accumulate ? j.g_pose_vec[6 * b + i] + out[i] : out[i];
+    j.g_pose_vec[6 * b + i] = g[i];
+  }
+  if (j.dpose) {   // pose_avg = reduce_mean(pose_pred, [1, 2]) backward (tde_spatial_mean_bwd's expression)
+    for (int p = 0; p < j.hw; ++p) {
+      float* o = j.dpose + ((long)b * j.hw + p) * j.dpose_cstride;
+      for (int c = 0; c < 6; ++c) {
+        const float v = g[c] / (float)j.hw;
+        o[c] = j.dpose_accumulate ? o[c] + v : v;
+      }
+    }
+  }
+}
+
+__device__ void pose_grad_one(int b, int B, int nscales, const float* vec, const float* Ks, long k_stride_b,
+                              const double* gP, const float* gT_extra, float* out) {
   double G[12];  // dL/dT rows 0..2
   for (int i = 0; i < 12; ++i) G[i] = gT_extra ? gT_extra[16 * b + i] : 0.0;
   for (int s = 0; s < nscales; ++s) {
@@ -431,10 +468,8 @@ __global__ void pose_grad_kernel(int B, int nscales, const float* vec, const flo
   // dS = dL/ds, dC = dL/dc (c enters as 1-c); ds/dth = c, dc/dth = -s
   const double dth_total = dS * c - dC * s;
   const double ada = a[0] * da[0] + a[1] * da[1] + a[2] * da[2];
-  float out[6];
   for (int i = 0; i < 3; ++i) out[i] = (float)G[4 * i + 3];
   for (int i = 0; i < 3; ++i) out[3 + i] = (float)((da[i] - a[i] * ada) / th + dth_total * a[i]);
-  for (int i = 0; i < 6; ++i) gvec[6 * b + i] = accumulate ? gvec[6 * b + i] + out[i] : out[i];
 }
 
 // Config 4 cam loss (train_depth_then_cam_lr.py:278-286):
@@ -870,6 +905,22 @@ int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, lon
   TDE_CHECK_ARG(B > 0 && nscales > 0 && pose_vec && K && gP && g_pose_vec);
   hipLaunchKernelGGL(pose_grad_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B,
                      nscales, pose_vec, K, k_stride_b, gP, gT_extra, g_pose_vec, accumulate);
+  return tde_launch_status();
+}
+
+int tde_pose_grad_spread(const tde_pose_grad_t* jobs, int n, void* stream) {
+  TDE_CHECK_ARG(jobs && n > 0 && n <= TDE_WARP_MULTI_MAX);
+  PoseGradMulti m;
+  int bmax = 0;
+  for (int c = 0; c < n; ++c) {
+    const tde_pose_grad_t& j = jobs[c];
+    TDE_CHECK_ARG(j.B > 0 && j.nscales > 0 && j.pose_vec && j.K && j.gP && j.g_pose_vec);
+    TDE_CHECK_ARG(!j.dpose || (j.hw > 0 && j.dpose_cstride >= 6));
+    m.j[c] = j;
+    bmax = std::max(bmax, j.B);
+  }
+  hipLaunchKernelGGL(pose_grad_spread_kernel, dim3((bmax + 63) / 64, n), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), m);
   return tde_launch_status();
 }
 

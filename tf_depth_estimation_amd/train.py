@@ -1079,10 +1079,18 @@ class DepthThenCamTrainer(Trainer):
                 for d in ("lr", "rl"):
                     Ls.warp_loss(self.acc, S["photo"], **calls[d][s])
         # pose gradients -> pose_pred (spatial mean backward)
+        gl, gr = self.d_out["pl"][4], self.d_out["pr"][4]
+        if LOSS_MULTI:
+            # both directions' pose gradients and their spatial-mean backward into the pose maps: one launch
+            jobs = (_lib.PoseGradArgs * 2)()
+            for j, (d, g) in enumerate((("lr", gl), ("rl", gr))):
+                jobs[j] = _lib.PoseGradArgs(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
+                                            ptr(self.g_pose[d]), 0, ptr(g), hw, 6, 0)
+            _lib.check(lib.tde_pose_grad_spread(jobs, 2, st), "pose grad spread")
+            return
         for d in ("lr", "rl"):
             _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
                                          ptr(self.g_pose[d]), 0, st), "pose grad")
-        gl, gr = self.d_out["pl"][4], self.d_out["pr"][4]
         if LOSS_MULTI and _halves(gl, gr):
             _lib.check(lib.tde_spatial_mean_bwd(2 * B, hw, 6, ptr(gl), 6, 0, ptr(self.g_pose2), st), "pose mean bwd")
         else:
