@@ -315,6 +315,36 @@ def instrumented_step(tr):
     return timer.totals(), timer.nbytes
 
 
+def graph_timed_conv(tr, replays=7):
+    """The conv family as the TIMED schedule runs it: the production step captured with a GraphTimer (an event-
+    record node before and after each conv entry call's kernels, program.GraphTimer), replayed `replays` times on
+    the trainer's streams; per family the median over replays of the summed span times.  Then the graphs are
+    dropped (the timed region captures its own, without event nodes)."""
+    from tf_depth_estimation_amd.program import GraphTimer
+    progs = tr.programs()
+    timer = GraphTimer()
+    for p in progs:
+        p.timer = timer
+    try:
+        tr.capture()
+    finally:
+        for p in progs:
+            p.timer = None
+    per = []
+    for _ in range(replays):
+        tr.step()
+        torch.cuda.synchronize()
+        per.append(timer.totals())
+    tr.flush()
+    tr.release_graphs()
+    torch.cuda.synchronize()
+    out = {}
+    for fam in per[0]:
+        ms = sorted(p[fam][0] for p in per)
+        out[fam] = (ms[len(ms) // 2], per[0][fam][1], per[0][fam][2])
+    return out, timer.nbytes
+
+
 def timed_steps(tr, steps, warmup, world, rank, use_graph):
     if use_graph:
         tr.capture()
@@ -345,6 +375,22 @@ def conv_family(fam):
     return sum(c[0] for c in conv), sum(c[1] for c in conv), sum(c[2] for c in conv)
 
 
+# Environment variables that change what a step computes or how it is scheduled for DIAGNOSTICS (timing
+# experiments, serial replays): a bench line is never taken with one set.  (The work-skipping switches exist only in
+# a -DTDE_TIMING_DIAG build of libtde.so; the shipped library ignores them, and bench refuses them anyway.)
+DIAG_ENV = ("TDE_SKIP_CONV_LE", "TDE_SKIP_CONV_GT", "TDE_SKIP_WHAT", "TDE_SKIP_WGRAD", "TDE_HWG_DIAG",
+            "TDE_DBG_PHASE", "TDE_C4_OV_SERIAL")
+
+
+def env_knobs():
+    """Every TDE_* tuning variable set in the environment (reported in the line); refuse the diagnostic ones."""
+    set_ = {k: v for k, v in os.environ.items() if k.startswith("TDE_")}
+    bad = sorted(k for k in set_ if k in DIAG_ENV)
+    if bad:
+        raise SystemExit(f"bench.py: diagnostic environment variables set ({', '.join(bad)}): refusing to measure")
+    return set_
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -359,7 +405,7 @@ def main():
                          "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the secondary workloads (config 2 and 3 timed after the headline at N = 1)")
+                    help="skip the secondary workloads (configs 2, 3 and 5 timed after the headline at N = 1)")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
     ap.add_argument("--adam-overlap", default="off", choices=["off", "side", "wgrad"],
                     help="N = 1: run each gradient bucket's Adam as soon as backward finalises it, on its own side "
@@ -385,6 +431,7 @@ def main():
     ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
                     help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
     args = ap.parse_args()
+    knobs = env_knobs()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -400,8 +447,15 @@ def main():
     _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[args.math]), "conv math")
     tr, opts = build_trainer(args, args.workload, N, world, rank)
     fam, fam_bytes = instrumented_step(tr)
-    conv_ms, conv_flops, conv_launches = conv_family(fam)
     use_graph = not args.no_graph and not args.sync_bn
+    # roofline: measured on the captured production schedule the timed region replays (N = 1); the instrumented
+    # eager step (conv and BN as separate calls, one stream) stays in the line as kernel_breakdown_ms
+    gfam = None
+    if use_graph and world == 1:
+        gfam, _ = graph_timed_conv(tr)
+        conv_ms, conv_flops, conv_launches = conv_family(gfam)
+    else:
+        conv_ms, conv_flops, conv_launches = conv_family(fam)
     el = timed_steps(tr, args.steps, args.warmup, world, rank, use_graph)
     loss = tr.total_loss()
     tr.flush()       # deferred Adam: apply the last step's owed update (outside the timed region)
@@ -454,10 +508,17 @@ def main():
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "peak_note": peak_note, "traffic": None,
+                         "timing": ("HIP event-record nodes around every conv entry call's kernels inside the "
+                                    "captured production step (the graphs the timed region replays, less the nodes), "
+                                    "median of 7 replays" if gfam is not None else
+                                    "HIP events around each conv call of an instrumented eager step on one stream"),
+                         "family_ms_per_step": ({k: round(v[0], 4) for k, v in sorted(gfam.items())}
+                                                if gfam is not None else None),
                          "flops_per_step": conv_flops, "conv_ms_per_step": round(conv_ms, 4),
-                         "launches_per_step": conv_launches,
+                         "conv_calls_per_step": conv_launches,
                          "survey_flops_per_step": gflop_unit * 1e9 * N},
             "kernel_breakdown_ms": {k: round(v[0], 4) for k, v in sorted(fam.items())},
+            "env_knobs": knobs,
             "final_loss": loss,
         }
         tr_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.math}_b{N}.json")
@@ -483,7 +544,7 @@ def main():
             rf["traffic_source"] = os.path.relpath(tr_path, ROOT)
         if world == 1 and not args.no_secondary:
             sec = {}
-            for name in ("config2", "config3"):
+            for name in ("config2", "config3", "config5"):
                 if name == args.workload:
                     continue
                 log(f"[bench] secondary workload {name} ...")

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 6
+#define TDE_ABI_VERSION 7
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
@@ -101,6 +101,13 @@ uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
  *       accumulation (<= ~3 * 2^-22 relative per product), half the MFMAs of bf16x6.  DEFAULT. */
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
+/* Measurement hook (no reference counterpart: bench.py's roofline timing).  Arms the calling thread's pair of
+ * hipEvent_t (timing enabled) for the NEXT conv entry call (any tde_conv2d_* / tde_deconv2d_* compute function):
+ * ev_begin is recorded right before its first conv-family kernel, ev_end right after its last (split-K reduce
+ * included, BatchNorm launches of a fused call excluded), both with hipEventRecordExternal, so inside a stream
+ * capture they become event-record nodes that time the kernels where the graph replays them.  (NULL, NULL)
+ * disarms.  Returns the number of events the previous arming recorded. */
+int tde_conv_span_arm(void* ev_begin, void* ev_end);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
 /* Weight pre-split (the halo-tiled stride-1 path keeps the layer's weights as split fp16 / bf16 tiles):
  * bytes of the split image op (0 forward, 1 data gradient) of layer d needs under the current conv math;

@@ -12,6 +12,14 @@ ParamChunk, and asserts on every rank; a non-zero exit fails the test.
                 with the pre_launch / side_streams callbacks of Trainer.enable_ddp; each bucket fires once
                 during its own program's schedule, the launch callbacks see the reporting chunk, and both
                 chunks end with the exact mean.
+  syncbn      : the SyncBN protocol of Trainer.enable_sync_bn / NetProgram (per-layer fp64 (sum z, sum z^2) and, in
+                backward, (sum g, sum g*xhat) all-reduced with SUM; statistics and coefficients from the global
+                sums over M x world rows; dbeta from the LOCAL sum, averaged by the gradient exchange), restated
+                with the formulas of bn.hip's bn_from_sums_kernel / bn_bwd_apply_kernel: every rank's normalised
+                output, dz, dbeta and moving averages equal whole-batch BatchNorm + ReLU (oracle tf_ops.batch_norm
+                and its fp64 autograd) on the concatenated batch, the reference's one-device semantics
+                (train_depth_then_cam_lr.py:130-136).  The kernels themselves run on the GPU in
+                tests/test_gpu_ddp_world2.py (c2_syncbn).
   oracle_step : one data-parallel config-2 step: each rank takes its shard of the global batch,
                 computes the oracle gradient, writes it op by op with hooks; after the exchange and
                 the oracle Adam, parameters are bit-identical across ranks and equal to Adam applied
@@ -142,6 +150,56 @@ def case_two_programs(rank, world):
     assert torch.all(chunk_s.grad == n) and torch.all(chunk_p.grad == 10 * n)
 
 
+def case_syncbn(rank, world):
+    from oracle import tf_ops as T
+    N, Hh, Ww, C = 3, 5, 7, 12           # per-rank shard: 105 rows x 12 channels
+    eps, decay = 1e-3, 0.99
+    g = torch.Generator().manual_seed(5)
+    z_all = torch.randn(world * N, Hh, Ww, C, generator=g, dtype=torch.float64) * 2.0 + 0.3
+    beta = torch.randn(C, generator=g, dtype=torch.float64) * 0.2
+    dy_all = torch.randn(world * N, Hh, Ww, C, generator=g, dtype=torch.float64)
+    mm0, mv0 = torch.randn(C, generator=g, dtype=torch.float64) * 0.1, torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sl = slice(rank * N, (rank + 1) * N)
+    z, dy_g = z_all[sl], dy_all[sl]
+    M, Mt = N * Hh * Ww, world * N * Hh * Ww
+    # ---- forward: local sums -> all-reduce (the Trainer's bn_sync) -> global statistics
+    zf = z.reshape(-1, C)
+    sums = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    mean = sums[:C] / Mt
+    var = (sums[C:] / Mt - mean * mean).clamp_min(0)
+    invstd = 1.0 / torch.sqrt(var + eps)
+    mm = mm0 - (mm0 - mean) * (1 - decay)
+    mv = mv0 - (mv0 - var * Mt / (Mt - 1)) * (1 - decay)
+    xh = (zf - mean) * invstd
+    y = torch.relu(xh + beta).reshape(z.shape)
+    # ---- reference: whole-batch BN + ReLU on one device (loss = mean over the global batch of <y, dy>)
+    zr = z_all.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    st = T.BNState(C)
+    st.moving_mean, st.moving_variance = mm0.clone(), mv0.clone()
+    yr = torch.relu(T.batch_norm(zr, br, st, True, decay, eps))
+    (yr * dy_all).sum().div(world * N).backward()
+    assert torch.allclose(y, yr.detach()[sl], rtol=1e-12, atol=1e-12), "SyncBN forward != whole-batch BN"
+    assert torch.allclose(mm, st.moving_mean, rtol=1e-12, atol=1e-14)
+    assert torch.allclose(mv, st.moving_variance, rtol=1e-12, atol=1e-14)
+    # ---- backward: this rank's loss is the mean over ITS shard, so its output gradient is world x the global one
+    dyl = (dy_g / N).reshape(-1, C)
+    gl = torch.where(xh + beta > 0, dyl, torch.zeros_like(dyl))
+    lsum = torch.cat([gl.sum(0), (gl * xh).sum(0)])
+    gsum = lsum.clone()
+    dist.all_reduce(gsum, op=dist.ReduceOp.SUM)
+    mg, mgx = gsum[:C] / Mt, gsum[C:] / Mt
+    dz = invstd * (gl - mg - xh * mgx)
+    dbeta = lsum[:C].clone()
+    dist.all_reduce(dbeta, op=dist.ReduceOp.SUM)   # the gradient exchange: sum ...
+    dbeta /= world                                  # ... and 1/world
+    # d(global loss)/dz = d(local loss)/dz / world on this rank's rows
+    assert torch.allclose(dz / world, zr.grad[sl].reshape(-1, C), rtol=1e-10, atol=1e-14), "SyncBN dz"
+    # the exchanged dbeta (mean over ranks of the local sums) is d(global loss)/dbeta
+    assert torch.allclose(dbeta, br.grad, rtol=1e-10, atol=1e-14), "SyncBN dbeta"
+
+
 def case_oracle_step(rank, world):
     from oracle import losses as OL
     from oracle import nets as ON
@@ -192,7 +250,7 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     try:
         {"mean": case_mean, "uses2": case_uses2, "two_programs": case_two_programs,
-         "oracle_step": case_oracle_step}[case](rank, world)
+         "oracle_step": case_oracle_step, "syncbn": case_syncbn}[case](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

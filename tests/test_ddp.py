@@ -78,7 +78,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("case", ["mean", "uses2", "two_programs", "oracle_step"])
+@pytest.mark.parametrize("case", ["mean", "uses2", "two_programs", "oracle_step", "syncbn"])
 def test_gloo_world2(case):
     env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

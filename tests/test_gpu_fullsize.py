@@ -155,6 +155,60 @@ def test_config4_step_full_resolution():
     assert len(names) >= 26
 
 
+def test_config4_forward_benched_batch():
+    """The exact code bench.py times for the headline (config 4 at its per-GPU batch 8, 192x256): the trainer's
+    twin batching -- disp_net once over [left; right] (2B = 16 rows) and depth_net once over
+    [concat(L,R); concat(R,L)], every BatchNorm row-grouped (groups=2: each half normalised over its own 8 rows,
+    as the reference's separate calls, train_depth_then_cam_lr.py:130-136,146-154) -- against the fp64 oracle's
+    FOUR separate calls: every network output (single and pair disparities, masks), both poses and every loss
+    term.  Forward-only on the oracle side (the gradients of this path are held at batch 2 above)."""
+    from tf_depth_estimation_amd import train
+    B, H, W = 8, 192, 256
+    tr = train.DepthThenCamTrainer(B, H, W)
+    assert tr.twin and tr.runs["s"].groups == 2 and tr.runs["p"].groups == 2 and tr.runs["s"].N == 2 * B
+    il, ir = texture(B, H, W, 51), texture(B, H, W, 52)
+    g = np.random.default_rng(53)
+    lab = g.uniform(0.1, 2.0, (B, H, W, 1))
+    lab[g.uniform(size=lab.shape) < 0.05] = np.nan
+    lab = torch.tensor(lab, dtype=torch.float32)
+    K = intrinsics(B, H, W)
+    gt = small_pose(B, 54)
+    tr.set_batch(il.cuda(), ir.cuda(), lab.cuda(), K.cuda(), gt.cuda())
+    Pss = oracle_params_from(tr.single.chunk, "", torch.float64)
+    Ppp = oracle_params_from(tr.pair.chunk, "", torch.float64)
+    tr.phase_compute()
+    torch.cuda.synchronize()
+    parts = tr.loss_parts()
+    out = {k: [t.detach().cpu() for t in v] for k, v in tr._out.items()}
+    pose_gpu = {d: tr.pose[d].detach().cpu() for d in ("lr", "rl")}
+    with torch.no_grad():
+        x = {k: v.double() for k, v in dict(il=il, ir=ir).items()}
+        dsl = ON.disp_net(Pss, x["il"], True, scope="model_singledepth/depth_net")
+        dsr = ON.disp_net(Pss, x["ir"], True, scope="model_singledepth/depth_net")
+        dpl, pr, ml = ON.depth_net(Ppp, torch.cat([x["il"], x["ir"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        dpr, pl, mr = ON.depth_net(Ppp, torch.cat([x["ir"], x["il"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        _, rparts = OL.loss_depth_then_cam_lr(dsl, dsr, dpl, dpr, pr, pl, ml, mr, x["il"], x["ir"], lab.double(),
+                                              K.double(), gt.double())
+    for i in range(4):
+        assert rel_err(out["sl"][i], dsl[i]) <= 1e-4, f"single disp{i + 1}"
+        assert rel_err(out["sr"][i], dsr[i]) <= 1e-4, f"single (right) disp{i + 1}"
+        assert rel_err(out["pl"][i], dpl[i]) <= 1e-4, f"pair disp{i + 1}"
+        assert rel_err(out["pr"][i], dpr[i]) <= 1e-4, f"pair (right) disp{i + 1}"
+        assert rel_err(out["pl"][5 + i], ml[i]) <= 1e-4, f"mask{i + 1}"
+        assert rel_err(out["pr"][5 + i], mr[i]) <= 1e-4, f"mask (right) {i + 1}"
+    assert rel_err(pose_gpu["lr"], pr.reshape(B, 6)) <= 1e-4, "pose lr"
+    assert rel_err(pose_gpu["rl"], pl.reshape(B, 6)) <= 1e-4, "pose rl"
+
+    def val(t):
+        return t.item() if torch.is_tensor(t) else float(t)
+    for k in ("smooth", "depth", "exp", "cam"):
+        assert abs(parts[k] - val(rparts[k])) <= 1e-5 * abs(val(rparts[k])) + 1e-9, k
+    assert abs(parts["photo"] - val(rparts["pixel"])) <= 1e-5 * val(rparts["pixel"]) + 1e-9
+    assert abs(parts["consist"] - val(rparts["consist"])) <= 1e-4 * val(rparts["consist"]) + 1e-9
+
+
 def test_config3_step_full_resolution():
     """Config 3 (train_optflow_combine.py:97-240) at 192x256, batch 4 of the per-GPU 32."""
     from tf_depth_estimation_amd import train

@@ -254,7 +254,9 @@ def test_deconv_pixel_shuffle_views(L, acc):
     against the fp64 conv2d_transpose (nets_optflow_depth.py:103-140 slim.conv2d_transpose, SAME)."""
     lib = L.load()
     st = L.stream_ptr()
-    N, h, w_, cin, cout = 3, 48, 64, 32, 16          # 9216 input pixels: above the default threshold
+    # 32768 input pixels: above TDE_DECONV_PS_MINM (8192) and >= TDE_DECONV_PS_MINBLOCKS (512) 64-row tiles, so the
+    # default rule takes the pixel-shuffle path
+    N, h, w_, cin, cout = 8, 64, 64, 32, 16
     H, W = 2 * h, 2 * w_
     icv, ico, ocv, oco = 40, 4, 48, 16
     x = rnd(N, h, w_, cin, seed=51)
@@ -276,6 +278,37 @@ def test_deconv_pixel_shuffle_views(L, acc):
     close(got[..., oco:oco + cout], want[..., oco:oco + cout], what="pixel-shuffle deconv view")
     assert torch.equal(got[..., :oco], out0[..., :oco].float().double())
     assert torch.equal(got[..., oco + cout:], out0[..., oco + cout:].float().double())
+
+
+@pytest.mark.parametrize("acc", [0, 1])
+def test_conv_bwd_data_pixel_shuffle(L, acc):
+    """The data gradient of a 3x3 stride-2 SAME conv (even input size: pad_top = pad_left = 0) is the same virtual
+    DGRAD as a deconv forward, so tde_conv2d_bwd_data takes the pixel-shuffle GEMM too when the rule allows it
+    (ADVICE r03): against the fp64 autograd data gradient of conv2d_same, written into / accumulated onto a channel
+    view of a wider buffer (the split data/filter-gradient calls of enable_wgrad_overlap use this entry point)."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, H, W, cin, cout = 8, 128, 128, 16, 32          # 32768 output pixels, 512 64-row tiles: the PS rule holds
+    OH, OW = H // 2, W // 2
+    xcv, xco = 24, 4
+    x = rnd(N, H, W, cin, seed=61).requires_grad_(True)
+    wt = rnd(3, 3, cin, cout, seed=62) * 0.2
+    gy = rnd(N, OH, OW, cout, seed=63)
+    (T.conv2d_same(x, wt, 2) * gy).sum().backward()
+    ref = x.grad.detach()
+    d = conv_desc(L, N=N, H=H, W=W, C=cin, OH=OH, OW=OW, K=cout, KH=3, KW=3, stride=2, pad_top=0, pad_left=0,
+                  w_cin=cin, x_cstride=xcv, x_coff=xco, y_cstride=cout, y_coff=0)
+    ws = ws_for(L, d)
+    base = rnd(N, H, W, xcv, seed=64)
+    gdx = dev(base)
+    L.check(lib.tde_conv2d_bwd_data(ctypes.byref(d), L.ptr(dev(gy)), L.ptr(dev(wt)), L.ptr(gdx), acc, L.ptr(ws),
+                                    ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    got = gdx.double().cpu()
+    want = ref + (base[..., xco:xco + cin].float().double() if acc else 0)
+    close(got[..., xco:xco + cin], want, what="conv bwd data (pixel shuffle)")
+    assert torch.equal(got[..., :xco], base[..., :xco].float().double())
+    assert torch.equal(got[..., xco + cin:], base[..., xco + cin:].float().double())
 
 
 BN_FUSED_CASES = [

@@ -356,16 +356,19 @@ def test_wgrad_overlap_matches_serial(cfg, graph):
         assert torch.equal(ga, gb) and torch.equal(pa, pb)
 
 
+@pytest.mark.parametrize("mid_flush", [False, True], ids=["end_flush", "mid_flush"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
 @pytest.mark.parametrize("cfg", ["config2", "config4"])
-def test_deferred_adam_matches_plain(cfg, graph):
+def test_deferred_adam_matches_plain(cfg, graph, mid_flush):
     """Trainer.enable_deferred_adam: each step's Adam runs at the start of the next step on a side stream,
     overlapped with that forward (per-bucket waits, the weight splits issued once their bucket is final).
     After flush() the parameters and Adam moments equal the plain trainer's bit for bit (config 4 with all
     terms, deterministic warp-loss mode); the loss of every step matches too (the forward sees the same
-    parameters; up to the other loss kernels' fp64 atomics' summation order)."""
+    parameters; up to the other loss kernels' fp64 atomics' summation order).  mid_flush: flush() after every
+    other step, as a checkpoint save (checkpoint.Saver) or a parameter read-out does mid-training -- the captured
+    graph's owed update must then not be applied a second time."""
     from tf_depth_estimation_amd import _api, train, variables
-    steps = 3
+    steps = 3 if not mid_flush else 4
 
     def run(deferred):
         variables.get_store().reset(seed=1)
@@ -389,10 +392,12 @@ def test_deferred_adam_matches_plain(cfg, graph):
         if graph:
             tr.capture(warmup=1)
             losses.append(tr.total_loss())
-        for _ in range(steps):
+        for k in range(steps):
             tr.step()
             torch.cuda.synchronize()
             losses.append(tr.total_loss())
+            if mid_flush and k % 2 == 0:
+                tr.flush()
         tr.flush()
         torch.cuda.synchronize()
         return losses, [(c.flat.clone(), c.adam_m.clone(), c.adam_v.clone()) for c in tr.chunks]

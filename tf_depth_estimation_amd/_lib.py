@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
@@ -110,6 +110,7 @@ _SIGS = {
     "tde_status_string": (ctypes.c_char_p, [c_int]),
     "tde_set_conv_math": (c_int, [c_int]),
     "tde_get_conv_math": (c_int, []),
+    "tde_conv_span_arm": (c_int, [P, P]),
     "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_deconv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),
@@ -213,27 +214,59 @@ _hip = None
 _own_streams = []
 
 
-def dedicated_stream(priority=None):
+def dedicated_stream():
     """A HIP stream of its own (non-blocking) wrapped as a torch ExternalStream, kept for the life of the process.
     torch.cuda.Stream() hands out streams from a fixed round-robin pool, so after enough of them a "new" stream can
     be the very HIP stream a graph is being captured on or another side stream: a cross-stream wait between the two
-    is then a self-wait.  priority: None (default), "high" or "low" (hipStreamCreateWithPriority over the device's
-    range; the hardware queue's priority orders the dispatch of workgroups from concurrently runnable kernels)."""
-    global _hip
-    if _hip is None:
-        _hip = ctypes.CDLL("libamdhip64.so")
+    is then a self-wait.  (Stream priorities were measured in round 3 -- mixing priority classes cost up to 40 % --
+    and are not offered.)"""
     s = ctypes.c_void_p()
-    if priority in ("high", "low"):
-        least, greatest = ctypes.c_int(), ctypes.c_int()
-        _hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
-        pv = greatest.value if priority == "high" else least.value
-        rc = _hip.hipStreamCreateWithPriority(ctypes.byref(s), ctypes.c_uint(1), ctypes.c_int(pv))
-    else:
-        rc = _hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
+    rc = hip().hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1))   # hipStreamNonBlocking
     if rc != 0 or not s.value:
         raise TdeError(f"hip stream creation failed ({rc})")
     _own_streams.append(s)
     return torch.cuda.ExternalStream(s.value)
+
+
+def hip():
+    """The HIP runtime (ctypes) for the few calls torch does not expose: dedicated streams and timing events that
+    a stream capture records as graph nodes."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+    return _hip
+
+
+class GraphEvent:
+    """A timing hipEvent_t recorded with hipEventRecordExternal: inside a stream capture the record becomes an
+    event-record node of the graph, so elapsed times between two such events measure the replayed graph (torch's
+    Event.record() inside a capture only orders streams and times nothing)."""
+
+    def __init__(self):
+        self.ev = ctypes.c_void_p()
+        rc = hip().hipEventCreate(ctypes.byref(self.ev))
+        if rc != 0:
+            raise TdeError(f"hipEventCreate failed ({rc})")
+
+    def record(self, stream=None):
+        st = (stream or torch.cuda.current_stream()).cuda_stream
+        rc = hip().hipEventRecordWithFlags(self.ev, ctypes.c_void_p(st), ctypes.c_uint(1))   # hipEventRecordExternal
+        if rc != 0:
+            raise TdeError(f"hipEventRecordWithFlags failed ({rc})")
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        rc = hip().hipEventElapsedTime(ctypes.byref(ms), self.ev, end.ev)
+        if rc != 0:
+            raise TdeError(f"hipEventElapsedTime failed ({rc})")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.ev and _hip is not None:
+                _hip.hipEventDestroy(self.ev)
+        except Exception:
+            pass
 
 
 # ---- cross-stream ordering inside stream capture
@@ -269,8 +302,13 @@ class capture_scope:
 
     def __exit__(self, *exc):
         _CAPTURE_DEPTH[0] -= 1
-        if _CAPTURE_DEPTH[0] == 0 and _GC_WAS_ON[0]:
-            gc.enable()
+        if _CAPTURE_DEPTH[0] == 0:
+            # every capture of the region has ended (its graph instantiated: a wait on an event recorded in the
+            # same capture became a graph edge), so the kept events can go (they used to accumulate
+            # for the life of the process, hundreds per capture)
+            _CAPTURE_EVENTS.clear()
+            if _GC_WAS_ON[0]:
+                gc.enable()
         return False
 
 
@@ -293,14 +331,14 @@ def wait_event(stream, ev):
     _keep(ev)
 
 
-def owned_stream(owner, name, priority=None):
+def owned_stream(owner, name):
     """A dedicated stream (dedicated_stream) cached on `owner` under `name`: created once per owner and role, so
     re-enabling an overlap or re-capturing a step never allocates another HIP stream, and no two roles ever share
-    one (the pool aliasing dedicated_stream avoids).  The priority applies when the stream is first created."""
+    one (the pool aliasing dedicated_stream avoids)."""
     cache = owner.__dict__.setdefault("_tde_streams", {})
     st = cache.get(name)
     if st is None:
-        st = cache[name] = dedicated_stream(priority)
+        st = cache[name] = dedicated_stream()
     return st
 
 

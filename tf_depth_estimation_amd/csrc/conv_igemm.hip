@@ -43,20 +43,12 @@ constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 // (zero past the 3x3 kernel: 9 of the 16 taps x class pairs), and whose epilogue scatters column (py, px, c) to
 // output pixel (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes.
 constexpr int MODE_PS = 3;
-// WGRAD pixel decode fast path for OW % 4 == 0 (conv_tile R4), off: ~60 VALU less per k-tile, but measured
-// neutral (big3x3 WGRAD 640 vs 649 us, config 4 8.19 vs 8.22 ms; scripts/sessions/r03n.sh) -- the loop waits
-// on its loads, not on address arithmetic -- so it is not worth the second set of WGRAD instantiations
-// TDE_DBG_PHASE (timing diagnostics only, wrong results), a bit mask: 1 no k-loop global loads, 2 no MFMAs,
-// 4 no staging (split + LDS stores)
+// TDE_DBG_PHASE (timing-diagnostic BUILDS only, -DTDE_DBG_PHASE=..., wrong results; never a runtime switch), a
+// bit mask: 1 no k-loop global loads, 2 no MFMAs, 4 no staging (split + LDS stores).  (Round 3's row-of-4 WGRAD
+// decode, XCD-grouped WGRAD order, write-through epilogue stores and software-pipelined two-tile k-loop were
+// measured neutral and removed in round 4: DESIGN.md section 6.)
 #ifndef TDE_DBG_PHASE
 #define TDE_DBG_PHASE 0
-#endif
-// TDE_PIPE: the PF 2 k-loop of the staged fp16x3 image interleaves the next tile's staging with the MFMAs
-#ifndef TDE_PIPE
-#define TDE_PIPE 1
-#endif
-#ifndef TDE_WGRAD_ROW4
-#define TDE_WGRAD_ROW4 0
 #endif
 constexpr int NT = 256;
 
@@ -76,8 +68,6 @@ struct ConvArgs {
   // fp16x3 (math 4) operand bounds |x| <= *bound of the x view, the y view and the weights (null: unscaled
   // x / y, fixed weight scale; split_math.h)
   const float* xmax; const float* ymax; const float* wmax;
-  int xcd;   // igemmx_kernel: XCD-grouped tile order (TDE_XCD_WGRAD)
-  int wt;    // epilogue stores written through L2 (sc1; TDE_WT): bit 0 split-K slabs, bit 1 direct outputs
   // MODE_PS: deconv output channels / height / width, weight input channels (w[3][3][ps_C][ps_K])
   int ps_C, ps_H, ps_W, ps_K;
   FDiv fpsC;
@@ -286,9 +276,7 @@ struct SmemSize {
 };
 
 // One output tile (bx, by) of split / class bz.  The kernels below map blocks onto tiles.
-// R4 (WGRAD, OW % 4 == 0): the row-of-4 pixel decode.  A template argument chosen once per block (a branch
-// inside the k-loop made hipcc drain every load at its merge point: 637 -> 752 us on big3x3 WGRAD).
-template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF, bool R4 = false>
+template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
 __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const int by, const int bz,
                                           typename ImgSel<MATH, BM>::T* smem) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
@@ -430,28 +418,13 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         int n = fdiv(pix0, p.fOHW);
         const int r = pix0 - n * p.OH * p.OW;
         int oh = fdiv(r, p.fOW), ow = r - oh * p.OW;
-        if constexpr (R4) {
-          // OW % 4 == 0 (every level down to 6x8; pix0 % 4 == 0): the 4 pixels share (n, oh) and step along
-          // one input row by S, so one row test, one address and per-pixel column tests (the general path
-          // below re-derives both per pixel: ~23 VALU per load)
-          const int ih = oh * p.S + a_i1[i], iw0 = ow * p.S + a_i2[i];
-          const bool rok = pix0 < Kd && (unsigned)ih < (unsigned)p.H;
-          const int b0 = a_pb[i] + ((n * p.H + oh * p.S) * p.W + ow * p.S) * p.xcs;
-          const int step = p.S * p.xcs;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const bool ok = rok && (unsigned)(iw0 + j * p.S) < (unsigned)p.W;
-            ra[i][j] = bload(rx, ok ? 4 * (b0 + j * step) : OOB);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int ih = oh * p.S, iw = ow * p.S;
-            const bool ok = pix0 + j < Kd && (unsigned)(ih + a_i1[i]) < (unsigned)p.H &&
-                            (unsigned)(iw + a_i2[i]) < (unsigned)p.W;
-            ra[i][j] = bload(rx, ok ? 4 * (a_pb[i] + ((n * p.H + ih) * p.W + iw) * p.xcs) : OOB);
-            if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int ih = oh * p.S, iw = ow * p.S;
+          const bool ok = pix0 + j < Kd && (unsigned)(ih + a_i1[i]) < (unsigned)p.H &&
+                          (unsigned)(iw + a_i2[i]) < (unsigned)p.W;
+          ra[i][j] = bload(rx, ok ? 4 * (a_pb[i] + ((n * p.H + ih) * p.W + iw) * p.xcs) : OOB);
+          if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++n; } }
         }
       }
     }
@@ -530,45 +503,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
           putB(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
       } else {
         putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
-      }
-    }
-  };
-
-  // store_tiles cut into PARTS slices (a slice = every put whose index u has u * PARTS / NPUT == part), so the
-  // staging of the next tile can be interleaved with the MFMAs of the current one (TDE_PIPE loop below)
-  constexpr int NPUT = A_PER * (A_T ? 4 : 1) + B_PER * (B_T ? 4 : 1);
-  auto store_part = [&](int buf, auto& ra, auto& rb, auto part_c, auto parts_c) {
-    constexpr int PART = decltype(part_c)::value, PARTS = decltype(parts_c)::value;
-    ET* A = As0 + buf * IA::SIZE;
-    ET* Bm = Bs0 + buf * IB::SIZE;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int s = tid + i * NT;
-#pragma unroll
-      for (int rr = 0; rr < (A_T ? 4 : 1); ++rr) {
-        const int u = i * (A_T ? 4 : 1) + rr;
-        if (u * PARTS / NPUT != PART || s >= A_SLOTS) continue;
-        if constexpr (A_T) {
-          const int r0 = 4 * (s % (BM / 4)), k0 = 4 * (s / (BM / 4));
-          putA(A, r0 + rr, k0, f4{ra[i][0][rr], ra[i][1][rr], ra[i][2][rr], ra[i][3][rr]});
-        } else {
-          putA(A, s >> 3, 4 * (s & 7), ra[i][0]);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int s = tid + i * NT;
-#pragma unroll
-      for (int rr = 0; rr < (B_T ? 4 : 1); ++rr) {
-        const int u = A_PER * (A_T ? 4 : 1) + i * (B_T ? 4 : 1) + rr;
-        if (u * PARTS / NPUT != PART || s >= B_SLOTS) continue;
-        if constexpr (B_T) {
-          const int r0 = 4 * (s % (BN / 4)), k0 = 4 * (s / (BN / 4));
-          putB(Bm, r0 + rr, k0, f4{rb[i][0][rr], rb[i][1][rr], rb[i][2][rr], rb[i][3][rr]});
-        } else {
-          putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
-        }
       }
     }
   };
@@ -740,69 +674,12 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     }
   };
 
-  // TDE_PIPE (PF 2, staged fp16x3): one k-tile = fragment reads of tile k, global loads of tile k+2, then the MFMAs
-  // of tile k with the split + LDS stores of tile k+1 (loaded one iteration earlier) between their rows -- the
-  // staging's VALU and LDS stores issue while the matrix pipe runs, instead of after it (sched_barrier keeps
-  // hipcc from clustering them again)
-  auto compute_pipe = [&](int cur, auto&& issue, int buf, auto& ra, auto& rb) {
-   if constexpr (MATH == 4 && TDE_F16_STAGE) {
-    const ET* A = As0 + cur * IA::SIZE;
-    const ET* Bm = Bs0 + cur * IB::SIZE;
-    h8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      ah[a] = IA::hi(A, wrow0 + a * 16 + r16, q);
-      al[a] = IA::lo(A, wrow0 + a * 16 + r16, q);
-    }
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      bh[b] = IB::hi(Bm, wcol0 + b * 16 + r16, q);
-      bl[b] = IB::lo(Bm, wcol0 + b * 16 + r16, q);
-    }
-    issue();
-    auto row = [&](auto a_c) {
-      constexpr int a = decltype(a_c)::value;
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-      }
-      store_part(buf, ra, rb, a_c, std::integral_constant<int, TM>{});
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    static_assert(TM <= 8, "rows");
-    row(std::integral_constant<int, 0>{});
-    if constexpr (TM > 1) row(std::integral_constant<int, 1>{});
-    if constexpr (TM > 2) row(std::integral_constant<int, 2>{});
-    if constexpr (TM > 3) row(std::integral_constant<int, 3>{});
-    if constexpr (TM > 4) row(std::integral_constant<int, 4>{});
-    if constexpr (TM > 5) row(std::integral_constant<int, 5>{});
-    if constexpr (TM > 6) row(std::integral_constant<int, 6>{});
-    if constexpr (TM > 7) row(std::integral_constant<int, 7>{});
-   }
-  };
-
   if (kt0 < kt1) {
     load_tiles(kt0, ra0, rb0);
     store_tiles(0, ra0, rb0);
     __syncthreads();
     int cur = 0;
-    if constexpr (PF == 2 && MATH == 4 && TDE_F16_STAGE && TDE_PIPE && !(TDE_DBG_PHASE & 6)) {
-      const int klast = kt1 - 1;
-      load_tiles(min(kt0 + 1, klast), ra1, rb1);
-      int kt = kt0;
-      while (true) {
-        compute_pipe(cur, [&] { load_tiles(min(kt + 2, klast), ra0, rb0); }, cur ^ 1, ra1, rb1);
-        __syncthreads();
-        cur ^= 1;
-        if (++kt >= kt1) break;
-        compute_pipe(cur, [&] { load_tiles(min(kt + 2, klast), ra1, rb1); }, cur ^ 1, ra0, rb0);
-        __syncthreads();
-        cur ^= 1;
-        if (++kt >= kt1) break;
-      }
-    } else if constexpr (PF == 1) {
+    if constexpr (PF == 1) {
       // one tile in flight: the load of tile kt+1 overlaps the MFMAs of tile kt
       for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = (kt + 1 < kt1);
@@ -963,22 +840,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       }
     }
   }
-  if (p.wt & (direct ? 2 : 1)) {
-    // write-through (sc1) stores: the tile's bytes leave no dirty L2 lines for the kernel-end release to write
-    // back (the boundary cost grows with them, MI355X_MICROARCH.md 'boundary' / 'publish-large')
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int n = n0 + wcol0 + b * 16 + r16;
-          if (rowaddr[a][r] >= 0 && n < Nn)
-            asm volatile("global_store_dword %0, %1, off sc1" : : "v"(base + rowaddr[a][r] + coff[b]),
-                         "v"(acc[a][b][r]) : "memory");
-        }
-    return;
-  }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -991,11 +852,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 }
 
 // Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
-// share a pixel slab -- was measured 5-20% SLOWER on config 2's layers: the round-robin order
-// already lets neighbouring tiles, dispatched together, share the slab through the Infinity Cache.)
-// p.xcd (WGRAD, TDE_XCD_WGRAD=1): the grid is re-ordered so that each XCD (hardware block b runs on XCD b % 8)
-// gets one contiguous run of the (x fastest, z slowest) tile order -- the tiles of one split-K pixel slice then
-// share their x / dy rows in ONE L2 instead of pulling them into all eight.
+// share a pixel slab -- was measured 5-20% SLOWER on config 2's layers, and an XCD-grouped WGRAD order neutral:
+// the round-robin order already lets neighbouring tiles, dispatched together, share the slab through the
+// Infinity Cache.)
 // TDE_PF2_WAVES: waves per SIMD the two-tiles-in-flight (PF 2) variants must fit (register cap 512 / W)
 #ifndef TDE_PF2_WAVES
 #define TDE_PF2_WAVES 2
@@ -1004,20 +863,7 @@ template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF == 2 ? TDE_PF2_WAVES : 1)))
 igemmx_kernel(const ConvArgs p) {
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (p.xcd) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    int l = tde_xcd_block(bx + gx * (by + gy * bz), gx * gy * gridDim.z);
-    bx = l % gx; l /= gx;
-    by = l % gy; bz = l / gy;
-  }
-  if constexpr (MODE == MODE_WGRAD && TDE_WGRAD_ROW4) {
-    if ((p.OW & 3) == 0) {
-      conv_tile<MATH, MODE, BM, BN, WM, WN, PF, true>(p, bx, by, bz, smem);
-      return;
-    }
-  }
-  conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, bx, by, bz, smem);
+  conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // The two backward GEMMs of one layer in ONE launch (horizontal fusion): blocks [0, nd) compute the
@@ -1037,12 +883,6 @@ __global__ void __launch_bounds__(NT) igemm_bwd2_kernel(const ConvArgs pd, const
     id -= nd;
     const int bx = id % gxw;
     id /= gxw;
-    if constexpr (TDE_WGRAD_ROW4) {
-      if ((pw.OW & 3) == 0) {
-        conv_tile<MATH, MODE_WGRAD, BM, BN, WM, WN, 1, true>(pw, bx, id % gyw, id / gyw, smem);
-        return;
-      }
-    }
     conv_tile<MATH, MODE_WGRAD, BM, BN, WM, WN, 1>(pw, bx, id % gyw, id / gyw, smem);
   }
 }
@@ -1508,13 +1348,8 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
 // prefetch depth (tiles in flight): 1 for 128-row tiles; for the 64-row tiles of the deep layers 2 in the
 // register-split maths, 1 in fp16x3 (depth 2 costs 187 VGPR+AGPR = 2 waves/SIMD, depth 1 136 = 3; measured
 // (scripts/r02zm.sh) icnv5 DGRAD 43.6 -> 36.6 us, config 2 2.82 -> 2.80 ms, config 4 13.30 -> 13.18 ms).
-// TDE_CONV_PF: 1 / 2 forces one depth for all (tuning experiments).
-static const long g_conv_pf = env_long("TDE_CONV_PF", 0);
-// TDE_PF128: prefetch depth of the 128-row tiles (2: two k-tiles in flight, capped at 256 VGPRs = 2 waves per
-// SIMD by TDE_PF2_WAVES -- the occupancy the 128-row tiles have anyway, 64 KiB of LDS per workgroup)
-static const long g_pf128 = env_long("TDE_PF128", 1);
-// TDE_PF64: the same for the 64-row tiles in fp16x3 (2: 153 VGPRs, still 3 waves per SIMD, with the pipelined loop)
-static const long g_pf64 = env_long("TDE_PF64", 1);
+// (Two tiles in flight for the fp16x3 tiles, with or without the staging interleaved with the MFMAs, measured
+// neutral in round 3 -- 604 vs 602 us on big3x3 WGRAD, config 4 within 0.5 % -- and removed.)
 // wave layout of a tile: 2 x 2 waves when BN is a multiple of TDE_WN_DIV, else 4 x 1 (all rows split)
 #ifndef TDE_WN_DIV
 #define TDE_WN_DIV 32
@@ -1534,19 +1369,15 @@ static int tile_math(int bn, int mode = -1) {
   return (g_conv_math == 3 && bn < lim) ? (int)g_narrow_math : g_conv_math;
 }
 
-static const long g_xcd_wgrad = env_long("TDE_XCD_WGRAD", 0);
-
 template <int MODE, int BM, int BN>
 static void launch_cfg(const ConvArgs& a0, dim3 grid, hipStream_t st) {
   ConvArgs a = a0;
-  a.xcd = (MODE == MODE_WGRAD && g_xcd_wgrad) ? 1 : 0;
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int math = tile_math(BN, MODE);
-  const int pf = g_conv_pf ? (int)g_conv_pf : (BM == 64 ? (math != 4 ? 2 : (int)g_pf64) : (int)g_pf128);
+  const int pf = (BM == 64 && math != 4) ? 2 : 1;
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
-  else if (math == 4 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
   else if (math == 4) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 3 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
   else if (math == 3) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
@@ -1617,11 +1448,8 @@ static bool desc_ok(const tde_conv_desc_t* d) {
   return true;
 }
 
-static const long g_wt = env_long("TDE_WT", 0);
-
 static ConvArgs make_args(const tde_conv_desc_t& d) {
   ConvArgs a{};
-  a.wt = (int)g_wt;
   a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.OH = d.OH; a.OW = d.OW; a.K = d.K;
   a.KH = d.KH; a.KW = d.KW; a.S = d.stride; a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
   a.xcs = d.x_cstride; a.xco = d.x_coff; a.ycs = d.y_cstride; a.yco = d.y_coff;
@@ -1631,11 +1459,31 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
   return a;
 }
 
-// Timing experiments only (results are garbage): skip every conv launch of layers whose forward
-// output has <= / > this many pixels, to measure what those layers cost inside the captured step.
+// Conv-kernel spans for bench.py's graph-timed roofline (tde_conv_span_arm): when the calling thread has armed a
+// pair of timing events, the next conv entry call records the first right before its first conv-family kernel
+// (GEMM, halo, halo-WGRAD or pixel-shuffle kernel) and the second right after its last one (split-K reduce
+// included; the BatchNorm launches of a fused conv + BN call come after it), with hipEventRecordExternal so that
+// under stream capture they become event-record nodes of the graph and time the kernels where the captured step
+// replays them.  Unarmed (always, outside bench's timing capture): no event, no cost.
+static thread_local hipEvent_t g_span_ev[2] = {nullptr, nullptr};
+static thread_local int g_span_marks = 0;
+static void span_mark(int which, hipStream_t st) {
+  if (g_span_ev[which] != nullptr && hipEventRecordWithFlags(g_span_ev[which], st, hipEventRecordExternal) == hipSuccess)
+    ++g_span_marks;
+}
+
+// Timing experiments only (results are garbage), compiled in ONLY by a diagnostic build (-DTDE_TIMING_DIAG; never
+// in the shipped libtde.so, so no environment variable can make the product skip work -- VERDICT r03): skip every
+// conv launch of layers whose forward output has <= / > this many pixels (TDE_SKIP_CONV_LE / _GT; TDE_SKIP_WHAT
+// bit 0: GEMM kernels, bit 1: reduces), or every filter gradient (TDE_SKIP_WGRAD), to measure what they cost.
+#ifdef TDE_TIMING_DIAG
 static const long g_skip_le = env_long("TDE_SKIP_CONV_LE", -1);
 static const long g_skip_gt = env_long("TDE_SKIP_CONV_GT", -1);
-static const long g_skip_what = env_long("TDE_SKIP_WHAT", 3);   // bit 0: GEMM kernels, bit 1: reduces
+static const long g_skip_what = env_long("TDE_SKIP_WHAT", 3);
+static const long g_skip_wgrad = env_long("TDE_SKIP_WGRAD", 0);
+#else
+static constexpr long g_skip_le = -1, g_skip_gt = -1, g_skip_what = 3, g_skip_wgrad = 0;
+#endif
 static bool skip_conv(const tde_conv_desc_t* d) {
   const long m = (long)d->N * d->OH * d->OW;
   return (g_skip_le >= 0 && m <= g_skip_le) || (g_skip_gt >= 0 && m > g_skip_gt);
@@ -1681,7 +1529,6 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
                   size_t ws_bytes, void* stream) {
   // the virtual DGRAD's operands: input = a0.dy (view y of d, K channels), output = a0.dx (view x of d, C channels)
   ConvArgs a{};
-  a.wt = a0.wt;
   a.N = d->N; a.H = d->OH; a.W = d->OW; a.C = d->K; a.OH = d->OH; a.OW = d->OW; a.K = 4 * d->C;
   a.KH = 2; a.KW = 2; a.S = 1; a.PT = 1; a.PL = 1; a.wcin = d->K;
   a.xcs = d->y_cstride; a.xco = d->y_coff; a.ycs = d->x_cstride; a.yco = d->x_coff;
@@ -1700,10 +1547,12 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   int BM = 0, BN = 0;
   ps_ok(*d, &BM, &BN);
   const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
+  span_mark(0, st);
   if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else if (BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  span_mark(1, st);
   if (bn) {
     // statistics from a grouped partial pass over z (the parity classes of a row tile are not one row range)
     const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
@@ -1726,7 +1575,9 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   if (MODE == MODE_WGRAD && hwg_plan(*d, wp, g_conv_math)) {
     // stride-1, narrow, high-resolution layer: halo-tiled filter gradient (halo_wgrad.hip)
     if (wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    span_mark(0, static_cast<hipStream_t>(stream));
     if (!skip) hwg_launch(wp, *d, a.x, a.dy, a.dw, accumulate, tde_ws_body(ws), static_cast<hipStream_t>(stream));
+    span_mark(1, static_cast<hipStream_t>(stream));
     return tde_launch_status();
   }
   HaloPlan hp;
@@ -1745,7 +1596,9 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     hipStream_t st = static_cast<hipStream_t>(stream);
     const float* in = MODE == MODE_FWD ? a.x : a.dy;
     float* z = MODE == MODE_FWD ? a.y : a.dx;
+    span_mark(0, st);
     if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, grouped_sa ? nullptr : part, st, a.bias, a.relu);
+    span_mark(1, st);
     if (bn) {
       const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
                     bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
@@ -1769,9 +1622,14 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   a.bnp = (bn && bp.path == BN_EPI) ? part : nullptr;
   a.bn_gx = pl.gx;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  span_mark(0, st);
   if (!skip) launch_mode<MODE>(pl, a, st);
   float* z = MODE == MODE_FWD ? a.y : (MODE == MODE_DGRAD ? a.dx : a.dw);
   if (!skipr && !(bn && bp.path == BN_REDUCE)) launch_reduce<MODE>(pl, a, st);
+  if (bn && bp.path == BN_REDUCE && !skipr)
+    hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws, pl.splits,
+                       pl.rows, pl.cols, z, bp.ch.rows_per_chunk, part);
+  span_mark(1, st);
   if (bn) {
     // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
     const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
@@ -1781,9 +1639,6 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     } else if (bp.path == BN_STANDALONE) {
       bn_fwd_standalone_launch(pl.rows, pl.cols, z, o, part, st);
     } else {
-      if (bp.path == BN_REDUCE && !skipr)
-        hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws,
-                           pl.splits, pl.rows, pl.cols, z, bp.ch.rows_per_chunk, part);
       bn_fwd_from_partials_launch(pl.rows, pl.cols, z, bp.nparts, part, o, st);
     }
   }
@@ -1823,9 +1678,6 @@ static void launch_bwd2(const Plan& p1, const ConvArgs& a1, const Plan& p2, cons
 }
 
 static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches (A/B experiments)
-// Timing experiment only (filter gradients are NOT computed): what the backward chain costs without the
-// filter-gradient work, i.e. the bound on taking it off the critical path
-static const long g_skip_wgrad = env_long("TDE_SKIP_WGRAD", 0);
 
 
 // Data + filter gradient of one layer.  MODE1 = the data-gradient GEMM of the virtual conv (DGRAD for a
@@ -2111,7 +1963,10 @@ int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, co
   ConvArgs a1 = make_args(db), a2 = make_args(db);
   a1.dy = dy; a1.w = w; a1.dx = dx;
   a2.x = x; a2.dy = dy; a2.dw = dw;
-  return run_bwd<MODE_DGRAD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  span_mark(0, static_cast<hipStream_t>(stream));
+  const int r = run_bwd<MODE_DGRAD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  span_mark(1, static_cast<hipStream_t>(stream));
+  return r;
 }
 
 int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, const float* w,
@@ -2125,7 +1980,10 @@ int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float*
   ConvArgs a1 = make_args(db), a2 = make_args(db);
   a1.x = dy_big; a1.w = w; a1.y = dx_small;          // data gradient = Conv2D(dy_big) (virtual FWD)
   a2.x = dy_big; a2.dy = x_small; a2.dw = dw;        // filter gradient (virtual WGRAD)
-  return run_bwd<MODE_FWD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  span_mark(0, static_cast<hipStream_t>(stream));
+  const int r = run_bwd<MODE_FWD>(&db, a1, accumulate_dx, a2, accumulate_dw, ws, ws_bytes, stream);
+  span_mark(1, static_cast<hipStream_t>(stream));
+  return r;
 }
 
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,
@@ -2146,6 +2004,16 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
   ConvArgs a = make_args(db);
   a.x = dy_big; a.dy = x_small; a.dw = dw;
   return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
+}
+
+// bench.py's graph-timed roofline: arm the calling thread's conv-kernel span events (hipEvent_t, timing enabled;
+// null, null disarms).  Returns how many span marks the previous arming recorded (2 after one conv entry call).
+int tde_conv_span_arm(void* ev_begin, void* ev_end) {
+  const int n = g_span_marks;
+  g_span_ev[0] = static_cast<hipEvent_t>(ev_begin);
+  g_span_ev[1] = static_cast<hipEvent_t>(ev_end);
+  g_span_marks = 0;
+  return n;
 }
 
 }  // extern "C"

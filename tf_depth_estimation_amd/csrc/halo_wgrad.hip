@@ -388,7 +388,12 @@ long env_hwg(const char* name, long dflt) {
 const long g_hwg = env_hwg("TDE_HWG", 1);                 // 0: never (A/B)
 const long g_hwg_blocks = tde_env_pos("TDE_HWG_BLOCKS", 768);  // grid size to aim for
 const long g_hwg_min_m = tde_env_pos("TDE_HWG_MIN_M", 16384);
+// TDE_HWG_DIAG (timing experiments, results garbage): read only by a diagnostic build (-DTDE_TIMING_DIAG)
+#ifdef TDE_TIMING_DIAG
 const long g_hwg_diag = env_hwg("TDE_HWG_DIAG", 0);
+#else
+constexpr long g_hwg_diag = 0;
+#endif
 const long g_hwg_min_items = env_hwg("TDE_HWG_MIN_ITEMS", 25);
 const long g_hwh = env_hwg("TDE_HWH", 1);                 // 0: fp32 halo WGRAD also in math 4 (A/B)
 const long g_hwh_min_items = env_hwg("TDE_HWH_MIN_ITEMS", 1);

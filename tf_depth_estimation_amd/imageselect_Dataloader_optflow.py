@@ -96,7 +96,9 @@ class DataLoader(object):
         self._started = False
         self._held = None
         self._retired = []              # (segment, slot) replaced when a slot's shared staging grew
-        self._drop_names = []           # names of unlinked segments the workers should let go of
+        # names of unlinked segments the workers should let go of, with the number of batches they are still sent
+        # with (a list that only grew was pickled into every later task)
+        self._drop_names = []
         self._task_timeout = float(task_timeout)   # seconds one worker task may take before the loader raises
         self.last_indices = None
         self._lib = _lib.load()
@@ -289,7 +291,11 @@ class DataLoader(object):
                 if self._ppool is not None:
                     # whole samples in the worker processes (image + label into shared memory, cam / proj parsed)
                     f, HW = self._files, self.image_height * self.image_width
-                    drop = tuple(self._drop_names)
+                    # each name rides along with the tasks of a bounded number of batches (2 per worker process:
+                    # every worker has normally run a task by then; one that has not keeps a mapping of an
+                    # unlinked segment until the pool closes -- memory, never data)
+                    drop = tuple(n for n, _ in self._drop_names)
+                    self._drop_names = [(n, k - 1) for n, k in self._drop_names if k > 1]
                     futs = [self._ppool.apply_async(
                         _decode_worker.load_sample,
                         (slot.shm.name, b * slot.stride, slot.stride, f["image_file_list"][i],
@@ -355,7 +361,7 @@ class DataLoader(object):
             keep = []
             for sh, owner in self._retired:
                 if owner is slot:
-                    self._drop_names.append(sh.name)
+                    self._drop_names.append((sh.name, max(4, 2 * self._procs)))
                     sh.close()
                     try:
                         sh.unlink()

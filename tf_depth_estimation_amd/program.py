@@ -417,6 +417,12 @@ class NetProgram:
     def _span(self, family, flops=0.0, nbytes=0.0):
         return NO_SPAN if self.timer is None else self.timer.span(family, flops, nbytes)
 
+    def _production(self):
+        """The shipped schedule runs (fused conv + BN calls, filter gradients on their side stream): no timer, or a
+        GraphTimer (which times that schedule where a captured graph replays it); a KernelTimer's instrumented eager
+        step instead splits conv and BN calls and keeps one stream."""
+        return self.timer is None or getattr(self.timer, "graph", False)
+
     # ---------------------------------------------------------------- helpers
     def P(self, name):
         return self.chunk.view(f"{self.prefix}/{name}")
@@ -467,8 +473,7 @@ class NetProgram:
         serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
         # dedicated HIP streams, one per role and program (torch.cuda.Stream() recycles a fixed pool: a pooled
         # side stream can alias a capture stream or another program's side stream, _lib.dedicated_stream)
-        prio = os.environ.get("TDE_WGRAD_PRIO") or None     # filter-gradient stream priority ("low" / "high")
-        self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0", prio)) if on else None
+        self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0")) if on else None
         # TDE_WGRAD_STREAMS > 1: the filter-gradient groups alternate over that many side streams (each with its
         # own workspace), so independent filter gradients may run concurrently with each other
         n = 1 if (serial or not on) else _env_pos("TDE_WGRAD_STREAMS", 1)
@@ -626,14 +631,15 @@ class NetProgram:
                                                         op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
                                                         ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st),
                                op.layer + " syncbn")
-                elif is_training and self.timer is None:
+                elif is_training and self._production():
                     # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
-                    # consumes the conv's split-K partials directly
+                    # consumes the conv's split-K partials directly (a GraphTimer times its conv kernels only)
                     bn = _lib.BnTrain(ptr(beta), 1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
                                       ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, run.groups)
                     fn = lib.tde_deconv2d_fwd_bn if op.deconv else lib.tde_conv2d_fwd_bn
-                    _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb, st),
-                               op.layer)
+                    with self._span("conv_fwd", conv_flops(op, N), conv_bytes(op, N)):
+                        _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb,
+                                      st), op.layer)
                 elif is_training:
                     # instrumented step (bench.py roofline): the same layer as separate conv and BN calls, so
                     # the conv kernel's time is measured on its own
@@ -714,7 +720,7 @@ class NetProgram:
         wsb = ws.numel() * 4
         iv = spec.input_view
         _lib.check(lib.tde_zero_bytes(run.absmax.numel() * 4, ptr(run.absmax), st), "zero dz bounds")
-        side = self.wgrad_stream if (self.timer is None and self.bn_sync is None) else None
+        side = self.wgrad_stream if (self._production() and self.bn_sync is None) else None
         if side is SERIAL:
             side = torch.cuda.current_stream()
         if side is not None:
@@ -783,9 +789,10 @@ class NetProgram:
                     wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
                     a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
 
-                    def wgrad_call(wsp, wsb2, wg=wg, d=d, a1=a1, a2=a2, gw=gw, layer=op.layer):
-                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, wsp, wsb2, _lib.stream_ptr()),
-                                   layer + " wgrad")
+                    def wgrad_call(wsp, wsb2, wg=wg, d=d, a1=a1, a2=a2, gw=gw, layer=op.layer, fl=fl, op=op):
+                        with self._span("conv_wgrad", fl, conv_bytes(op, N)):
+                            _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, wsp, wsb2, _lib.stream_ptr()),
+                                       layer + " wgrad")
                     self._wg_pending.append((wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
                     ev = None
                     if len(self._wg_pending) >= self.wgrad_group:
@@ -793,12 +800,14 @@ class NetProgram:
                         ev.record()
                     if src_needs:
                         acc = mark(op.src)
-                        if op.deconv:
-                            _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
-                                                                 acc, ptr(ws), wsb, st), op.layer + " bwd data")
-                        else:
-                            _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
-                                                               acc, ptr(ws), wsb, st), op.layer + " bwd data")
+                        with self._span("conv_dgrad", fl, conv_bytes(op, N)):
+                            if op.deconv:
+                                _lib.check(lib.tde_deconv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w),
+                                                                     run.vptr(op.src, True), acc, ptr(ws), wsb, st),
+                                           op.layer + " bwd data")
+                            else:
+                                _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
+                                                                   acc, ptr(ws), wsb, st), op.layer + " bwd data")
                     if ev is not None:
                         self._flush_wgrad(ev)
                 elif src_needs:
@@ -918,6 +927,62 @@ class KernelTimer:
     def by_tag(self):
         torch.cuda.synchronize()
         return [(fam, tag, a.elapsed_time(b), fl) for fam, a, b, fl, tag in self.spans]
+
+
+class GraphTimer:
+    """Conv-kernel spans of the PRODUCTION step as captured and replayed (bench.py's roofline): each conv entry
+    call is preceded by tde_conv_span_arm with a fresh pair of timing events, which the library records with
+    hipEventRecordExternal right before the call's first conv-family kernel and right after its last (split-K
+    reduce included, the BatchNorm launches of a fused conv + BN call excluded).  Captured, they are event-record
+    nodes of the step's graphs; after a replay, elapsed time per span is the time its kernels took where the graph
+    ran them (filter gradients on their side stream, two networks on two streams).  Only the conv families are
+    timed; every other span is a no-op."""
+
+    graph = True
+    FAMILIES = ("conv_fwd", "conv_bwd", "conv_dgrad", "conv_wgrad")
+
+    def __init__(self, max_spans=2048):
+        self.spans = []   # (family, begin GraphEvent, end GraphEvent, flops, tag)
+        self.tag = None
+        self.nbytes = {}
+        # the events exist before the capture opens: creating one inside a thread-local capture is a prohibited
+        # call (hipErrorStreamCaptureUnsupported, picked up by the next launch-status check)
+        self._pool = [(_lib.GraphEvent(), _lib.GraphEvent()) for _ in range(max_spans)]
+
+    def span(self, family, flops=0.0, nbytes=0.0):
+        # only inside a capture: the capture's eager warm-up steps record nothing
+        if family not in self.FAMILIES or not torch.cuda.is_current_stream_capturing():
+            return NO_SPAN
+        self.nbytes[family] = self.nbytes.get(family, 0.0) + nbytes
+        return _GraphSpan(self, family, flops)
+
+    def totals(self):
+        """family -> (ms, flops, launches) of the LAST replay (call after a replay and a synchronize)."""
+        out = {}
+        for fam, a, b, fl, _ in self.spans:
+            t, f, n = out.get(fam, (0.0, 0.0, 0))
+            out[fam] = (t + a.elapsed_ms(b), f + fl, n + 1)
+        return out
+
+
+class _GraphSpan:
+    def __init__(self, timer, family, flops):
+        self.timer, self.family, self.flops = timer, family, flops
+
+    def __enter__(self):
+        if not self.timer._pool:
+            raise _lib.TdeError("GraphTimer: more conv calls than max_spans")
+        self.a, self.b = self.timer._pool.pop()
+        _lib.load().tde_conv_span_arm(self.a.ev, self.b.ev)
+        return self
+
+    def __exit__(self, *exc):
+        n = _lib.load().tde_conv_span_arm(None, None)
+        if exc[0] is None:
+            if n != 2:
+                raise _lib.TdeError(f"conv span of {self.timer.tag}: {n} marks recorded, expected 2")
+            self.timer.spans.append((self.family, self.a, self.b, self.flops, self.timer.tag))
+        return False
 
 
 class _Span:

@@ -163,21 +163,6 @@ class AdamOverlap:
             _lib.wait_stream(torch.cuda.current_stream(), st)
 
 
-class ChainAdam(AdamOverlap):
-    """Config 4's overlapped network (depth_net) in the two-chain schedule: its Adam per gradient bucket on that
-    network's filter-gradient stream as soon as backward has finalised the bucket (AdamOverlap with
-    on_wgrad_stream), so the update hides under the rest of its backward instead of ending the step's critical
-    chain.  begin_step() / finish() run on the chain's own stream, inside its captured piece; no other stream is
-    involved (the base class's side stream stays unused and is never waited on)."""
-
-    def finish(self):
-        rest = [b for b in self.buckets if id(b) not in self.done]
-        if rest:
-            self.launch(rest)
-        for st in set(self.streams.values()):
-            _lib.wait_stream(torch.cuda.current_stream(), st)
-
-
 class DeferredAdam:
     """Single-GPU: the optimizer step of step k runs at the START of step k+1 on a side stream, overlapped
     with that step's forward, which waits (per parameter bucket, in forward order) only for the buckets of
@@ -280,6 +265,7 @@ class Trainer:
 
     adam_ov = None
     dadam = None
+    _graph_owes = False      # deferred Adam: the captured step begins with an owed update
     net_stream = None        # enable_net_overlap: the second program's calls on their own stream
 
     det_ws = None            # enable_deterministic: workspace of the deterministic warp-loss scatter
@@ -303,14 +289,14 @@ class Trainer:
         (enable_ddp).  Not combinable with the Adam overlaps or SyncBN."""
         if on and (self.adam_ov is not None or self.dadam is not None or getattr(self, "sync_bn", False)):
             raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / SyncBN")
-        # TDE_NET_PRIO: priority of the second stream ("high": its network is the longer chain of config 4)
-        self.net_stream = _lib.owned_stream(self, "net", os.environ.get("TDE_NET_PRIO") or None) if on else None
+        self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
     def _overlap_stream(self):
         """The second stream when the overlap applies to this call (not under the instrumented eager step,
         whose per-family HIP-event timer records on one stream)."""
-        if self.net_stream is None or any(getattr(p, "timer", None) is not None for p in self.programs()):
+        if self.net_stream is None or any(getattr(p, "timer", None) is not None and not getattr(p.timer, "graph", False)
+                                          for p in self.programs()):
             return None
         return self.net_stream
 
@@ -333,7 +319,9 @@ class Trainer:
         return self.dadam
 
     def flush(self):
-        """Apply the update a deferred-Adam step still owes (before reading or saving the parameters)."""
+        """Apply the update a deferred-Adam step still owes (before reading or saving the parameters).  In graph
+        mode the captured step begins with the owed update unconditionally, so after an eager flush the next
+        step() runs eagerly once (no update owed at its start) and replays resume after it (step())."""
         if self.dadam is not None and self.dadam.pending:
             self.phase_update()
             self.dadam.pending = False
@@ -446,9 +434,6 @@ class Trainer:
 
     def hook(self, chunk):
         """on_grads callback for NetProgram.backward (None without an overlapped exchange)."""
-        cadam = getattr(self, "_cadam", None)
-        if cadam is not None and id(chunk) in cadam.streams:
-            return cadam.hook(chunk)
         if self.adam_ov is not None:
             return self.adam_ov.hook(chunk)
         gs = self.grad_sync
@@ -463,6 +448,14 @@ class Trainer:
         if gs is not None:
             gs()
         self._update()
+
+    def release_graphs(self):
+        """Drop the captured graphs (their memory pools go with them); step() runs eagerly until the next capture."""
+        self.graphs = self.segments = None
+        if hasattr(self, "ov_seq"):
+            self.ov_seq = None
+        if hasattr(self, "ov_upd"):
+            self.ov_upd = None
 
     def capture(self, warmup=2, **kw):
         """Warm up on a side stream (allocates every lazily created buffer), then record.  Every cross-stream wait
@@ -482,6 +475,9 @@ class Trainer:
         gs = self.grad_sync
         if gs is None:
             g = torch.cuda.CUDAGraph()
+            # deferred Adam: whether the captured step begins with an owed update (it is recorded only if one
+            # is owed at capture time); step() replays only when that matches the owed state
+            self._graph_owes = self.dadam is not None and self.dadam.pending
             with torch.cuda.graph(g, stream=_lib.owned_stream(self, "capture"), capture_error_mode=CAPTURE_MODE):
                 self._begin()
                 self.phase_compute()
@@ -542,7 +538,14 @@ class Trainer:
             gs.finish()
             self.graphs[-1].replay()
         elif len(self.graphs) == 1:
+            if self.dadam is not None and self.dadam.pending != self._graph_owes:
+                # an eager flush() (checkpoint save, read-out) already applied the update the graph would apply
+                # first: one eager step (which owes nothing at its start), after which replays line up again
+                self.step_eager()
+                return
             self.graphs[0].replay()
+            if self.dadam is not None:
+                self.dadam.pending = True     # the replayed step's own update is owed
         else:
             self.graphs[0].replay()
             self.grad_sync()
@@ -774,40 +777,13 @@ class DepthThenCamTrainer(Trainer):
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
     def _chain_pair(self):
-        cadam = self._chain_adam("pair")
-        if cadam is not None:
-            cadam.begin_step()
         self._p_fwd_pair()
         self._p_loss()
         self._p_bwd_pair()
-        if cadam is not None:
-            cadam.finish()
 
     def _chain_single(self):
-        cadam = self._chain_adam("single")
-        if cadam is not None:
-            cadam.begin_step()
         self._p_fwd_single()
         self._p_bwd_single()
-        if cadam is not None:
-            cadam.finish()
-
-    def _chain_adam(self, net):
-        """ChainAdam of `net` when that network is the overlapped one of the two-chain schedule and runs its
-        filter gradients on ONE side stream, with TDE_C4_CHAIN_ADAM=1 (default off: measured 1043 -> 777 pairs/s,
-        profiles/ab_r03s2e_chain_adam.txt); else None (inline Adam after its backward)."""
-        if not (self._inline_adam() and C4_CHAINS and net == self.ov_net and self._overlap_stream() is not None
-                and os.environ.get("TDE_C4_CHAIN_ADAM", "0") == "1"):
-            return None
-        p = getattr(self, net)
-        if p.wgrad_stream is None or isinstance(p.wgrad_stream, str) or len(p.wgrad_streams) != 1:
-            return None
-        c = getattr(self, "_cadam", None)
-        if c is None or c.streams.get(id(p.chunk)) is not p.wgrad_stream:
-            opt = self.opt.opts[0 if net == "single" else 1]
-            c = self._cadam = ChainAdam([opt], float(os.environ.get("TDE_C4_CHAIN_ADAM_MB", "16")),
-                                        {id(p.chunk): self.BACKWARD_USES}, streams={id(p.chunk): p.wgrad_stream})
-        return c
 
     def _p_inputs(self):
         self._p_concat()
@@ -906,7 +882,7 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("pr", self.pair, True)
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
-        if self._inline_adam() and self._chain_adam("pair") is None:
+        if self._inline_adam():
             self.opt.opts[1].step()
 
     def _p_bwd_single(self):
@@ -915,7 +891,7 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("sr", self.single, True)
             self._bwd("sl", self.single, False)
-        if self._inline_adam() and self._chain_adam("single") is None:
+        if self._inline_adam():
             self.opt.opts[0].step()
 
     def phase_compute(self):
