@@ -330,11 +330,13 @@ def graph_timed_conv(tr, replays=7):
     finally:
         for p in progs:
             p.timer = None
-    per = []
+    per, spans, busy = [], None, []
     for _ in range(replays):
         tr.step()
         torch.cuda.synchronize()
         per.append(timer.totals())
+        busy.append(timer.busy_ms())
+        spans = timer.per_span_ms()
     tr.flush()
     tr.release_graphs()
     torch.cuda.synchronize()
@@ -342,7 +344,8 @@ def graph_timed_conv(tr, replays=7):
     for fam in per[0]:
         ms = sorted(p[fam][0] for p in per)
         out[fam] = (ms[len(ms) // 2], per[0][fam][1], per[0][fam][2])
-    return out, timer.nbytes
+    busy.sort()
+    return out, spans, busy[len(busy) // 2]
 
 
 def timed_steps(tr, steps, warmup, world, rank, use_graph):
@@ -404,6 +407,7 @@ def main():
                          "precision, the fp32-accurate 3-way bf16 split (LDS-staged / register-split) or the "
                          "fp32-accurate scaled 2-way fp16 split (3 fp16 MFMAs per product; the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph-spans", default="", help="write the per-call conv spans of the graph timing (JSON)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workloads (configs 2, 3 and 5 timed after the headline at N = 1)")
     ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
@@ -451,9 +455,15 @@ def main():
     # roofline: measured on the captured production schedule the timed region replays (N = 1); the instrumented
     # eager step (conv and BN as separate calls, one stream) stays in the line as kernel_breakdown_ms
     gfam = None
+    gbusy = None
     if use_graph and world == 1:
-        gfam, _ = graph_timed_conv(tr)
-        conv_ms, conv_flops, conv_launches = conv_family(gfam)
+        gfam, gspans, gbusy = graph_timed_conv(tr)
+        if args.graph_spans:
+            with open(args.graph_spans, "w") as fh:
+                json.dump([{"family": f, "layer": t, "ms": round(ms, 5), "gflop": fl / 1e9} for f, t, ms, fl in gspans],
+                          fh, indent=0)
+        span_sum_ms, conv_flops, conv_launches = conv_family(gfam)
+        conv_ms = gbusy
     else:
         conv_ms, conv_flops, conv_launches = conv_family(fam)
     el = timed_steps(tr, args.steps, args.warmup, world, rank, use_graph)
@@ -508,10 +518,17 @@ def main():
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "peak_note": peak_note, "traffic": None,
-                         "timing": ("HIP event-record nodes around every conv entry call's kernels inside the "
-                                    "captured production step (the graphs the timed region replays, less the nodes), "
-                                    "median of 7 replays" if gfam is not None else
+                         "timing": ("conv-busy wall time of the captured production step: a one-wave stamp kernel "
+                                    "(device real-time counter) before and after every conv entry call's kernels "
+                                    "inside the graphs the timed region replays (less the stamps), the union of the "
+                                    "stamped intervals over the step's 2-3 concurrent streams, median of 7 replays"
+                                    if gfam is not None else
                                     "HIP events around each conv call of an instrumented eager step on one stream"),
+                         "sum_of_call_spans_ms": round(span_sum_ms, 4) if gfam is not None else None,
+                         "sum_of_call_spans_note": ("per-call spans added up: calls running concurrently on "
+                                                    "different streams each count in full (their kernels share the "
+                                                    "CUs), so this exceeds the busy time" if gfam is not None
+                                                    else None),
                          "family_ms_per_step": ({k: round(v[0], 4) for k, v in sorted(gfam.items())}
                                                 if gfam is not None else None),
                          "flops_per_step": conv_flops, "conv_ms_per_step": round(conv_ms, 4),

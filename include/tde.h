@@ -102,12 +102,12 @@ uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
 /* Measurement hook (no reference counterpart: bench.py's roofline timing).  Arms the calling thread's pair of
- * hipEvent_t (timing enabled) for the NEXT conv entry call (any tde_conv2d_* / tde_deconv2d_* compute function):
- * ev_begin is recorded right before its first conv-family kernel, ev_end right after its last (split-K reduce
- * included, BatchNorm launches of a fused call excluded), both with hipEventRecordExternal, so inside a stream
- * capture they become event-record nodes that time the kernels where the graph replays them.  (NULL, NULL)
- * disarms.  Returns the number of events the previous arming recorded. */
-int tde_conv_span_arm(void* ev_begin, void* ev_end);
+ * device timestamp slots for the NEXT conv entry call (any tde_conv2d_* / tde_deconv2d_* compute function): a
+ * one-wave kernel writes the 100 MHz real-time counter into *stamp_begin right before the call's first
+ * conv-family kernel and into *stamp_end right after its last (split-K reduce included, BatchNorm launches of a
+ * fused call excluded), so inside a stream capture the stamps time the kernels where the graph replays them.
+ * (NULL, NULL) disarms.  Returns the number of stamps the previous arming launched. */
+int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp_end);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
 /* Weight pre-split (the halo-tiled stride-1 path keeps the layer's weights as split fp16 / bf16 tiles):
  * bytes of the split image op (0 forward, 1 data gradient) of layer d needs under the current conv math;

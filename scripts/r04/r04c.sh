@@ -4,6 +4,6 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python bench.py > gpurun_out/bench_r04c.json 2> gpurun_out/bench_r04c.err
+timeout -k 10 600 python bench.py --graph-spans gpurun_out/spans_r04c.json > gpurun_out/bench_r04c.json 2> gpurun_out/bench_r04c.err
 rc=$?; echo "[r04c] bench rc=$rc"; head -c 2500 gpurun_out/bench_r04c.json; echo; tail -5 gpurun_out/bench_r04c.err
 exit $rc

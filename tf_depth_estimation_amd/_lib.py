@@ -229,44 +229,11 @@ def dedicated_stream():
 
 
 def hip():
-    """The HIP runtime (ctypes) for the few calls torch does not expose: dedicated streams and timing events that
-    a stream capture records as graph nodes."""
+    """The HIP runtime (ctypes) for the few calls torch does not expose (dedicated streams)."""
     global _hip
     if _hip is None:
         _hip = ctypes.CDLL("libamdhip64.so")
     return _hip
-
-
-class GraphEvent:
-    """A timing hipEvent_t recorded with hipEventRecordExternal: inside a stream capture the record becomes an
-    event-record node of the graph, so elapsed times between two such events measure the replayed graph (torch's
-    Event.record() inside a capture only orders streams and times nothing)."""
-
-    def __init__(self):
-        self.ev = ctypes.c_void_p()
-        rc = hip().hipEventCreate(ctypes.byref(self.ev))
-        if rc != 0:
-            raise TdeError(f"hipEventCreate failed ({rc})")
-
-    def record(self, stream=None):
-        st = (stream or torch.cuda.current_stream()).cuda_stream
-        rc = hip().hipEventRecordWithFlags(self.ev, ctypes.c_void_p(st), ctypes.c_uint(1))   # hipEventRecordExternal
-        if rc != 0:
-            raise TdeError(f"hipEventRecordWithFlags failed ({rc})")
-
-    def elapsed_ms(self, end):
-        ms = ctypes.c_float()
-        rc = hip().hipEventElapsedTime(ctypes.byref(ms), self.ev, end.ev)
-        if rc != 0:
-            raise TdeError(f"hipEventElapsedTime failed ({rc})")
-        return ms.value
-
-    def __del__(self):
-        try:
-            if self.ev and _hip is not None:
-                _hip.hipEventDestroy(self.ev)
-        except Exception:
-            pass
 
 
 # ---- cross-stream ordering inside stream capture

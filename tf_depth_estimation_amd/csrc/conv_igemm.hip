@@ -1460,16 +1460,23 @@ static ConvArgs make_args(const tde_conv_desc_t& d) {
 }
 
 // Conv-kernel spans for bench.py's graph-timed roofline (tde_conv_span_arm): when the calling thread has armed a
-// pair of timing events, the next conv entry call records the first right before its first conv-family kernel
-// (GEMM, halo, halo-WGRAD or pixel-shuffle kernel) and the second right after its last one (split-K reduce
-// included; the BatchNorm launches of a fused conv + BN call come after it), with hipEventRecordExternal so that
-// under stream capture they become event-record nodes of the graph and time the kernels where the captured step
-// replays them.  Unarmed (always, outside bench's timing capture): no event, no cost.
-static thread_local hipEvent_t g_span_ev[2] = {nullptr, nullptr};
+// pair of device timestamp slots, the next conv entry call launches a one-wave stamp kernel right before its first
+// conv-family kernel (GEMM, halo, halo-WGRAD or pixel-shuffle kernel) and one right after its last (split-K reduce
+// included; the BatchNorm launches of a fused conv + BN call come after it).  Kernels of one stream (and dependent
+// graph nodes) run one after another, so the two stamps bracket the call's kernels where a captured graph replays
+// them.  (Timing events cannot serve: recording one inside the trainer's thread-local capture is refused,
+// hipErrorStreamCaptureUnsupported.)  The stamp is the 100 MHz constant real-time counter.  Unarmed (always,
+// outside bench's timing capture): no launch, no cost.
+__global__ void __launch_bounds__(64) span_stamp_kernel(unsigned long long* slot) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) slot[threadIdx.x] = t;      // a per-lane (vector) address
+}
+static thread_local unsigned long long* g_span_slot[2] = {nullptr, nullptr};
 static thread_local int g_span_marks = 0;
 static void span_mark(int which, hipStream_t st) {
-  if (g_span_ev[which] != nullptr && hipEventRecordWithFlags(g_span_ev[which], st, hipEventRecordExternal) == hipSuccess)
-    ++g_span_marks;
+  if (g_span_slot[which] == nullptr) return;
+  hipLaunchKernelGGL(span_stamp_kernel, dim3(1), dim3(64), 0, st, g_span_slot[which]);
+  ++g_span_marks;
 }
 
 // Timing experiments only (results are garbage), compiled in ONLY by a diagnostic build (-DTDE_TIMING_DIAG; never
@@ -2006,12 +2013,12 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
   return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
-// bench.py's graph-timed roofline: arm the calling thread's conv-kernel span events (hipEvent_t, timing enabled;
-// null, null disarms).  Returns how many span marks the previous arming recorded (2 after one conv entry call).
-int tde_conv_span_arm(void* ev_begin, void* ev_end) {
+// bench.py's graph-timed roofline: arm the calling thread's conv-kernel span stamp slots (device uint64, 8-byte
+// aligned; null, null disarms).  Returns how many stamps the previous arming launched (2 after one conv entry call).
+int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp_end) {
   const int n = g_span_marks;
-  g_span_ev[0] = static_cast<hipEvent_t>(ev_begin);
-  g_span_ev[1] = static_cast<hipEvent_t>(ev_end);
+  g_span_slot[0] = stamp_begin;
+  g_span_slot[1] = stamp_end;
   g_span_marks = 0;
   return n;
 }

@@ -931,37 +931,60 @@ class KernelTimer:
 
 class GraphTimer:
     """Conv-kernel spans of the PRODUCTION step as captured and replayed (bench.py's roofline): each conv entry
-    call is preceded by tde_conv_span_arm with a fresh pair of timing events, which the library records with
-    hipEventRecordExternal right before the call's first conv-family kernel and right after its last (split-K
-    reduce included, the BatchNorm launches of a fused conv + BN call excluded).  Captured, they are event-record
-    nodes of the step's graphs; after a replay, elapsed time per span is the time its kernels took where the graph
-    ran them (filter gradients on their side stream, two networks on two streams).  Only the conv families are
-    timed; every other span is a no-op."""
+    call is preceded by tde_conv_span_arm with a fresh pair of device timestamp slots; the library launches a
+    one-wave stamp kernel (100 MHz real-time counter) right before the call's first conv-family kernel and one right
+    after its last (split-K reduce included, the BatchNorm launches of a fused conv + BN call excluded).  Captured,
+    the stamps are nodes of the step's graphs; after a replay, end - begin per span is the time its kernels took
+    where the graph ran them (filter gradients on their side stream, two networks on two streams).  Only the conv
+    families are timed; every other span is a no-op, and nothing is recorded outside a capture."""
 
     graph = True
     FAMILIES = ("conv_fwd", "conv_bwd", "conv_dgrad", "conv_wgrad")
+    TICK_MS = 1e-5        # s_memrealtime: 100 MHz
 
     def __init__(self, max_spans=2048):
-        self.spans = []   # (family, begin GraphEvent, end GraphEvent, flops, tag)
+        self.spans = []   # (family, span index, flops, tag)
         self.tag = None
         self.nbytes = {}
-        # the events exist before the capture opens: creating one inside a thread-local capture is a prohibited
-        # call (hipErrorStreamCaptureUnsupported, picked up by the next launch-status check)
-        self._pool = [(_lib.GraphEvent(), _lib.GraphEvent()) for _ in range(max_spans)]
+        self.stamps = torch.zeros((max_spans, 2), dtype=torch.int64, device="cuda")
 
     def span(self, family, flops=0.0, nbytes=0.0):
-        # only inside a capture: the capture's eager warm-up steps record nothing
         if family not in self.FAMILIES or not torch.cuda.is_current_stream_capturing():
             return NO_SPAN
+        if len(self.spans) >= self.stamps.shape[0]:
+            raise _lib.TdeError("GraphTimer: more conv calls than max_spans")
         self.nbytes[family] = self.nbytes.get(family, 0.0) + nbytes
         return _GraphSpan(self, family, flops)
 
+    def per_span_ms(self):
+        """[(family, tag, ms, flops)] of the LAST replay (call after a replay and a synchronize)."""
+        st = self.stamps.cpu()
+        return [(fam, tag, float(st[k, 1] - st[k, 0]) * self.TICK_MS, fl) for fam, k, fl, tag in self.spans]
+
+    def busy_ms(self):
+        """Wall time of the last replay during which at least one conv span was open: the union of the spans'
+        [begin, end] intervals over all the step's streams (the stamp counter is device-wide), so concurrent
+        kernels on two or three streams are not counted twice."""
+        st = self.stamps.cpu()
+        iv = sorted((int(st[k, 0]), int(st[k, 1])) for _, k, _, _ in self.spans)
+        tot, cur_a, cur_b = 0, None, None
+        for a, b in iv:
+            if cur_b is None or a > cur_b:
+                if cur_b is not None:
+                    tot += cur_b - cur_a
+                cur_a, cur_b = a, b
+            else:
+                cur_b = max(cur_b, b)
+        if cur_b is not None:
+            tot += cur_b - cur_a
+        return tot * self.TICK_MS
+
     def totals(self):
-        """family -> (ms, flops, launches) of the LAST replay (call after a replay and a synchronize)."""
+        """family -> (ms, flops, calls) of the last replay."""
         out = {}
-        for fam, a, b, fl, _ in self.spans:
+        for fam, _, ms, fl in self.per_span_ms():
             t, f, n = out.get(fam, (0.0, 0.0, 0))
-            out[fam] = (t + a.elapsed_ms(b), f + fl, n + 1)
+            out[fam] = (t + ms, f + fl, n + 1)
         return out
 
 
@@ -970,18 +993,17 @@ class _GraphSpan:
         self.timer, self.family, self.flops = timer, family, flops
 
     def __enter__(self):
-        if not self.timer._pool:
-            raise _lib.TdeError("GraphTimer: more conv calls than max_spans")
-        self.a, self.b = self.timer._pool.pop()
-        _lib.load().tde_conv_span_arm(self.a.ev, self.b.ev)
+        self.k = len(self.timer.spans)
+        base = self.timer.stamps.data_ptr() + 16 * self.k
+        _lib.load().tde_conv_span_arm(ctypes.c_void_p(base), ctypes.c_void_p(base + 8))
         return self
 
     def __exit__(self, *exc):
         n = _lib.load().tde_conv_span_arm(None, None)
         if exc[0] is None:
             if n != 2:
-                raise _lib.TdeError(f"conv span of {self.timer.tag}: {n} marks recorded, expected 2")
-            self.timer.spans.append((self.family, self.a, self.b, self.flops, self.timer.tag))
+                raise _lib.TdeError(f"conv span of {self.timer.tag}: {n} stamps launched, expected 2")
+            self.timer.spans.append((self.family, self.k, self.flops, self.timer.tag))
         return False
 
 
