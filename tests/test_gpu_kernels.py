@@ -580,7 +580,8 @@ def test_head_fwd_bwd(L, case):
 
 
 @pytest.mark.parametrize("M,C,ycs,yco", [(8 * 96 * 128, 32, 68, 32), (32, 512, 1024, 512), (8 * 12 * 16, 256, 256, 0),
-                                         (2048, 20, 24, 4), (2049, 20, 20, 0), (8, 1024, 1024, 0), (8193, 64, 64, 0)])
+                                         (2048, 20, 24, 4), (2049, 20, 20, 0), (8, 1024, 1024, 0), (8192, 16, 20, 4),
+                                         (8193, 64, 64, 0)])
 def test_bn_train_fwd_bwd(L, M, C, ycs, yco):
     lib = L.load()
     st = L.stream_ptr()

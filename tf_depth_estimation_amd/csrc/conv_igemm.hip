@@ -1153,7 +1153,7 @@ static int g_conv_math = []() {
   const long m = env_long("TDE_CONV_MATH", 4);
   return (int)(m >= 0 && m <= 4 ? m : 4);
 }();
-static const long g_split_target = tde_env_pos("TDE_SPLIT_TARGET", 512);   // blocks to aim for
+static const long g_split_target = tde_env_pos("TDE_SPLIT_TARGET", 384);   // blocks to aim for (round 4: 384, see make_plan)
 static const long g_split_minkt = tde_env_pos("TDE_SPLIT_MINKT", 4);       // >= k-tiles per split
 static const long g_split_slab = tde_env_pos("TDE_SPLIT_SLAB_MB", 128) << 20;
 // tile / split overrides for kernel exploration (scripts/conv_micro.py); 0 = planner's choice
@@ -1231,7 +1231,11 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
   const int nkt = tde_cdiv(Kd, BK);
-  // split K until ~2 blocks per CU, keeping >= 4 k-tiles (128 reduction elements) per split
+  // split K until ~1.5 blocks per CU (g_split_target 384), keeping >= 4 k-tiles (128 reduction elements) per split.
+  // Round 4: 384 instead of 512 -- with config 4's two networks on two streams each GEMM no longer has to fill the
+  // chip alone, and fewer splits mean fewer slab bytes and shorter reduces (same box, alternating x2: config 4
+  // 1043-1047 -> 1066-1067 pairs/s, config 2 2917-2918 -> 2924-2927; 256: config 4 1065, config 2 -1.3 %;
+  // profiles/r04/ab_r04e_split.txt)
   int splits = 1;
   const long target = g_split_target;
   if (tiles < target) {
