@@ -395,6 +395,11 @@ def env_knobs():
 
 
 def main():
+    # the ONE JSON line goes to the original stdout; everything native libraries print there (RCCL's version banner at
+    # communicator creation, for one) is sent to stderr instead, so stdout holds nothing but the line
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -430,8 +435,8 @@ def main():
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
                          "Measured config 4 605 -> 665 samples/s")
     ap.add_argument("--sync-bn", action="store_true",
-                    help="BatchNorm over the global batch (one RCCL all-reduce per BN layer and direction; the step "
-                         "runs eagerly, RCCL is not captured)")
+                    help="BatchNorm over the global batch (one RCCL all-reduce of every row group's sums per BN layer "
+                         "and direction, on a communicator of its own, captured into the step's graphs)")
     ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
                     help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
     args = ap.parse_args()
@@ -441,8 +446,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1 or args.sync_bn:
+        # (--sync-bn at N = 1: a world-1 RCCL group, so the SyncBN step -- sums kernels and the captured
+        # all-reduce nodes -- runs as it does at N > 1)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
 
     from tf_depth_estimation_amd import _api, _lib, variables
 
@@ -451,7 +460,7 @@ def main():
     _lib.check(_lib.load().tde_set_conv_math(_lib.CONV_MATH[args.math]), "conv math")
     tr, opts = build_trainer(args, args.workload, N, world, rank)
     fam, fam_bytes = instrumented_step(tr)
-    use_graph = not args.no_graph and not args.sync_bn
+    use_graph = not args.no_graph
     # roofline: measured on the captured production schedule the timed region replays (N = 1); the instrumented
     # eager step (conv and BN as separate calls, one stream) stays in the line as kernel_breakdown_ms
     gfam = None
@@ -585,8 +594,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.workload, N)
             log("[bench] depth L1 vs the float64 reference restatement ...")
             out["depth_l1_vs_ref"] = depth_l1_vs_ref(args.workload, N)
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -18,6 +18,11 @@ non-zero exit fails the test.  The global batch is 2 x B (rank r takes rows [rB,
              oracle's whole-batch loss (1e-5), and the exchanged gradient is the whole-batch gradient within the
              oracle bars -- the reference's single-device semantics at the global batch
              (train_depth_then_cam_lr.py:130-136: one BatchNorm batch per call).
+  c4_syncbn: config 4 with twin batching and SyncBN: every row group (left images / right images, (L,R) pairs /
+             (R,L) pairs) normalised over its rows on BOTH ranks, the groups' sums in one all-reduce per layer; each
+             rank's outputs and poses equal the float64 oracle's four calls on the whole 2B batch (1e-4), the mean of
+             the rank losses its loss terms (1e-5; consistency 1e-4), the exchanged gradient the whole-batch gradient
+             within the oracle bars.
 """
 import os
 import sys
@@ -192,6 +197,75 @@ def case_c2_syncbn(rank, world, mode):
         print(f"c2_syncbn: whole-batch gradient vs fp64 oracle {e_gpu:.2e} (fp32 oracle {e_cpu:.2e})")
 
 
+def case_c4_syncbn(rank, world, mode):
+    from oracle import losses as OL
+    from oracle import nets as ON
+    from test_gpu_nets import GRAD_FACTOR, check_grads_global, oracle_params_from, rel_err
+    from tf_depth_estimation_amd import _lib
+    assert mode == "eager", "SyncBN over gloo all-reduces on the host: eager only"
+    from test_gpu_trainers import intrinsics, small_pose, texture
+    from tf_depth_estimation_amd import _api, train, variables
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    G = 2 * B
+    il, ir = texture(G, H, W, 31), texture(G, H, W, 32)
+    lab = torch.tensor(np.random.default_rng(33).uniform(0.1, 2.0, (G, H, W, 1)), dtype=torch.float32)
+    K, gt = intrinsics(G, H, W), small_pose(G, 34)
+    sl = slice(rank * B, (rank + 1) * B)
+    tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
+    assert tr.twin and tr.runs["s"].groups == 2
+    tr.set_batch(il[sl].cuda(), ir[sl].cuda(), lab[sl].cuda(), K[sl].cuda(), gt[sl].cuda())
+    tr.enable_sync_bn(world)
+    tr.enable_ddp(world, bucket_mb=4.0)
+    P64 = [oracle_params_from(c, "", torch.float64) for c in tr.chunks]
+    P32 = [oracle_params_from(c, "", torch.float32) for c in tr.chunks]
+    tr.grad_sync.begin_step()
+    tr.phase_compute()
+    tr.grad_sync.finish()
+    torch.cuda.synchronize()
+    parts = tr.loss_parts()
+    out = {k: [t.detach().cpu() for t in v] for k, v in tr._out.items()}
+    pose = {d: tr.pose[d].detach().cpu() for d in ("lr", "rl")}
+    vals = torch.tensor([parts[k] for k in ("smooth", "depth", "exp", "cam", "photo", "consist")], dtype=torch.float64)
+    al = gather(vals)
+    mean_parts = (al[0] + al[1]) / world
+    grads = {}
+    for dt, Ps in ((torch.float64, P64), (torch.float32, P32)):
+        Pss, Ppp = Ps
+        x = {"il": il.to(dt), "ir": ir.to(dt)}                 # the WHOLE batch on one device
+        dsl = ON.disp_net(Pss, x["il"], True, scope="model_singledepth/depth_net")
+        dsr = ON.disp_net(Pss, x["ir"], True, scope="model_singledepth/depth_net")
+        dpl, pr, ml = ON.depth_net(Ppp, torch.cat([x["il"], x["ir"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        dpr, pl, mr = ON.depth_net(Ppp, torch.cat([x["ir"], x["il"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        total, rp = OL.loss_depth_then_cam_lr(dsl, dsr, dpl, dpr, pr, pl, ml, mr, x["il"], x["ir"], lab.to(dt),
+                                              K.to(dt), gt.to(dt))
+        if dt == torch.float64:
+            for i in range(4):
+                for key, ref in (("sl", dsl), ("sr", dsr), ("pl", dpl), ("pr", dpr)):
+                    e = rel_err(out[key][i], ref[i][sl])
+                    assert e <= 1e-4, f"rank {rank} {key} disp{i + 1}: SyncBN vs whole-batch BN {e:.2e}"
+                assert rel_err(out["pl"][5 + i], ml[i][sl]) <= 1e-4 and rel_err(out["pr"][5 + i], mr[i][sl]) <= 1e-4
+            assert rel_err(pose["lr"], pr.reshape(G, 6)[sl]) <= 1e-4 and rel_err(pose["rl"], pl.reshape(G, 6)[sl]) <= 1e-4
+
+            def v(t):
+                return t.item() if torch.is_tensor(t) else float(t)
+            want = [v(rp["smooth"]), v(rp["depth"]), v(rp["exp"]), v(rp["cam"]), v(rp["pixel"]), v(rp["consist"])]
+            for name, got, w, tol in zip(("smooth", "depth", "exp", "cam", "photo", "consist"), mean_parts.tolist(),
+                                         want, (1e-5,) * 5 + (1e-4,)):
+                assert abs(got - w) <= tol * abs(w) + 1e-9, (name, got, w)
+        total.backward()
+        grads[dt] = {n: t.grad for P in Ps for n, t in P.vars.items()}
+    gpu = {}
+    for c in tr.chunks:
+        gpu.update({n: c.grad_view(n) for n in c.names()})
+    e_gpu, e_cpu = check_grads_global(gpu, grads[torch.float64], grads[torch.float32],
+                                      GRAD_FACTOR[_lib.load().tde_get_conv_math()])
+    if rank == 0:
+        print(f"c4_syncbn: whole-batch gradient vs fp64 oracle {e_gpu:.2e} (fp32 oracle {e_cpu:.2e})")
+
+
 def main():
     case, mode = sys.argv[1], sys.argv[2]
     torch.cuda.set_device(0)            # both ranks share the box's one GPU
@@ -200,7 +274,7 @@ def main():
     assert world == 2
     torch.set_num_threads(4)
     try:
-        {"c4_local": case_c4_local, "c2_syncbn": case_c2_syncbn}[case](rank, world, mode)
+        {"c4_local": case_c4_local, "c2_syncbn": case_c2_syncbn, "c4_syncbn": case_c4_syncbn}[case](rank, world, mode)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -7,7 +7,9 @@ runs over RCCL).  tests/ddp_gpu_worker.py holds the cases and their assertions:
       exchange; exchanged gradient == mean of the ranks' local gradients bit for bit, within the oracle bars of the
       mean of the fp64 per-shard gradients, replicas bit-identical after Adam and over later (replayed) steps;
   c2_syncbn (eager): SyncBN across the two ranks == whole-batch BatchNorm (outputs 1e-4, loss 1e-5, gradient within
-      the oracle bars of the whole-batch fp64 gradient)."""
+      the oracle bars of the whole-batch fp64 gradient);
+  c4_syncbn (eager): the same for config 4's twin-batched, row-grouped SyncBN (each call's BatchNorm batch spans both
+      ranks: the reference's one-device batch of 2B)."""
 import os
 import socket
 import subprocess
@@ -26,7 +28,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("case,mode", [("c4_local", "eager"), ("c4_local", "graph"), ("c2_syncbn", "eager")])
+@pytest.mark.parametrize("case,mode", [("c4_local", "eager"), ("c4_local", "graph"), ("c2_syncbn", "eager"),
+                                       ("c4_syncbn", "eager")])
 def test_two_ranks_on_one_gpu(case, mode):
     env = dict(os.environ, OMP_NUM_THREADS="4", PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

@@ -407,11 +407,12 @@ class NetProgram:
             if sp is not None:
                 d.w_split[0], d.w_split[1] = sp[0], sp[1]
 
-    def _sums(self, i, K, which):
-        key = (i, which)
+    def _sums(self, i, K, which, G=1):
+        """fp64 per-channel sums [G][2K] of op i (which: 0 forward, 1 local backward, 2 all-reduced backward)."""
+        key = (i, which, G)
         t = self._bn_sums.get(key)
         if t is None:
-            t = self._bn_sums[key] = torch.empty(2 * K, dtype=torch.float64, device="cuda")
+            t = self._bn_sums[key] = torch.empty((G, 2 * K), dtype=torch.float64, device="cuda")
         return t
 
     def _span(self, family, flops=0.0, nbytes=0.0):
@@ -559,8 +560,6 @@ class NetProgram:
         if fold_bn and (is_training or self._folded is None):
             raise ValueError("fold_bn needs is_training=False and weights folded by fold_bn()")
         N = run.N
-        if self.bn_sync is not None and run.groups > 1:
-            raise NotImplementedError("SyncBN over row-grouped runs")
         lib = _lib.load()
         st = _lib.stream_ptr()
         spec = self.spec
@@ -620,17 +619,26 @@ class NetProgram:
                         _lib.check(fn(ctypes_ref(fd), run.vptr(op.src), ptr(wf), ptr(bf), 1, run.vptr(op.dst), ptr(ws),
                                       wsb, st), op.layer)
                 elif is_training and self.bn_sync is not None:
-                    # SyncBN: conv, local (sum z, sum z^2), all-reduce, BN over all replicas' rows
+                    # SyncBN: conv, local (sum z, sum z^2) per row group, ONE all-reduce of all groups' sums, then
+                    # each group normalised over its rows of all replicas (a twin run's left / right halves stay
+                    # separate BatchNorm batches, as the reference's two calls, train_depth_then_cam_lr.py:130-136)
                     fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
                     _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
-                    sums = self._sums(i, op.K, 0)
-                    _lib.check(lib.tde_bn_sums(M, op.K, ptr(z), None, 0, 0, None, None, None, 0, 0, ptr(sums), ptr(ws),
-                                               wsb, st), op.layer + " bn sums")
+                    G = run.groups
+                    Mg = M // G
+                    sums = self._sums(i, op.K, 0, G)
+                    for g in range(G):
+                        _lib.check(lib.tde_bn_sums(Mg, op.K, ptr(z[g * (N // G):]), None, 0, 0, None, None, None, 0, 0,
+                                                   ptr(sums[g]), ptr(ws), wsb, st), op.layer + " bn sums")
                     self.bn_sync(sums)
-                    _lib.check(lib.tde_bn_fwd_from_sums(M, op.K, M * self.bn_world, ptr(z), ptr(sums), ptr(beta), 1e-3,
-                                                        op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
-                                                        ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st),
-                               op.layer + " syncbn")
+                    ystride = Mg * op.dst.buf.cs * 4
+                    for g in range(G):
+                        _lib.check(lib.tde_bn_fwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(z[g * (N // G):]),
+                                                            ptr(sums[g]), ptr(beta), 1e-3, op.decay, int(self.bessel),
+                                                            ptr(mm), ptr(mv), ptr(sm[0][g * op.K:]),
+                                                            ptr(sm[1][g * op.K:]),
+                                                            ctypes.c_void_p(run.vptr(op.dst).value + g * ystride),
+                                                            op.dst.buf.cs, op.dst.coff, 1, st), op.layer + " syncbn")
                 elif is_training and self._production():
                     # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
                     # consumes the conv's split-K partials directly (a GraphTimer times its conv kernels only)
@@ -757,20 +765,32 @@ class NetProgram:
                                                          ptr(self.G(f"{op.layer}/biases")), pacc, run.absmax_ptr(i),
                                                          ptr(ws), wsb, st), op.layer + " bias_relu_bwd")
                 elif self.bn_sync is not None:
-                    # SyncBN backward: local (sum g, sum g*xhat) -> all-reduced copy -> dz from the global means,
-                    # dbeta from the local sum (the gradient all-reduce averages it like every parameter)
-                    ls, gs = self._sums(i, op.K, 1), self._sums(i, op.K, 2)
+                    # SyncBN backward: local (sum g, sum g*xhat) per row group -> all-reduced copy -> dz from the global
+                    # means; dbeta from the local sums, groups added in order (the gradient all-reduce averages it like
+                    # every parameter)
+                    G = run.groups
+                    Mg = M // G
+                    ls, gs = self._sums(i, op.K, 1, G), self._sums(i, op.K, 2, G)
                     beta = self.P(f"{op.layer}/BatchNorm/beta")
-                    _lib.check(lib.tde_bn_sums(M, op.K, ptr(run.z[i]), run.vptr(op.dst, True), op.dst.buf.cs,
-                                               op.dst.coff, ptr(sm[0]), ptr(sm[1]), ptr(beta), 1, 1, ptr(ls), ptr(ws),
-                                               wsb, st), op.layer + " bn sums")
+                    zi = run.z[i]
+                    dystride = Mg * op.dst.buf.cs * 4
+                    dyp = run.vptr(op.dst, True).value
+                    for g in range(G):
+                        _lib.check(lib.tde_bn_sums(Mg, op.K, ptr(zi[g * (N // G):]), ctypes.c_void_p(dyp + g * dystride),
+                                                   op.dst.buf.cs, op.dst.coff, ptr(sm[0][g * op.K:]),
+                                                   ptr(sm[1][g * op.K:]), ptr(beta), 1, 1, ptr(ls[g]), ptr(ws), wsb, st),
+                                   op.layer + " bn sums")
                     gs.copy_(ls)
                     self.bn_sync(gs)
-                    _lib.check(lib.tde_bn_bwd_from_sums(M, op.K, M * self.bn_world, ptr(run.z[i]), ptr(sm[0]),
-                                                        ptr(sm[1]), ptr(beta), run.vptr(op.dst, True), op.dst.buf.cs,
-                                                        op.dst.coff, ptr(gs), ptr(ls), ptr(dz),
-                                                        ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,
-                                                        run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " syncbn bwd")
+                    for g in range(G):
+                        _lib.check(lib.tde_bn_bwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(zi[g * (N // G):]),
+                                                            ptr(sm[0][g * op.K:]), ptr(sm[1][g * op.K:]), ptr(beta),
+                                                            ctypes.c_void_p(dyp + g * dystride), op.dst.buf.cs,
+                                                            op.dst.coff, ptr(gs[g]), ptr(ls[g]),
+                                                            ptr(dz[g * Mg * op.K:]),
+                                                            ptr(self.G(f"{op.layer}/BatchNorm/beta")),
+                                                            pacc if g == 0 else 1, 1, run.absmax_ptr(i), ptr(ws), wsb,
+                                                            st), op.layer + " syncbn bwd")
                 else:
                     with self._span("bn_bwd"):
                         _lib.check(lib.tde_bn_bwd(M, op.K, run.groups, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),

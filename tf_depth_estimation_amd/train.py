@@ -417,9 +417,17 @@ class Trainer:
 
     def enable_sync_bn(self, world, group=None):
         """SyncBN: every BatchNorm of every network normalises over the rows of all `world`
-        replicas (one RCCL all-reduce of fp64 per-channel sums per BN layer and direction) -- the
-        reference's semantics at the global batch.  RCCL is not captured, so the step runs eagerly."""
+        replicas (one all-reduce of fp64 per-channel sums per BN layer and direction, all row groups of a twin
+        run in one) -- the reference's semantics at the global batch.
+
+        Over RCCL the sums all-reduce on a communicator of their own (a new process group: the gradient exchange's
+        bucket all-reduces run on another stream, and two streams' collectives on ONE communicator may meet in
+        different orders on different GPUs) and the step can be captured: the all-reduces become nodes of the
+        graph.  Over gloo (host collectives) the step runs eagerly."""
         import torch.distributed as dist
+        nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        if nccl and group is None:
+            group = dist.new_group(backend="nccl")
 
         def sync(t):
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
@@ -427,6 +435,7 @@ class Trainer:
         for p in self.programs():
             p.bn_sync, p.bn_world = sync, world
         self.sync_bn = True
+        self.sync_bn_capturable = nccl
 
     def programs(self):
         return [p for p in (getattr(self, "prog", None), getattr(self, "single", None), getattr(self, "pair", None))
@@ -464,8 +473,9 @@ class Trainer:
             return self._capture(warmup, **kw)
 
     def _capture(self, warmup=2):
-        if getattr(self, "sync_bn", False):
-            raise NotImplementedError("SyncBN all-reduces inside the forward/backward: run step() eagerly")
+        if getattr(self, "sync_bn", False) and not getattr(self, "sync_bn_capturable", False):
+            raise NotImplementedError("SyncBN over gloo all-reduces on the host inside forward/backward: run step() "
+                                      "eagerly")
         s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
