@@ -1,5 +1,5 @@
 """Head-kernel micro-benchmark (diagnostic): us per tde_head_fwd / tde_head_bwd call at the reference nets'
-high-resolution head shapes.   python scripts/head_micro.py   (TDE_HEAD_TILE=0/1 selects the path)"""
+high-resolution head shapes.   python scripts/head_micro.py   (TDE_HEAD_TILE=0/1, TDE_HEAD_RW=0/1 select the path)"""
 import ctypes
 import os
 import sys
@@ -13,6 +13,7 @@ L = _lib
 lib = L.load()
 st = L.stream_ptr()
 SHAPES = [  # name, N, H, W, C, K, k
+    ("disp1_b16", 16, 192, 256, 16, 1, 3), ("disp2_b16", 16, 96, 128, 32, 1, 3), ("disp3_b16", 16, 48, 64, 64, 1, 3),
     ("disp1", 8, 192, 256, 16, 1, 3), ("disp2", 8, 96, 128, 32, 1, 3), ("mask1", 8, 192, 256, 16, 2, 7),
     ("mask2", 8, 96, 128, 32, 2, 5), ("flow1", 32, 192, 256, 16, 2, 3), ("c5disp1", 2, 480, 640, 16, 1, 3)]
 

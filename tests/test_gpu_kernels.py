@@ -540,6 +540,9 @@ HEAD_CASES = [
     (2, 150, 130, 32, 2, 5, 0, 1.0, 0.0, 32, 0),     # ragged rows and columns, 2 channel groups (dgrad)
     (1, 190, 200, 64, 1, 3, 1, 10.0, 0.001, 68, 4),  # 4 channel groups, offset view, ragged
     (2, 130, 160, 32, 1, 3, 0, 1.0, 0.0, 32, 0),     # disp2-like
+    # 3x3, K <= 2, w_cin == C, >= 32768 pixels: the row-walk kernels (head_rw_*; the cases above with C 16/32/64 too)
+    (3, 96, 128, 32, 2, 3, 1, 4.0, 0.0, 36, 4),      # two outputs, sigmoid, offset view
+    (2, 192, 100, 16, 1, 3, 1, 4.0, 0.0, 16, 0),     # ragged last segment (100 = 6 x 16 + 4)
     # 3-channel LINEAR disparity heads of nets.disp_net (nets.py:122-144: activation_fn=None, no BN, no scaling)
     (2, 24, 32, 128, 3, 3, 0, 1.0, 0.0, 128, 0),     # disp4 at 96x128 input
     (2, 48, 64, 64, 3, 3, 0, 1.0, 0.0, 64, 0),       # disp3

@@ -44,7 +44,8 @@ constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 // output pixel (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes.
 constexpr int MODE_PS = 3;
 // TDE_DBG_PHASE (timing-diagnostic BUILDS only, -DTDE_DBG_PHASE=..., wrong results; never a runtime switch), a
-// bit mask: 1 no k-loop global loads, 2 no MFMAs, 4 no staging (split + LDS stores).  (Round 3's row-of-4 WGRAD
+// bit mask: 1 no k-loop global loads, 2 no MFMAs, 4 no staging (split + LDS stores), 8 no B-operand loads or
+// staging (its fragments read whatever LDS holds), 16 the same for the A operand.  (Round 3's row-of-4 WGRAD
 // decode, XCD-grouped WGRAD order, write-through epilogue stores and software-pipelined two-tile k-loop were
 // measured neutral and removed in round 4: DESIGN.md section 6.)
 #ifndef TDE_DBG_PHASE
@@ -402,6 +403,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       // weight offset of this thread's (tap, co) shared by all its B slots (which differ in ci only)
       dg_wtap = ((g.khs + p.S * t_h) * p.KW + g.kws + p.S * t_w) * p.wcin * p.K + kx;
     }
+#if !(TDE_DBG_PHASE & 16)
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       if constexpr (FWDLIKE) {
@@ -428,6 +430,10 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         }
       }
     }
+#endif
+#if TDE_DBG_PHASE & 8
+    if (true) return;
+#endif
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int s = tid + i * NT;
@@ -479,6 +485,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #endif
     ET* A = As0 + buf * IA::SIZE;
     ET* Bm = Bs0 + buf * IB::SIZE;
+#if !(TDE_DBG_PHASE & 16)
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int s = tid + i * NT;
@@ -492,6 +499,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         putA(A, s >> 3, 4 * (s & 7), ra[i][0]);
       }
     }
+#endif
+#if !(TDE_DBG_PHASE & 8)
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int s = tid + i * NT;
@@ -505,6 +514,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         putB(Bm, s >> 3, 4 * (s & 7), rb[i][0]);
       }
     }
+#endif
   };
 
   f4 acc[TM][TN];

@@ -701,6 +701,276 @@ __global__ void __launch_bounds__(64) head_wgrad_reduce_t_kernel(const float* pa
   }
 }
 
+// ------------------------------------------------------------------ row-walk 3x3 heads (round 4)
+// The disparity heads (nets_optflow_depth.py:122-144: 3x3, stride 1, one output; the masks' 3x3 level too) at the
+// high resolutions are pure streams -- ~9 FMAs per input byte -- and the halo-tiled kernels above ran them at a
+// quarter to a sixth of the HBM rate (rocprofv3, config 4: disp fwd 23 us, wgrad 31 us per call against ~8 us of
+// reads for disp1).  Here no LDS staging and no barrier in the loop: thread = (channel quad q, 16-pixel segment of
+// one row); it walks its segment with a 3 x 3 window of f4 in registers, loading one new input column (3 f4) per
+// pixel (unrolled by 4: 12 loads in flight), weights in registers.  The CQ = C/4 lanes of a pixel are adjacent, so a
+// pixel's channels are one contiguous read and its quads combine by xor shuffles.  Rows r-1..r+1 of one image are
+// walked by neighbouring threads of the same block (their reads meet in L1/L2): x leaves HBM about once.
+constexpr int RW_SEG = 16;    // output pixels per thread
+
+struct RwGeom {
+  int CQ, segs, rows;   // lanes per pixel, segments per row, N * OH rows
+};
+__device__ __forceinline__ void rw_decode(const HeadArgs& p, int CQ, int segs, long t, int& q, int& x0, int& n,
+                                          int& r) {
+  q = (int)(t % CQ);
+  const long u = t / CQ;
+  x0 = (int)(u % segs) * RW_SEG;
+  const long rr = u / segs;
+  n = (int)(rr / p.OH);
+  r = (int)(rr - (long)n * p.OH);
+}
+
+// x quad at (n, ih, iw) or 0 outside the image (buffer load: branch-free)
+__device__ __forceinline__ f4 rw_x(const HeadArgs& p, __amdgpu_buffer_rsrc_t rx, int n, int ih, int iw, int q) {
+  const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+  return bload(rx, ok ? 4 * (((n * p.H + ih) * p.W + iw) * p.xcs + p.xco + 4 * q) : OOB);
+}
+
+template <int KC>
+__global__ void __launch_bounds__(256) head_rw_fwd_kernel(const HeadArgs p, int CQ, int segs, long threads) {
+  const long t = blockIdx.x * 256L + threadIdx.x;
+  int q, x0, n, r;
+  rw_decode(p, CQ, segs, t < threads ? t : 0, q, x0, n, r);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  float w[9][4][KC];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) w[tap][j][k] = p.w[(tap * p.wcin + 4 * q + j) * KC + k];
+  // window columns x0-1, x0 (rows r-1 .. r+1); column x0+1+i is loaded at step i
+  f4 win[3][3];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    win[kh][0] = rw_x(p, rx, n, r + kh - 1, x0 - 1, q);
+    win[kh][1] = rw_x(p, rx, n, r + kh - 1, x0, q);
+  }
+  const int lanebase = (int)(threadIdx.x & 63) & ~(CQ - 1);
+  for (int i0 = 0; i0 < RW_SEG; i0 += 4) {
+    f4 col[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) col[u][kh] = rw_x(p, rx, n, r + kh - 1, x0 + i0 + u + 1, q);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) win[kh][2] = col[u][kh];
+      float acc[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < KC; ++k) acc[k] = fmaf(win[kh][kw][j], w[kh * 3 + kw][j][k], acc[k]);
+      // the CQ quads of this pixel: xor tree over the adjacent lanes (fixed order)
+      for (int o = 1; o < CQ; o <<= 1)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+      const int ow = x0 + i0 + u;
+      if (q == 0 && t < threads && ow < p.OW) {
+        float* yp = p.y + ((long)(n * p.OH + r) * p.OW + ow) * p.ycs + p.yco;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) yp[k] = head_act(acc[k] + p.b[k], p.act, p.scale, p.offset);
+      }
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) { win[kh][0] = win[kh][1]; win[kh][1] = win[kh][2]; }
+    }
+  }
+  (void)lanebase;
+}
+
+// dz (dL / d pre-activation) at output pixel (n, oh, ow), zero outside the image
+template <int KC>
+__device__ __forceinline__ void rw_dz(const HeadArgs& p, int n, int oh, int ow, float (&d)[KC]) {
+  dz_at<KC>(p, n, oh, ow, d);
+}
+
+// Filter gradient partials: per block, dW[tap][c][k] (+ the bias sums) over its threads' pixels, written
+// transposed part[output][block] for head_wgrad_reduce_t_kernel (fixed-order fp64 sums over blocks).
+template <int KC>
+__global__ void __launch_bounds__(256) head_rw_wgrad_kernel(const HeadArgs p, int CQ, int segs, long threads,
+                                                            float* part) {
+  constexpr int NA = 9 * 4 * KC;
+  __shared__ float red[4 * 16 * (NA + KC)];
+  const long t = blockIdx.x * 256L + threadIdx.x;
+  int q, x0, n, r;
+  rw_decode(p, CQ, segs, t < threads ? t : 0, q, x0, n, r);
+  const bool live = t < threads;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  float acc[9][4][KC], bacc[KC];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) acc[tap][j][k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) bacc[k] = 0.f;
+  f4 win[3][3];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    win[kh][0] = rw_x(p, rx, n, r + kh - 1, x0 - 1, q);
+    win[kh][1] = rw_x(p, rx, n, r + kh - 1, x0, q);
+  }
+  for (int i0 = 0; i0 < RW_SEG; i0 += 4) {
+    f4 col[4][3];
+    float d[4][KC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) col[u][kh] = rw_x(p, rx, n, r + kh - 1, x0 + i0 + u + 1, q);
+      const int ow = x0 + i0 + u;
+      rw_dz<KC>(p, n, live ? r : p.OH, ow, d[u]);          // outside the image (or a dead thread): 0
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) win[kh][2] = col[u][kh];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < KC; ++k) acc[kh * 3 + kw][j][k] = fmaf(win[kh][kw][j], d[u][k], acc[kh * 3 + kw][j][k]);
+#pragma unroll
+      for (int k = 0; k < KC; ++k) bacc[k] += d[u][k];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) { win[kh][0] = win[kh][1]; win[kh][1] = win[kh][2]; }
+    }
+  }
+  // block combine (fixed order): xor tree over the lanes of a wave that hold the same quad (lane bits >= log2 CQ),
+  // then the 4 waves' sums through LDS in wave order
+  for (int o = CQ; o < 64; o <<= 1) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) acc[tap][j][k] += __shfl_xor(acc[tap][j][k], o, 64);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) bacc[k] += __shfl_xor(bacc[k], o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < CQ) {
+    float* mine = red + (wv * 16 + lane) * (NA + KC);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) mine[(tap * 4 + j) * KC + k] = acc[tap][j][k];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) mine[NA + k] = bacc[k];     // (every quad lane summed the same dz: quad 0's is used)
+  }
+  __syncthreads();
+  const int E = 9 * p.wcin;
+  const long R = gridDim.x;
+  const int nout = E * KC + KC;
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    int qq = 0, slot;
+    if (o < E * KC) {
+      const int k = o % KC, e = o / KC, tap = e / p.wcin, c = e - tap * p.wcin;
+      qq = c >> 2;
+      slot = (tap * 4 + (c & 3)) * KC + k;
+    } else {
+      slot = NA + (o - E * KC);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += red[(w * 16 + qq) * (NA + KC) + slot];
+    part[(long)o * R + blockIdx.x] = s;
+  }
+}
+
+// Data gradient: thread = (channel quad, 16-pixel segment of one input row); a 3 x 3 window of dz (KC floats each,
+// recomputed from y, dy) slides along the row, weights in registers.
+template <int KC>
+__global__ void __launch_bounds__(256) head_rw_dgrad_kernel(const HeadArgs p, int CQ, int segs, long threads) {
+  const long t = blockIdx.x * 256L + threadIdx.x;
+  if (t >= threads) return;
+  int q, x0, n, r;
+  rw_decode(p, CQ, segs, t, q, x0, n, r);     // (input pixels: H = OH, W = OW for the stride-1 SAME heads)
+  float w[9][4][KC];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < KC; ++k) w[tap][j][k] = p.w[(tap * p.wcin + 4 * q + j) * KC + k];
+  // dz window: rows r+1, r, r-1 (tap kh = 0, 1, 2 reads output row r + 1 - kh), columns iw+1, iw, iw-1
+  float dw_[3][3][KC];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    rw_dz<KC>(p, n, r + 1 - kh, x0 - 1, dw_[kh][0]);
+    rw_dz<KC>(p, n, r + 1 - kh, x0, dw_[kh][1]);
+  }
+  for (int i0 = 0; i0 < RW_SEG; i0 += 4) {
+    float nd[4][3][KC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) rw_dz<KC>(p, n, r + 1 - kh, x0 + i0 + u + 1, nd[u][kh]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) dw_[kh][2][k] = nd[u][kh][k];
+      // dx[iw] = sum_{kh,kw} dz[r + 1 - kh][iw + 1 - kw] w[kh][kw]: column iw + 1 - kw is window slot 2 - kw
+      f4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int k = 0; k < KC; ++k) {
+            const float dv = dw_[kh][2 - kw][k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = fmaf(dv, w[kh * 3 + kw][j][k], o[j]);
+          }
+      const int iw = x0 + i0 + u;
+      if (iw < p.W) {
+        float* dst = p.dx + ((long)(n * p.H + r) * p.W + iw) * p.xcs + p.xco + 4 * q;
+        if (p.acc_dx) o += *reinterpret_cast<const f4*>(dst);
+        *reinterpret_cast<f4*>(dst) = o;
+      }
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int k = 0; k < KC; ++k) { dw_[kh][0][k] = dw_[kh][1][k]; dw_[kh][1][k] = dw_[kh][2][k]; }
+    }
+  }
+}
+
+// Measured per call (scripts/head_micro.py, r04k, us): forward disp1 / disp2 / disp3 at twin batch 16 19.6 / 14.3 /
+// 12.1 against 30.5 / 15.3 / 17.6 halo-tiled; filter gradient (with its reduce) 31 / 19 / 16 against 39 / 33 / 25;
+// equal at batch 8.
+// row-walk path: 3x3, stride 1, SAME, K <= 2, every channel a weight row (w_cin == C), C / 4 lanes per pixel a power
+// of two <= 16 (C = 16 / 32 / 64), at least TDE_HEAD_TILE_MIN pixels; TDE_HEAD_RW=0 keeps the halo-tiled kernels
+static const bool g_head_rw_on = !(std::getenv("TDE_HEAD_RW") && std::atol(std::getenv("TDE_HEAD_RW")) == 0);
+bool head_rw(const tde_conv_desc_t* d) {
+  const int cq = d->C / 4;
+  return g_head_rw_on && d->stride == 1 && d->KH == 3 && d->KW == 3 && d->pad_top == 1 && d->pad_left == 1 &&
+         (d->K == 1 || d->K == 2) && d->w_cin == d->C && (cq == 4 || cq == 8 || cq == 16) && d->OH == d->H &&
+         d->OW == d->W && (long)d->N * d->H * d->W >= 32768;
+}
+long rw_threads(const tde_conv_desc_t* d) {
+  return (long)d->N * d->OH * ((d->OW + RW_SEG - 1) / RW_SEG) * (d->C / 4);
+}
+
 struct WgPlan {
   int chunks, ppc, tgroups;
 };
@@ -890,7 +1160,8 @@ extern "C" {
 size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   if (!head_desc_ok(d)) return 0;
   const WgPlan w = wg_plan(d);
-  const long rows = head_tiled(d) ? head_tiles(d, HT_TWG_TH) : w.chunks;
+  long rows = head_tiled(d) ? head_tiles(d, HT_TWG_TH) : w.chunks;
+  if (head_rw(d)) rows = (rw_threads(d) + 255) / 256;
   const size_t part = (size_t)rows * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
   return dz_bytes(d) + part;
 }
@@ -902,6 +1173,15 @@ int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   a.x = x; a.w = w; a.b = bias; a.y = y; a.act = act; a.scale = scale; a.offset = offset;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const long M = (long)d->N * d->OH * d->OW;
+  if (head_rw(d)) {
+    const long th = rw_threads(d);
+    const int segs = (d->OW + RW_SEG - 1) / RW_SEG;
+    if (d->K == 1)
+      hipLaunchKernelGGL(head_rw_fwd_kernel<1>, dim3((th + 255) / 256), dim3(256), 0, st, a, d->C / 4, segs, th);
+    else
+      hipLaunchKernelGGL(head_rw_fwd_kernel<2>, dim3((th + 255) / 256), dim3(256), 0, st, a, d->C / 4, segs, th);
+    return tde_launch_status();
+  }
   if (head_tiled(d)) {
     launch_tiled(d, a, 0, nullptr, st);
     return tde_launch_status();
@@ -934,6 +1214,30 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
   a.dzw = dz;
   TDE_CHECK_ARG(!dx || tde_aligned16(dx));
   TDE_CHECK_ARG(!dw || dbias != nullptr);
+  if (head_rw(d)) {
+    // dz recomputed from (y, dy) where each kernel needs it: no dz pass
+    const long th = rw_threads(d);
+    const int segs = (d->OW + RW_SEG - 1) / RW_SEG, CQ = d->C / 4;
+    const int rows = (int)((th + 255) / 256);
+    const int total = 9 * d->w_cin * d->K + d->K;
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
+    if (dw) {
+      if (d->K == 1) hipLaunchKernelGGL(head_rw_wgrad_kernel<1>, dim3(rows), dim3(256), 0, st, a, CQ, segs, th, part);
+      else hipLaunchKernelGGL(head_rw_wgrad_kernel<2>, dim3(rows), dim3(256), 0, st, a, CQ, segs, th, part);
+    }
+    if (dx) {
+      // the data gradient stays on the halo-tiled kernel where it applies: its dz halo is computed once per tile, while
+      // every quad lane of the row walk recomputes its dz window (measured, scripts/head_micro.py r04k: disp2 / disp3
+      // dgrad 15.2 / 9.8 us tiled vs 17.8 / 14.5 us row-walk at batch 16; flow1 47.8 vs 78.5 us)
+      if (head_tiled(d)) launch_tiled(d, a, 1, nullptr, st);
+      else if (d->K == 1) hipLaunchKernelGGL(head_rw_dgrad_kernel<1>, dim3(rows), dim3(256), 0, st, a, CQ, segs, th);
+      else hipLaunchKernelGGL(head_rw_dgrad_kernel<2>, dim3(rows), dim3(256), 0, st, a, CQ, segs, th);
+    }
+    if (dw)
+      hipLaunchKernelGGL(head_wgrad_reduce_t_kernel, dim3(total), dim3(64), 0, st, part, rows, 9 * d->w_cin * d->K, dw,
+                         dbias, accumulate_dw);
+    return tde_launch_status();
+  }
   if (head_tiled(d)) {
     // dz recomputed from (y, dy) at each kernel's staging: no dz pass
     const int E = d->KH * d->KW * d->w_cin;
