@@ -295,7 +295,12 @@ def build_trainer(args, name, N, world, rank):
         tr.enable_deferred_adam()
     if net_overlap:
         tr.enable_net_overlap()
-    return tr, dict(deferred=deferred, net_overlap=net_overlap, wgrad_progs=wg_progs)
+    branch = (getattr(args, "branch_overlap", "on") == "on" and world == 1 and args.adam_overlap == "off" and
+              not deferred and not args.sync_bn)
+    if branch:
+        tr.enable_branch_overlap()
+    branch = branch and tr._branch_on()
+    return tr, dict(deferred=deferred, net_overlap=net_overlap, wgrad_progs=wg_progs, branch_overlap=branch)
 
 
 def instrumented_step(tr):
@@ -434,6 +439,9 @@ def main():
                     help="config 4: depth_net's calls on a second stream beside disp_net's (independent "
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
                          "Measured config 4 605 -> 665 samples/s")
+    ap.add_argument("--branch-overlap", default="on", choices=["on", "off"],
+                    help="N = 1: depth_net's pose and explainability-mask branches on a stream of their own beside the "
+                         "decoder, forward and backward (bit-identical to the same calls on one stream)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce of every row group's sums per BN layer "
                          "and direction, on a communicator of its own, captured into the step's graphs)")
@@ -521,7 +529,7 @@ def main():
                        "wgrad_overlap": args.wgrad_overlap == "on", "wgrad_progs": opts.get("wgrad_progs"),
                        "adam_overlap": args.adam_overlap if world == 1 else "off",
                        "deferred_adam": opts["deferred"],
-                       "net_overlap": opts["net_overlap"],
+                       "net_overlap": opts["net_overlap"], "branch_overlap": opts.get("branch_overlap", False),
                        "unit_note": "1 unit = 1 training sample: an image pair (configs 3/4); configs 2/5 train on "
                                     "one image of it"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,

@@ -146,7 +146,9 @@ def depth_net_spec(H, W, cin, levels=4, scope="depth_cam_net", decay=None, scale
     spec = NetSpec(scope, H, W, cin)
     dec = Decoder(spec, hs, ws, "", 1, levels)
     feats = build_encoder(spec, dec.skip_slots(levels), decay)
-    # pose head (:178-186)
+    # pose head (:178-186) and explainability-mask branch (:189-206): side branches off the encoder that feed only
+    # the loss (NetProgram.enable_branch_overlap runs them on a stream of their own)
+    first_branch = len(spec.ops)
     cam = spec.dense("pose/cam_cnv7", hs[7], ws[7], 256)
     spec.add(ConvBN("pose/cam_cnv7", feats["cnv6b"], cam, 256, 3, 2, decay=decay))
     pose = spec.dense("pose/pred", hs[7], ws[7], 6)
@@ -173,6 +175,8 @@ def depth_net_spec(H, W, cin, levels=4, scope="depth_cam_net", decay=None, scale
         m1 = spec.dense("exp/mask1", e1.H, e1.W, 2)
         spec.add(Head("exp/mask1", e1, m1, 2, 7, 0))
         masks = [m1, m2, m3, m4]
+    for op in spec.ops[first_branch:]:
+        op.branch = 1
     cnv7 = spec.dense("cnv7", hs[7], ws[7], 512)
     spec.add(ConvBN("cnv7", feats["cnv6b"], cnv7, 512, 3, 2, decay=decay))
     cnv7b = spec.dense("cnv7b", hs[7], ws[7], 512)

@@ -74,6 +74,7 @@ class View:
 
 class Op:
     params = ()
+    branch = 0      # 1: a side branch of the network (NetProgram.enable_branch_overlap)
 
 
 class ConvBN(Op):
@@ -553,10 +554,42 @@ class NetProgram:
         w = self._ws.setdefault(N, Workspace())
         return w.get(ws, dz, "cuda")
 
+    # ---------------------------------------------------------------- branch overlap
+    def enable_branch_overlap(self, on=True, serial=False):
+        """Run the spec's side branches (ops with `branch == 1`: depth_net's pose and explainability-mask heads,
+        nets_optflow_depth_pairtest.py:178-206, which read encoder features and feed only the loss) on a stream of
+        their own, beside the decoder, in forward and backward.  Their ops use their own workspace, their own dz
+        buffers and the split filter / data-gradient calls (no filter-gradient side stream: every fork of a
+        captured step stays one level deep).  A branch op's data gradient into an encoder feature's gradient (the
+        one write the branch shares with the main chain) is ordered after the main chain's earlier writes to that
+        buffer and before its later ones (events), so every buffer sees the serial order of writes: results equal
+        serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
+        has = any(getattr(op, "branch", 0) for op in self.spec.ops)
+        self.branch_stream = None
+        if on and has:
+            self.branch_stream = SERIAL if serial else _lib.owned_stream(self, "branch")
+        self._branch_bufs = {op.dst.buf.name for op in self.spec.ops if getattr(op, "branch", 0)}
+        return self
+
+    def _branch_mode(self):
+        """The branch stream (or SERIAL) when the branch overlap applies to this call: not with SyncBN and not under
+        the instrumented eager step (its HIP-event timer records on one stream)."""
+        bs = getattr(self, "branch_stream", None)
+        if bs is None or self.bn_sync is not None or not self._production():
+            return None
+        return bs
+
     # ---------------------------------------------------------------- forward
     def forward(self, run, x, is_training=True, fold_bn=False):
         """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors.  fold_bn (inference only):
         run each conv/deconv + BN + ReLU as ONE bias+ReLU conv on the weights of fold_bn()."""
+        main = torch.cuda.current_stream()
+        try:
+            return self._forward(run, x, is_training, fold_bn)
+        finally:
+            torch.cuda.set_stream(main)
+
+    def _forward(self, run, x, is_training, fold_bn):
         if fold_bn and (is_training or self._folded is None):
             raise ValueError("fold_bn needs is_training=False and weights folded by fold_bn()")
         N = run.N
@@ -579,7 +612,24 @@ class NetProgram:
             self._cur_split = (key, {})
             for job in plan:
                 split_todo.setdefault(job[0], []).append(job)
+        main = torch.cuda.current_stream()
+        bmode = self._branch_mode() if is_training and not fold_bn else None
+        ws_a, wsb_a = ws, wsb
+        forked = False
         for i, op in enumerate(spec.ops):
+            br = bmode is not None and getattr(op, "branch", 0) == 1
+            if br and bmode is not SERIAL:
+                if not forked:
+                    # the branches read encoder features only, all issued by now
+                    _lib.wait_stream(bmode, main)
+                    forked = True
+                torch.cuda.set_stream(bmode)
+                ws = self._scratch_side(N, "branch")
+                wsb = ws.numel() * 4
+            else:
+                torch.cuda.set_stream(main)
+                ws, wsb = ws_a, wsb_a
+            st = _lib.stream_ptr()
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             if self.pre_op is not None and isinstance(op, (ConvBN, Head)):
@@ -587,8 +637,11 @@ class NetProgram:
             if isinstance(op, ConvBN):
                 if i in split_todo:
                     # one split launch for every pending layer whose weights are final by now (all of them
-                    # unless an optimizer step is still running on a side stream)
-                    ready = [j for j in split_todo if self.params_ready is None or self.params_ready(self, j)]
+                    # unless an optimizer step is still running on a side stream); a branch op splits only its own
+                    # (main-chain ops read theirs on the other stream)
+                    ready = ([i] if br else
+                             [j for j in split_todo if (self.params_ready is None or self.params_ready(self, j)) and
+                              not (forked and getattr(spec.ops[j], "branch", 0))])
                     self._issue_split([job for j in ready for job in split_todo.pop(j)])
                 d = op.desc(N)
                 if not fold_bn:
@@ -682,6 +735,9 @@ class NetProgram:
                 s, t = op.src, op.dst
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(s), s.buf.cs, s.coff, run.vptr(t),
                                              t.buf.cs, t.coff, 0, st), "copy")
+        torch.cuda.set_stream(main)
+        if forked:
+            _lib.wait_stream(main, bmode)
         return [run.view_tensor(v) for v in spec.outputs]
 
     # ---------------------------------------------------------------- backward
@@ -692,6 +748,13 @@ class NetProgram:
         and the kernels skip the read-modify-write).  Returns d(input) if requested.  on_grads(names),
         if given, is called after each op with the full variable names whose gradient that op just
         wrote (the data-parallel exchange launches a bucket once all its parameters are final, ddp.py)."""
+        main = torch.cuda.current_stream()
+        try:
+            return self._backward(run, grad_outputs, need_input_grad, on_grads, grad_accumulate)
+        finally:
+            torch.cuda.set_stream(main)
+
+    def _backward(self, run, grad_outputs, need_input_grad, on_grads, grad_accumulate):
         pacc = 1 if grad_accumulate else 0
         N = run.N
         if self.pre_backward is not None:
@@ -738,13 +801,46 @@ class NetProgram:
         for j, o in enumerate(spec.ops):
             if isinstance(o, ConvBN):
                 conv_rank[j] = len(conv_rank)
+        # branch overlap (enable_branch_overlap): the side branches' ops on their stream from the start of backward
+        # (their output gradients come from the loss); pend: gradient buffer -> event after a branch op's write into
+        # it that the main chain also writes or reads later
+        main = torch.cuda.current_stream()
+        bmode = self._branch_mode()
+        ws_a, wsb_a, dz_a = ws, wsb, dz
+        e0 = None
+        if bmode is not None and bmode is not SERIAL:
+            e0 = torch.cuda.Event()
+            e0.record(main)
+        b_started = False
+        pend = {}
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
+            br = bmode is not None and getattr(op, "branch", 0) == 1
+            real_br = br and bmode is not SERIAL
+            if real_br:
+                if not b_started:
+                    _lib.wait_event(bmode, e0)
+                    b_started = True
+                torch.cuda.set_stream(bmode)
+                ws = self._scratch_side(N, "branch")
+                wsb = ws.numel() * 4
+            else:
+                torch.cuda.set_stream(main)
+                ws, wsb, dz = ws_a, wsb_a, dz_a
+                for name in {op.dst.buf.name, op.src.buf.name} if pend else ():
+                    ev = pend.pop(name, None)
+                    if ev is not None:
+                        _lib.wait_event(main, ev)
+            st = _lib.stream_ptr()
+            # a branch op whose input is a main-chain buffer (an encoder feature): its data gradient is the shared write
+            shared = br and op.src.buf.name not in self._branch_bufs
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
+            if br and not isinstance(op, ConvBN):
+                assert not shared, f"{type(op).__name__} in a branch writes a main-chain gradient"
             if isinstance(op, ConvBN):
-                use_side = (side is not None and conv_rank[i] >= self.wgrad_tail and
+                use_side = (side is not None and not br and conv_rank[i] >= self.wgrad_tail and
                             N * op.dst.H * op.dst.W > self.wgrad_inline_m)
                 d = op.desc(N)
                 self._use_split(d, i, N)
@@ -755,7 +851,7 @@ class NetProgram:
                     d.y_absmax = run.absmax_ptr(i)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats.get(i)
-                if side is not None:
+                if side is not None or br:
                     dz = self._dz_layer(N, i, M * op.K)
                 if not op.bn:
                     # BN-free layer: dz = dy * relu'(y), bias gradient (fixed-order fp64 sums)
@@ -800,7 +896,28 @@ class NetProgram:
                                                   run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
-                if use_side:
+                if br:
+                    # branch op: filter gradient, then data gradient, as two calls on the branch stream; a data
+                    # gradient into a main-chain buffer waits for the main chain's writes issued before it
+                    wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
+                    a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
+                    with self._span("conv_wgrad", fl, conv_bytes(op, N)):
+                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
+                    if src_needs:
+                        if shared and real_br:
+                            ev = torch.cuda.Event()
+                            ev.record(main)
+                            _lib.wait_event(bmode, ev)
+                        acc = mark(op.src)
+                        fd = lib.tde_deconv2d_bwd_data if op.deconv else lib.tde_conv2d_bwd_data
+                        with self._span("conv_dgrad", fl, conv_bytes(op, N)):
+                            _lib.check(fd(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True), acc, ptr(ws), wsb,
+                                          st), op.layer + " bwd data")
+                        if shared and real_br:
+                            ev = torch.cuda.Event()
+                            ev.record(bmode)
+                            pend[op.src.buf.name] = ev
+                elif use_side:
                     # this layer's filter gradient joins the deferred group; the group goes to the side stream
                     # behind one event recorded after the BN backward that completes it.  The data gradient is
                     # issued BEFORE the side stream waits on that event: under capture the graph executor keeps
@@ -863,7 +980,7 @@ class NetProgram:
                 acc = mark(op.src) if src_needs else 0
                 hw, hgw, hgb = (ptr(self.P(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/weights")),
                                 ptr(self.G(f"{op.layer}/biases")))
-                if side is not None and self.head_wgrad_side:
+                if side is not None and self.head_wgrad_side and not br:
                     # the head's filter gradient joins the deferred group on the side stream (it reads x, y and
                     # dy, none of which the rest of backward rewrites); the data gradient stays on this stream
                     def head_wgrad_call(wsp, wsb2, d=d, x=run.vptr(op.src), y=run.vptr(op.dst),
@@ -907,6 +1024,11 @@ class NetProgram:
                 acc = mark(s)
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
+        torch.cuda.set_stream(main)
+        for ev in pend.values():
+            _lib.wait_event(main, ev)
+        if b_started:
+            _lib.wait_stream(main, bmode)
         if side is not None:
             self._flush_wgrad()
             names, self._wg_issued = self._wg_issued, []

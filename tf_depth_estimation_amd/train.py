@@ -303,8 +303,8 @@ class Trainer:
     def enable_deferred_adam(self, first_mb=2.0):
         """Run each step's Adam at the start of the next step, overlapped with its forward (DeferredAdam).
         The parameters then lag the gradients by one update until flush()."""
-        if self.grad_sync is not None or self.adam_ov is not None:
-            raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap")
+        if self.grad_sync is not None or self.adam_ov is not None or self._branch_on():
+            raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap or branch overlap")
         if self.net_stream is not None:
             # the overlapped capture has no _begin() piece: a deferred update would never be launched
             raise ValueError("deferred Adam and net overlap are exclusive")
@@ -331,8 +331,9 @@ class Trainer:
         with a data-parallel exchange the update must wait for the all-reduce).  on_wgrad_stream: on each
         program's filter-gradient stream (enable_wgrad_overlap first), behind the filter gradients it holds,
         so the compute stream never waits for it until the end of the step."""
-        if self.grad_sync is not None:
-            raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
+        if self.grad_sync is not None or self._branch_on():
+            raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it) without "
+                             "branch overlap")
         if self.net_stream is not None:
             raise ValueError("Adam overlap and net overlap are exclusive")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
@@ -362,6 +363,20 @@ class Trainer:
                 continue
             p.enable_wgrad_overlap(on and (only is None or name in only), serial)
         return self
+
+    def enable_branch_overlap(self, on=True, serial=False):
+        """The networks' side branches (depth_net's pose and explainability-mask heads) on a stream of their own,
+        beside the decoder, forward and backward (NetProgram.enable_branch_overlap; serial=True: the same calls on
+        one stream, the bit-exact reference).  Single-GPU step without Adam overlap / deferred Adam: a bucket launch
+        point of the exchange must not cut a graph while a branch is forked."""
+        if on and (self.grad_sync is not None or self.adam_ov is not None or self.dadam is not None):
+            raise ValueError("branch overlap is for the single-GPU step without Adam overlap / deferred Adam")
+        for p in self.programs():
+            p.enable_branch_overlap(on, serial)
+        return self
+
+    def _branch_on(self):
+        return any(getattr(p, "branch_stream", None) is not None for p in self.programs())
 
     def join_wgrad(self):
         for p in self.programs():
@@ -408,8 +423,8 @@ class Trainer:
 
     def enable_ddp(self, world, bucket_mb=32.0, group=None):
         from .ddp import GradSync
-        if self.adam_ov is not None:
-            raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
+        if self.adam_ov is not None or self._branch_on():
+            raise ValueError("Adam overlap / branch overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
                                   pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams)
