@@ -295,8 +295,8 @@ def build_trainer(args, name, N, world, rank):
         tr.enable_deferred_adam()
     if net_overlap:
         tr.enable_net_overlap()
-    branch = (getattr(args, "branch_overlap", "on") == "on" and world == 1 and args.adam_overlap == "off" and
-              not deferred and not args.sync_bn)
+    branch = (getattr(args, "branch_overlap", "on") == "on" and args.adam_overlap == "off" and not deferred and
+              not args.sync_bn)
     if branch:
         tr.enable_branch_overlap()
     branch = branch and tr._branch_on()
@@ -440,8 +440,8 @@ def main():
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
                          "Measured config 4 605 -> 665 samples/s")
     ap.add_argument("--branch-overlap", default="on", choices=["on", "off"],
-                    help="N = 1: depth_net's pose and explainability-mask branches on a stream of their own beside the "
-                         "decoder, forward and backward (bit-identical to the same calls on one stream)")
+                    help="depth_net's pose and explainability-mask branches on a stream of their own beside the decoder, "
+                         "forward and backward (bit-identical to the same calls on one stream)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce of every row group's sums per BN layer "
                          "and direction, on a communicator of its own, captured into the step's graphs)")

@@ -106,7 +106,7 @@ def test_sync_bn_world1_step_parity(pg):
     _api.clear_programs()
 
 
-def _c4_trainer(ddp, graph, net_overlap, steps=2):
+def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
@@ -122,6 +122,8 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2):
         assert len(gs.buckets) > 4
     if net_overlap:
         tr.enable_net_overlap()
+    if branch:
+        tr.enable_branch_overlap(serial=branch == "serial")
     if graph:
         tr.capture(warmup=1)
         if ddp and net_overlap:
@@ -144,6 +146,19 @@ def test_config4_exchange_with_net_overlap(pg, graph):
     for a, b in zip(ref, _c4_trainer(True, graph, True)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
     for a, b in zip(ref, _c4_trainer(True, graph, False)):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_config4_exchange_with_branch_overlap(pg, graph):
+    """The benched config-4 schedule with depth_net's pose / mask branches on their own stream (enable_branch_overlap)
+    under the bucketed exchange: a branch's parameters are reported from the main stream, a bucket launch point joins
+    the branch before it cuts the graph, the comm stream waits on the branch's tail eagerly -- parameters, gradients
+    and moments equal the same branch schedule without an exchange, and its serial form, bit for bit."""
+    ref = _c4_trainer(False, graph, True, branch="serial")
+    for a, b in zip(ref, _c4_trainer(False, graph, True, branch=True)):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+    for a, b in zip(ref, _c4_trainer(True, graph, True, branch=True)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 

@@ -495,7 +495,7 @@ def test_branch_overlap_matches_serial(graph, combo):
         assert e <= 1e-4, f"branch vs plain schedule first-step gradient rel-L2 {e:.2e}"
 
 
-def test_branch_overlap_exclusive_with_exchange():
+def test_branch_overlap_exclusive_with_adam_overlaps():
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
     _api.clear_programs()

@@ -579,6 +579,22 @@ class NetProgram:
             return None
         return bs
 
+    def join_branch(self):
+        """Order the current (main) stream after everything the side-branch stream issued in this backward, if it
+        was forked: a graph segment must end with its forked branches joined (the exchange's launch points).  A
+        later branch op forks again from the main stream."""
+        bst = getattr(self, "_bst", None)
+        if bst is None or not bst["started"] or bst["refork"]:
+            return
+        _lib.wait_stream(torch.cuda.current_stream(), bst["stream"])
+        bst["pend"].clear()
+        bst["refork"] = True
+
+    def branch_streams(self):
+        """The side-branch stream while a backward has it forked (the exchange's comm stream waits on its tail)."""
+        bst = getattr(self, "_bst", None)
+        return (bst["stream"],) if bst is not None and bst["started"] and not bst["refork"] else ()
+
     # ---------------------------------------------------------------- forward
     def forward(self, run, x, is_training=True, fold_bn=False):
         """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors.  fold_bn (inference only):
@@ -807,30 +823,41 @@ class NetProgram:
         main = torch.cuda.current_stream()
         bmode = self._branch_mode()
         ws_a, wsb_a, dz_a = ws, wsb, dz
-        e0 = None
+        bst = self._bst = None
         if bmode is not None and bmode is not SERIAL:
+            # fork: the event the branch's first op waits on; pend: gradient buffer -> event after a branch op's
+            # write into it that the main chain also touches later; refork: join_branch() joined the branch
             e0 = torch.cuda.Event()
             e0.record(main)
-        b_started = False
-        pend = {}
+            bst = self._bst = dict(main=main, stream=bmode, fork=e0, started=False, pend={}, refork=False)
+        br_names = []     # parameters a branch op has written, reported (on_grads) from the main stream
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             br = bmode is not None and getattr(op, "branch", 0) == 1
             real_br = br and bmode is not SERIAL
             if real_br:
-                if not b_started:
-                    _lib.wait_event(bmode, e0)
-                    b_started = True
+                if not bst["started"] or bst["refork"]:
+                    if bst["refork"]:
+                        bst["fork"] = torch.cuda.Event()
+                        bst["fork"].record(main)
+                    _lib.wait_event(bmode, bst["fork"])
+                    bst["started"], bst["refork"] = True, False
                 torch.cuda.set_stream(bmode)
                 ws = self._scratch_side(N, "branch")
                 wsb = ws.numel() * 4
             else:
                 torch.cuda.set_stream(main)
                 ws, wsb, dz = ws_a, wsb_a, dz_a
+                pend = bst["pend"] if bst is not None else None
                 for name in {op.dst.buf.name, op.src.buf.name} if pend else ():
                     ev = pend.pop(name, None)
                     if ev is not None:
                         _lib.wait_event(main, ev)
+                if br_names and on_grads is not None:
+                    # the branch's finished parameters, reported from the main stream: the exchange's launch point
+                    # (a graph cut under capture) joins the branch first (Trainer._join_chunk_wgrad -> join_branch)
+                    names, br_names = br_names, []
+                    on_grads(names)
             st = _lib.stream_ptr()
             # a branch op whose input is a main-chain buffer (an encoder feature): its data gradient is the shared write
             shared = br and op.src.buf.name not in self._branch_bufs
@@ -916,7 +943,7 @@ class NetProgram:
                         if shared and real_br:
                             ev = torch.cuda.Event()
                             ev.record(bmode)
-                            pend[op.src.buf.name] = ev
+                            bst["pend"][op.src.buf.name] = ev
                 elif use_side:
                     # this layer's filter gradient joins the deferred group; the group goes to the side stream
                     # behind one event recorded after the BN backward that completes it.  The data gradient is
@@ -965,7 +992,9 @@ class NetProgram:
                     a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
                     with self._span("conv_wgrad", fl, conv_bytes(op, N)):
                         _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
-                if side is not None:
+                if br:
+                    br_names += [f"{self.prefix}/{n}" for n, _, _ in op.params]
+                elif side is not None:
                     # report the parameters of the filter gradients issued so far (a deferred one is reported
                     # once its group is on the side stream)
                     names, self._wg_issued = self._wg_issued, []
@@ -1010,7 +1039,9 @@ class NetProgram:
                                                 run.vptr(op.src, True) if src_needs else None, acc,
                                                 hgw, hgb, pacc, op.act, op.scale, op.offset, ptr(ws), wsb, st),
                                op.layer + " bwd")
-                if on_grads is not None:
+                if br:
+                    br_names += [f"{self.prefix}/{n}" for n, _, _ in op.params]
+                elif on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Resize):
                 s, t = op.src, op.dst
@@ -1025,10 +1056,10 @@ class NetProgram:
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
         torch.cuda.set_stream(main)
-        for ev in pend.values():
-            _lib.wait_event(main, ev)
-        if b_started:
-            _lib.wait_stream(main, bmode)
+        self.join_branch()
+        self._bst = None
+        if br_names and on_grads is not None:
+            on_grads(br_names)
         if side is not None:
             self._flush_wgrad()
             names, self._wg_issued = self._wg_issued, []

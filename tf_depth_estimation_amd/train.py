@@ -367,10 +367,12 @@ class Trainer:
     def enable_branch_overlap(self, on=True, serial=False):
         """The networks' side branches (depth_net's pose and explainability-mask heads) on a stream of their own,
         beside the decoder, forward and backward (NetProgram.enable_branch_overlap; serial=True: the same calls on
-        one stream, the bit-exact reference).  Single-GPU step without Adam overlap / deferred Adam: a bucket launch
-        point of the exchange must not cut a graph while a branch is forked."""
-        if on and (self.grad_sync is not None or self.adam_ov is not None or self.dadam is not None):
-            raise ValueError("branch overlap is for the single-GPU step without Adam overlap / deferred Adam")
+        one stream, the bit-exact reference).  With the data-parallel exchange a branch's finished parameters are
+        reported from the main stream, a bucket launch point joins the branch first (a graph segment ends with its
+        forks joined) and the comm stream waits on the branch stream's tail eagerly.  Not with the Adam overlap or
+        deferred Adam."""
+        if on and (self.adam_ov is not None or self.dadam is not None):
+            raise ValueError("branch overlap and the Adam overlap / deferred Adam are exclusive")
         for p in self.programs():
             p.enable_branch_overlap(on, serial)
         return self
@@ -408,23 +410,23 @@ class Trainer:
         program's) stream -- a graph segment must end with its forked branches joined.  Only that program's:
         the other program may be mid-capture on its own stream (net overlap)."""
         p = self._program_of(chunk)
-        if p is not None:
-            p.join_wgrad()
-        else:
-            self.join_wgrad()
+        for q in ([p] if p is not None else self.programs()):
+            q.join_wgrad()
+            q.join_branch()
 
     def _chunk_side_streams(self, chunk):
         """Eagerly: the streams besides the current one that write `chunk`'s gradients (its program's
         filter-gradient streams); the comm stream waits on events at their tails, nobody else waits."""
         p = self._program_of(chunk)
-        if p is None or p.wgrad_stream is None or isinstance(p.wgrad_stream, str):
+        if p is None:
             return ()
-        return tuple(p.wgrad_streams)
+        wg = () if p.wgrad_stream is None or isinstance(p.wgrad_stream, str) else tuple(p.wgrad_streams)
+        return wg + p.branch_streams()
 
     def enable_ddp(self, world, bucket_mb=32.0, group=None):
         from .ddp import GradSync
-        if self.adam_ov is not None or self._branch_on():
-            raise ValueError("Adam overlap / branch overlap and the data-parallel exchange are exclusive")
+        if self.adam_ov is not None:
+            raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
                                   pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams)
