@@ -108,6 +108,9 @@ int tde_get_conv_math(void);
  * fused call excluded), so inside a stream capture the stamps time the kernels where the graph replays them.
  * (NULL, NULL) disarms.  Returns the number of stamps the previous arming launched. */
 int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp_end);
+/* Diagnostic timeline (probe/step_timeline.py): one one-wave kernel on `stream` that writes the device's 100 MHz
+ * real-time counter into *slot when the stream reaches it (inside a capture: when the replayed graph does). */
+int tde_stamp(unsigned long long* slot, void* stream);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
 /* Weight pre-split (the halo-tiled stride-1 path keeps the layer's weights as split fp16 / bf16 tiles):
  * bytes of the split image op (0 forward, 1 data gradient) of layer d needs under the current conv math;

@@ -26,4 +26,8 @@ for s in "" bnf bnb bnf,bnb head warp,pyr adam resize,copy; do
   rc3=$?; [ $rc3 -ne 0 ] && { echo "[r04l] skip '$s' rc=$rc3"; cat gpurun_out/skip_r04l.txt; exit $rc3; }
 done
 cat gpurun_out/skip_r04l.txt
+for b in on off; do
+  BRANCH=$b timeout -k 10 240 python probe/step_timeline.py gpurun_out/timeline_r04l_br$b.txt > gpurun_out/timeline_r04l_br$b.log 2>&1
+  rc4=$?; head -60 gpurun_out/timeline_r04l_br$b.log; [ $rc4 -ne 0 ] && exit $rc4
+done
 exit $((rcb != 0 ? rcb : rc))

@@ -111,6 +111,7 @@ _SIGS = {
     "tde_set_conv_math": (c_int, [c_int]),
     "tde_get_conv_math": (c_int, []),
     "tde_conv_span_arm": (c_int, [P, P]),
+    "tde_stamp": (c_int, [P, P]),
     "tde_conv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_deconv2d_workspace_size": (c_size_t, [P, c_int]),
     "tde_conv2d_fwd": (c_int, [P, P, P, P, c_int, P, c_size_t, P]),

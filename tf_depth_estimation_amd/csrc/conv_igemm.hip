@@ -2027,6 +2027,12 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
   return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
+int tde_stamp(unsigned long long* slot, void* stream) {
+  TDE_CHECK_ARG(slot != nullptr);
+  hipLaunchKernelGGL(span_stamp_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), slot);
+  return tde_launch_status();
+}
+
 // bench.py's graph-timed roofline: arm the calling thread's conv-kernel span stamp slots (device uint64, 8-byte
 // aligned; null, null disarms).  Returns how many stamps the previous arming launched (2 after one conv entry call).
 int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp_end) {

@@ -353,6 +353,7 @@ class NetProgram:
         self.pre_op = None
         self.params_ready = None
         self.pre_backward = None    # called first thing in backward (before any gradient is written)
+        self.timeline = None        # StepTimeline (diagnostic): a device stamp after every op, under capture only
 
     def _split_plan(self, N):
         """The convs whose forward or data-gradient call takes the halo-tiled path (their weights are kept as
@@ -632,13 +633,19 @@ class NetProgram:
         bmode = self._branch_mode() if is_training and not fold_bn else None
         ws_a, wsb_a = ws, wsb
         forked = False
+        tl = self.timeline
         for i, op in enumerate(spec.ops):
+            if tl is not None and i > 0:
+                tl.mark(self.prefix, "F", spec.ops[i - 1])
             br = bmode is not None and getattr(op, "branch", 0) == 1
             if br and bmode is not SERIAL:
                 if not forked:
                     # the branches read encoder features only, all issued by now
                     _lib.wait_stream(bmode, main)
                     forked = True
+                    if tl is not None:
+                        with torch.cuda.stream(bmode):
+                            tl.mark(self.prefix, "F", "branch fork")
                 torch.cuda.set_stream(bmode)
                 ws = self._scratch_side(N, "branch")
                 wsb = ws.numel() * 4
@@ -751,6 +758,8 @@ class NetProgram:
                 s, t = op.src, op.dst
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(s), s.buf.cs, s.coff, run.vptr(t),
                                              t.buf.cs, t.coff, 0, st), "copy")
+        if tl is not None and spec.ops:
+            tl.mark(self.prefix, "F", spec.ops[-1])
         torch.cuda.set_stream(main)
         if forked:
             _lib.wait_stream(main, bmode)
@@ -831,8 +840,11 @@ class NetProgram:
             e0.record(main)
             bst = self._bst = dict(main=main, stream=bmode, fork=e0, started=False, pend={}, refork=False)
         br_names = []     # parameters a branch op has written, reported (on_grads) from the main stream
+        tl = self.timeline
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
+            if tl is not None and i + 1 < len(spec.ops):
+                tl.mark(self.prefix, "B", spec.ops[i + 1])
             br = bmode is not None and getattr(op, "branch", 0) == 1
             real_br = br and bmode is not SERIAL
             if real_br:
@@ -842,6 +854,9 @@ class NetProgram:
                         bst["fork"].record(main)
                     _lib.wait_event(bmode, bst["fork"])
                     bst["started"], bst["refork"] = True, False
+                    if tl is not None:
+                        with torch.cuda.stream(bmode):
+                            tl.mark(self.prefix, "B", "branch fork")
                 torch.cuda.set_stream(bmode)
                 ws = self._scratch_side(N, "branch")
                 wsb = ws.numel() * 4
@@ -1055,6 +1070,8 @@ class NetProgram:
                 acc = mark(s)
                 _lib.check(lib.tde_copy_view(N * s.H * s.W, s.C, run.vptr(t, True), t.buf.cs, t.coff,
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
+        if tl is not None and spec.ops:
+            tl.mark(self.prefix, "B", spec.ops[0])
         torch.cuda.set_stream(main)
         self.join_branch()
         self._bst = None
@@ -1158,6 +1175,44 @@ class GraphTimer:
         for fam, _, ms, fl in self.per_span_ms():
             t, f, n = out.get(fam, (0.0, 0.0, 0))
             out[fam] = (t + ms, f + fl, n + 1)
+        return out
+
+
+class StepTimeline:
+    """Diagnostic step timeline (probe/step_timeline.py): under capture, a device stamp (tde_stamp, the 100 MHz
+    real-time counter) is appended to the stream an op ran on right after the op's launches; after a replay, an op's
+    time is its stamp minus the previous stamp on the same stream -- its kernels plus any cross-stream wait it began
+    with.  The stamp kernels are extra graph nodes (about a microsecond each), so the replay is slower than the
+    production step; the picture of which stream is busy with what, not the total, is the point."""
+
+    TICK_US = 1e-2
+
+    def __init__(self, max_marks=8192):
+        self.stamps = torch.zeros(max_marks, dtype=torch.int64, device="cuda")
+        self.marks = []       # (label, stream handle)
+
+    def mark(self, prefix, phase, op_or_label):
+        if not torch.cuda.is_current_stream_capturing():
+            return
+        if len(self.marks) >= self.stamps.numel():
+            raise _lib.TdeError("StepTimeline: more marks than max_marks")
+        name = op_or_label if isinstance(op_or_label, str) else getattr(op_or_label, "layer", type(op_or_label).__name__)
+        if not isinstance(op_or_label, str) and getattr(op_or_label, "branch", 0):
+            name += " [branch]"
+        s = torch.cuda.current_stream()
+        _lib.check(_lib.load().tde_stamp(ctypes.c_void_p(self.stamps.data_ptr() + 8 * len(self.marks)),
+                                         ctypes.c_void_p(s.cuda_stream)), "stamp")
+        self.marks.append((f"{phase} {prefix.split('/')[0]}:{name}", s.cuda_stream))
+
+    def intervals(self):
+        """[(label, stream, start_us, end_us)] of the last replay: per stream, marks in issue order."""
+        st = self.stamps.cpu().tolist()
+        last, out = {}, []
+        for k, (label, sid) in enumerate(self.marks):
+            t = st[k]
+            if sid in last:
+                out.append((label, sid, last[sid] * self.TICK_US, t * self.TICK_US))
+            last[sid] = t
         return out
 
 

@@ -377,6 +377,17 @@ class Trainer:
             p.enable_branch_overlap(on, serial)
         return self
 
+    timeline = None           # program.StepTimeline (diagnostic, probe/step_timeline.py)
+
+    def set_timeline(self, tl):
+        self.timeline = tl
+        for p in self.programs():
+            p.timeline = tl
+
+    def _tl(self, label):
+        if self.timeline is not None:
+            self.timeline.mark("trainer", "T", label)
+
     def _branch_on(self):
         return any(getattr(p, "branch_stream", None) is not None for p in self.programs())
 
@@ -804,18 +815,24 @@ class DepthThenCamTrainer(Trainer):
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
     def _chain_pair(self):
+        self._tl("pair chain start")
         self._p_fwd_pair()
         self._p_loss()
+        self._tl("pair loss")
         self._p_bwd_pair()
 
     def _chain_single(self):
+        self._tl("single chain start")
         self._p_fwd_single()
+        self._tl("single pyramids")
         self._p_bwd_single()
 
     def _p_inputs(self):
+        self._tl("inputs start")
         self._p_concat()
         if C4_CHAINS:
             self._area_pyramids()
+        self._tl("inputs")
 
     def _p_concat(self):
         lib, st = _lib.load(), _lib.stream_ptr()
@@ -911,6 +928,7 @@ class DepthThenCamTrainer(Trainer):
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
         if self._inline_adam():
             self.opt.opts[1].step()
+            self._tl("pair adam")
 
     def _p_bwd_single(self):
         if self.twin:
@@ -920,6 +938,7 @@ class DepthThenCamTrainer(Trainer):
             self._bwd("sl", self.single, False)
         if self._inline_adam():
             self.opt.opts[0].step()
+            self._tl("single adam")
 
     def phase_compute(self):
         self._out = {}
