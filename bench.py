@@ -271,7 +271,7 @@ def build_trainer(args, name, N, world, rank):
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     if args.sync_bn:
         tr.enable_sync_bn(world)
-    net_overlap = (args.net_overlap == "on" and args.adam_overlap == "off" and not args.sync_bn and
+    net_overlap = (args.net_overlap == "on" and args.adam_overlap == "off" and
                    len(tr.programs()) > 1 and not (args.deferred_adam == "on" and world == 1))
     wg_progs = []
     if args.wgrad_overlap == "on":
@@ -295,8 +295,7 @@ def build_trainer(args, name, N, world, rank):
         tr.enable_deferred_adam()
     if net_overlap:
         tr.enable_net_overlap()
-    branch = (getattr(args, "branch_overlap", "on") == "on" and args.adam_overlap == "off" and not deferred and
-              not args.sync_bn)
+    branch = getattr(args, "branch_overlap", "on") == "on" and args.adam_overlap == "off" and not deferred
     if branch:
         tr.enable_branch_overlap()
     branch = branch and tr._branch_on()

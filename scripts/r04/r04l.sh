@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 ok() { case $1 in 0|1) return 0;; *) echo "[r04l] $2 rc=$1: stopping GPU work"; exit $1;; esac; }
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_trainers.py tests/test_gpu_ddp.py \
-  -k "branch" > gpurun_out/tests_r04l_branch.log 2>&1
+  -k "branch or sync_bn_captured" > gpurun_out/tests_r04l_branch.log 2>&1
 rcb=$?; tail -8 gpurun_out/tests_r04l_branch.log; ok $rcb "branch tests"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_r04l.log 2>&1
 rc=$?; tail -4 gpurun_out/tests_r04l.log; echo "[r04l] tests rc=$rc"; ok $rc "gpu suite"

@@ -162,7 +162,7 @@ def test_config4_exchange_with_branch_overlap(pg, graph):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
-def _c4_syncbn(pg, graph, sync=True, steps=3):
+def _c4_syncbn(pg, graph, sync=True, steps=3, overlaps=None):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
@@ -175,6 +175,16 @@ def _c4_syncbn(pg, graph, sync=True, steps=3):
     if sync:
         tr.enable_sync_bn(1)
         assert tr.sync_bn_capturable
+    if overlaps is not None:
+        # the benched schedule (or its serial form): depth_net's filter gradients on a side stream, the two
+        # networks on two streams, depth_net's pose / mask branches on a third -- each program (and its branches)
+        # all-reducing on a communicator of its own
+        serial = overlaps == "serial"
+        tr.enable_wgrad_overlap(serial=serial, only=["pair"])
+        if not serial:
+            tr.enable_net_overlap()
+        tr.enable_branch_overlap(serial=serial)
+        assert tr._branch_on()
     n = steps
     if graph:
         tr.capture(warmup=1)
@@ -197,6 +207,11 @@ def test_sync_bn_captured_config4(pg):
     g_cap, o_cap = _c4_syncbn(pg, True)
     for a, b in zip(g_ref, g_cap):
         assert all(torch.equal(x, y) for x, y in zip(a, b)), "captured SyncBN step != eager SyncBN step"
+    # the overlapped schedule under SyncBN (per-program and per-branch communicators) == its serial form
+    g_ser, _ = _c4_syncbn(pg, False, overlaps="serial")
+    g_ov, _ = _c4_syncbn(pg, True, overlaps="overlap")
+    for a, b in zip(g_ser, g_ov):
+        assert all(torch.equal(x, y) for x, y in zip(a, b)), "overlapped SyncBN step != its serial form"
     _, o_loc = _c4_syncbn(pg, False, sync=False, steps=1)
     _, o_sb1 = _c4_syncbn(pg, False, sync=True, steps=1)
     for k in o_loc:

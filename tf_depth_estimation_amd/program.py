@@ -327,6 +327,7 @@ class NetProgram:
         # SyncBN: bn_sync(t) all-reduces (sums) a float64 device tensor in place across
         # bn_world data-parallel replicas; None = BatchNorm over the local batch (the default)
         self.bn_sync, self.bn_world = None, 1
+        self.bn_sync_branch = None   # SyncBN of the side branches' layers (their own communicator, branch overlap)
         self._bn_sums = {}
         self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
         # filter-gradient overlap (enable_wgrad_overlap): side stream, its workspace per batch, dz ring
@@ -573,10 +574,11 @@ class NetProgram:
         return self
 
     def _branch_mode(self):
-        """The branch stream (or SERIAL) when the branch overlap applies to this call: not with SyncBN and not under
-        the instrumented eager step (its HIP-event timer records on one stream)."""
+        """The branch stream (or SERIAL) when the branch overlap applies to this call: not under the instrumented
+        eager step (its HIP-event timer records on one stream), and with SyncBN only when the branches have a
+        communicator of their own (RCCL, Trainer.enable_sync_bn)."""
         bs = getattr(self, "branch_stream", None)
-        if bs is None or self.bn_sync is not None or not self._production():
+        if bs is None or (self.bn_sync is not None and self.bn_sync_branch is None) or not self._production():
             return None
         return bs
 
@@ -706,7 +708,7 @@ class NetProgram:
                     for g in range(G):
                         _lib.check(lib.tde_bn_sums(Mg, op.K, ptr(z[g * (N // G):]), None, 0, 0, None, None, None, 0, 0,
                                                    ptr(sums[g]), ptr(ws), wsb, st), op.layer + " bn sums")
-                    self.bn_sync(sums)
+                    (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(sums)
                     ystride = Mg * op.dst.buf.cs * 4
                     for g in range(G):
                         _lib.check(lib.tde_bn_fwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(z[g * (N // G):]),
@@ -816,7 +818,7 @@ class NetProgram:
         wsb = ws.numel() * 4
         iv = spec.input_view
         _lib.check(lib.tde_zero_bytes(run.absmax.numel() * 4, ptr(run.absmax), st), "zero dz bounds")
-        side = self.wgrad_stream if (self._production() and self.bn_sync is None) else None
+        side = self.wgrad_stream if self._production() else None
         if side is SERIAL:
             side = torch.cuda.current_stream()
         if side is not None:
@@ -919,7 +921,7 @@ class NetProgram:
                                                    ptr(sm[1][g * op.K:]), ptr(beta), 1, 1, ptr(ls[g]), ptr(ws), wsb, st),
                                    op.layer + " bn sums")
                     gs.copy_(ls)
-                    self.bn_sync(gs)
+                    (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(gs)
                     for g in range(G):
                         _lib.check(lib.tde_bn_bwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(zi[g * (N // G):]),
                                                             ptr(sm[0][g * op.K:]), ptr(sm[1][g * op.K:]), ptr(beta),

@@ -286,9 +286,11 @@ class Trainer:
         each piece is its own graph on its stream).  The two programs share no buffer, parameter, gradient or
         moving statistic, and each program's calls keep their order, so the step is bit-identical to the serial
         one.  With the data-parallel exchange each program's bucket launch points cut its own piece's graphs
-        (enable_ddp).  Not combinable with the Adam overlaps or SyncBN."""
-        if on and (self.adam_ov is not None or self.dadam is not None or getattr(self, "sync_bn", False)):
-            raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / SyncBN")
+        (enable_ddp).  Not combinable with the Adam overlaps or host-side (gloo) SyncBN; RCCL SyncBN gives each
+        program its own communicator (enable_sync_bn)."""
+        if on and (self.adam_ov is not None or self.dadam is not None or
+                   (getattr(self, "sync_bn", False) and not getattr(self, "sync_bn_capturable", False))):
+            raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / host-side SyncBN")
         self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
@@ -454,14 +456,24 @@ class Trainer:
         graph.  Over gloo (host collectives) the step runs eagerly."""
         import torch.distributed as dist
         nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
-        if nccl and group is None:
-            group = dist.new_group(backend="nccl")
 
-        def sync(t):
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        def make_sync(g):
+            def sync(t):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
+            return sync
 
         for p in self.programs():
-            p.bn_sync, p.bn_world = sync, world
+            # over RCCL one communicator PER PROGRAM (created in program order on every rank): each program's
+            # collectives are then issued from one stream in a fixed order, so the two networks of config 4 may run
+            # on two streams (enable_net_overlap) without their all-reduces meeting in different orders on
+            # different GPUs
+            g = dist.new_group(backend="nccl") if nccl and group is None else group
+            p.bn_sync, p.bn_world = make_sync(g), world
+            # the program's side branches (enable_branch_overlap) issue theirs from the branch stream: a communicator
+            # of their own as well
+            p.bn_sync_branch = None
+            if nccl and group is None and any(getattr(op, "branch", 0) for op in p.spec.ops):
+                p.bn_sync_branch = make_sync(dist.new_group(backend="nccl"))
         self.sync_bn = True
         self.sync_bn_capturable = nccl
 
