@@ -20,6 +20,9 @@ for b in on off; do
   rc2=$?; echo "[r04l] bench branch=$b rc=$rc2"; [ $rc2 -ne 0 ] && { tail -5 gpurun_out/bench_r04l_br$b.err; ok $rc2 bench; continue; }
   python -c "import json;d=json.load(open('gpurun_out/bench_r04l_br$b.json'));print('value',d['value'],'ms',d['ms_per_step'],'frac',d['roofline']['frac']);print(d.get('secondary'))"
 done
+timeout -k 10 600 python bench.py --sync-bn --no-secondary --no-cpu-baseline > gpurun_out/bench_r04l_syncbn.json 2> gpurun_out/bench_r04l_syncbn.err
+rc5=$?; echo "[r04l] bench syncbn rc=$rc5"; ok $rc5 "syncbn bench"
+[ $rc5 -eq 0 ] && python -c "import json;d=json.load(open('gpurun_out/bench_r04l_syncbn.json'));print('syncbn value',d['value'],'ms',d['ms_per_step'],d['config'])"
 : > gpurun_out/skip_r04l.txt
 for s in "" bnf bnb bnf,bnb head warp,pyr adam resize,copy; do
   SKIP=$s timeout -k 10 180 python probe/skip_family.py 100 >> gpurun_out/skip_r04l.txt 2>/dev/null
