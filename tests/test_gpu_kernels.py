@@ -326,6 +326,8 @@ BN_FUSED_CASES = [
     (True, 8, 48, 64, 32, 16, 3, 2),             # deconv, no split, BN partials from the epilogue
     (False, 8, 48, 64, 64, 64, 5, 1),            # cnv2b-like (halo path in the bf16x6 modes: tile partials)
     (False, 2, 96, 128, 32, 32, 7, 1),           # cnv1b-like: halo path, BN partials per pixel tile
+    (True, 4, 96, 128, 32, 16, 3, 2),            # pixel-shuffle deconv (64-row tiles), BN records per row tile
+    (True, 4, 96, 128, 32, 64, 3, 2),            # pixel-shuffle deconv, 2 column tiles of 2 classes each
 ]
 
 
@@ -394,7 +396,8 @@ def test_conv_fused_bn_grouped(L, case):
     """Row-grouped BatchNorm (tde_bn_train_t.groups = 2: the left / right calls of one shared-variable network
     batched, train_depth_then_cam_lr.py:130-136): each half of the batch is normalised over its own rows, the
     moving averages take the halves' updates in order, y = relu(BN_g(z)) per half -- on every fused path
-    (small, epilogue partials, split-K / deconv -> grouped standalone pass, halo tile partials)."""
+    (small, epilogue partials incl. a deconv's parity classes group-major and the pixel-shuffle records, split-K
+    reduce partials per group, halo tile partials)."""
     deconv, N, H, W, C, K, k, s = case
     G = 2
     lib = L.load()

@@ -61,8 +61,11 @@ struct ConvArgs {
   float* ws; int splits; int accumulate;
   int kt_per;  // k-tiles per split
   FDiv fC, fK, fKW, fOW, fOHW;
-  double* bnp;  // BN statistics partials [row tile][2][Nn] from the epilogue (FWD/DGRAD, splits == 1)
+  double* bnp;  // BN statistics partials [row tile][2][Nn] from the epilogue (FWD/DGRAD/PS, splits == 1)
   int bn_gx;    // row tiles per DGRAD class (grid x)
+  int bn_G;     // BN row groups (DGRAD: partials ordered group-major over the parity classes; the host checks that
+                // every class's rows per group are whole row tiles)
+  int bn_gy;    // MODE_PS: column tiles (one partial record [2][ps_C] per (row tile, column tile))
   // inference epilogue (FWD / DGRAD outputs only; accumulate == 0): v = conv + bias[col], then ReLU
   // (BN folded into the weights, tde_conv2d_fwd_bias_act); bias null and relu 0 = plain conv
   const float* bias; int relu;
@@ -736,7 +739,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   // sum and sum of squares over the tile's rows (rows past M hold exact zeros: their operand rows loaded
   // as zero), lanes -> waves in a fixed order, one fp64 partial per row tile.  Workgroup-local: the
   // cross-tile reduction is the next kernel's (a launch costs what an in-kernel hand-off costs).
-  if constexpr (MODE != MODE_WGRAD && MODE != MODE_PS) {
+  if constexpr (MODE != MODE_WGRAD) {
     if (p.bnp != nullptr) {
       float cs[TN], cq[TN];
 #pragma unroll
@@ -758,11 +761,42 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         }
       }
       __syncthreads();
-      if (tid < BN && n0 + tid < Nn) {
-        // dense row-tile index (class-major for DGRAD: classes own disjoint pixel sets)
+      if constexpr (MODE == MODE_PS) {
+        // column (py, px, c) is channel c of output-pixel class (py, px): a tile of BN columns covers whole classes
+        // (the host checks BN % ps_C == 0), so channel c's record sums its classes' columns in class order
+        const int Cc = p.ps_C;
+        if (tid < Cc) {
+          double sv = 0.0, sq = 0.0;
+          for (int k = 0; k * Cc < BN; ++k) {
+            const int col = k * Cc + tid;
+            if (n0 + col >= Nn) break;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) { sv += red[w * BN + col]; sq += red[(WM + w) * BN + col]; }
+          }
+          const size_t j = (size_t)bx * p.bn_gy + by;
+          p.bnp[j * 2 * Cc + tid] = sv;
+          p.bnp[j * 2 * Cc + Cc + tid] = sq;
+        }
+      } else if (tid < BN && n0 + tid < Nn) {
+        // dense row-tile index (class-major for DGRAD: classes own disjoint pixel sets; with row groups group-major,
+        // each group's tiles of every class before the next group's)
         int j = bx;
-        if constexpr (MODE == MODE_DGRAD)
-          for (int c = 0; c < (int)(bz % (p.S * p.S)); ++c) j += (dg_class(p, c).M + BM - 1) / BM;
+        if constexpr (MODE == MODE_DGRAD) {
+          const int ncls = p.S * p.S, cls = bz % ncls;
+          if (p.bn_G > 1) {
+            int off = 0, tot = 0, tg = 1;
+            for (int c = 0; c < ncls; ++c) {
+              const int t = dg_class(p, c).M / p.bn_G / BM;
+              if (c < cls) off += t;
+              if (c == cls) tg = t;
+              tot += t;
+            }
+            const int gi = bx / tg;
+            j = gi * tot + off + (bx - gi * tg);
+          } else {
+            for (int c = 0; c < cls; ++c) j += (dg_class(p, c).M + BM - 1) / BM;
+          }
+        }
         double sv = 0.0, sq = 0.0;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { sv += red[w * BN + tid]; sq += red[(WM + w) * BN + tid]; }
@@ -1090,7 +1124,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
 // splitk_reduce_kernel) written densely, plus per-row-chunk fp64 statistics partials [chunk][2][cols].
 // Grid (row chunk, 64-channel group): a thread owns one channel quad of a row lane.
 __global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, int splits, int rows, int cols,
-                                                               float* z, int rows_per_chunk, double* part) {
+                                                               float* z, const BnChunks cp, double* part) {
   __shared__ double sh[2][256 * 4];
   const int q0 = blockIdx.y * 16;
   const int nq = min(16, cols / 4 - q0);
@@ -1099,7 +1133,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, 
   const int c = 4 * (q0 + tx);
   const long stride = (long)rows * cols;
   double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  const int r0 = blockIdx.x * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
+  int r0, r1;
+  bn_chunk_rows(cp, blockIdx.x, r0, r1);   // row groups: every chunk inside one group (group-major partials)
   if (ty < ty_n) {
     float f0[4] = {0, 0, 0, 0}, f1[4] = {0, 0, 0, 0};
     for (int r = r0 + ty; r < r1; r += ty_n) {
@@ -1291,9 +1326,17 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl, int G 
   BnPlan b{};
   if (G < 1) G = 1;
   const int Mg = pl.rows / G;
+  // a deconv's parity classes: every class's rows per group whole row tiles (group-major epilogue partials)
+  bool cls_aligned = true;
+  if (mode == MODE_DGRAD)
+    for (int c = 0; c < d.stride * d.stride; ++c) {
+      const int py = c / d.stride, px = c - py * d.stride;
+      const long mc = (long)d.N * ((d.H - py + d.stride - 1) / d.stride) * ((d.W - px + d.stride - 1) / d.stride);
+      if (mc % G != 0 || (mc / G) % pl.bm != 0) cls_aligned = false;
+    }
   if (Mg <= BN_SMALL_M) {
     b.path = BN_SMALL;
-  } else if (G > 1 && (pl.splits > 1 || mode == MODE_DGRAD || Mg % pl.bm != 0)) {
+  } else if (G > 1 && pl.splits == 1 && (mode == MODE_DGRAD ? !cls_aligned : Mg % pl.bm != 0)) {
     // row groups whose boundaries the epilogue's row tiles (or a deconv's parity-class tiles) do not respect:
     // the statistics come from a separate grouped partial pass over z
     b.path = BN_STANDALONE;
@@ -1309,8 +1352,9 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl, int G 
     else
       b.nparts = pl.gx;
   } else {
+    // split-K: the reduce kernel writes z and the partials, one per row chunk, every chunk inside one row group
     b.path = BN_REDUCE;
-    b.ch = bn_chunk_plan(pl.rows, pl.cols, pl.splits);
+    b.ch = bn_chunk_plan(pl.rows, pl.cols, pl.splits, G);
     b.nparts = b.ch.chunks;
   }
   b.part_bytes = (size_t)b.nparts * 2 * pl.cols * sizeof(double);
@@ -1349,11 +1393,19 @@ static size_t hwg_ws_bytes(const tde_conv_desc_t& d) {
   return b;
 }
 
+static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr);
+
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   const Plan pl = make_plan(d, mode);
   const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
   const size_t halo = halo_ws_bytes(d, mode, bn);
   size_t b = igemm > halo ? igemm : halo;
+  int pbm = 0, pbn = 0;
+  if (mode == MODE_DGRAD && bn && ps_ok(d, &pbm, &pbn)) {
+    // pixel-shuffle path: one partial record [2][C] per (row tile, column tile)
+    const size_t pb = (size_t)tde_cdiv((long)d.N * d.OH * d.OW, pbm) * (4 * d.C / pbn) * 2 * d.C * sizeof(double);
+    if (pb > b) b = pb;
+  }
   HwgPlan wp;
   if (mode == MODE_WGRAD && hwg_ws_bytes(d) > b) b = hwg_ws_bytes(d);
   return b;
@@ -1530,7 +1582,7 @@ static const long g_ps_minm = env_long("TDE_DECONV_PS_MINM", 8192);
 // 128 rows, else >= 512 of 64 rows (measured, batch 8, us: upcnv1 48.2 -> 35.5 with 768 blocks of 128 rows;
 // upcnv2 28.7 -> 29.7 with 192, upcnv3 32.8 -> 37.7 with 96, upcnv4 29.5 -> 57.3 with 24: r03x)
 static const long g_ps_minblocks = env_long("TDE_DECONV_PS_MINBLOCKS", 512);
-static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr) {
+static bool ps_ok(const tde_conv_desc_t& d, int* bm, int* bn) {
   if (!(g_ps_minm > 0 && g_conv_math == 4 && d.stride == 2 && d.KH == 3 && d.KW == 3 && d.pad_top == 0 &&
         d.pad_left == 0 && d.H == 2 * d.OH && d.W == 2 * d.OW && d.w_cin == d.C && d.C % 16 == 0 && d.K % 4 == 0 &&
         (long)d.N * d.OH * d.OW >= g_ps_minm))
@@ -1563,11 +1615,21 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   const int Nn = 4 * d->C;
   const int G = bn && bn->groups > 1 ? bn->groups : 1;
   if (rows % G != 0) return TDE_ERR_ARG;
-  if (bn && (!ws || !tde_aligned16(ws) || bn_part_bytes(rows, d->C) > ws_bytes)) return TDE_ERR_WORKSPACE;
-  hipStream_t st = static_cast<hipStream_t>(stream);
   int BM = 0, BN = 0;
   ps_ok(*d, &BM, &BN);
   const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
+  // BN statistics from the epilogue (one record per (row tile, column tile)) when every row group is whole row tiles
+  // and a tile covers whole classes; else a grouped partial pass over z
+  const bool epi = bn && rows / G > BN_SMALL_M && (M % G == 0) && ((M / G) % BM == 0) && BN % d->C == 0;
+  const size_t epi_bytes = (size_t)grid.x * grid.y * 2 * d->C * sizeof(double);
+  if (bn && (!ws || !tde_aligned16(ws) || bn_part_bytes(rows, d->C) > ws_bytes || (epi && epi_bytes > ws_bytes)))
+    return TDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  double* part = bn ? reinterpret_cast<double*>(tde_ws_body(ws)) : nullptr;
+  if (epi) {
+    a.bnp = part;
+    a.bn_gy = (int)grid.y;
+  }
   span_mark(0, st);
   if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
@@ -1575,11 +1637,11 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   span_mark(1, st);
   if (bn) {
-    // statistics from a grouped partial pass over z (the parity classes of a row tile are not one row range)
     const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
                   bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
     if (rows / G <= BN_SMALL_M) bn_fwd_small_launch((int)rows, d->C, a.y, o, st);
-    else bn_fwd_standalone_launch((int)rows, d->C, a.y, o, reinterpret_cast<double*>(tde_ws_body(ws)), st);
+    else if (epi) bn_fwd_from_partials_launch((int)rows, d->C, a.y, (int)(grid.x * grid.y), part, o, st);
+    else bn_fwd_standalone_launch((int)rows, d->C, a.y, o, part, st);
   }
   return tde_launch_status();
 }
@@ -1642,6 +1704,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   a.accumulate = accumulate;
   a.bnp = (bn && bp.path == BN_EPI) ? part : nullptr;
   a.bn_gx = pl.gx;
+  a.bn_G = G;
   hipStream_t st = static_cast<hipStream_t>(stream);
   span_mark(0, st);
   if (!skip) launch_mode<MODE>(pl, a, st);
@@ -1649,7 +1712,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   if (!skipr && !(bn && bp.path == BN_REDUCE)) launch_reduce<MODE>(pl, a, st);
   if (bn && bp.path == BN_REDUCE && !skipr)
     hipLaunchKernelGGL(splitk_reduce_bn_kernel, dim3(bp.ch.chunks, bp.ch.groups), dim3(256), 0, st, a.ws, pl.splits,
-                       pl.rows, pl.cols, z, bp.ch.rows_per_chunk, part);
+                       pl.rows, pl.cols, z, bp.ch, part);
   span_mark(1, st);
   if (bn) {
     // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
