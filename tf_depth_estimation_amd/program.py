@@ -587,7 +587,12 @@ class NetProgram:
         was forked: a graph segment must end with its forked branches joined (the exchange's launch points).  A
         later branch op forks again from the main stream."""
         bst = getattr(self, "_bst", None)
-        if bst is None or not bst["started"] or bst["refork"]:
+        if bst is None or bst["refork"]:
+            return
+        if not bst["started"]:
+            # a graph cut before the branch's first op: the fork event recorded at the start of backward belongs to
+            # an ended capture segment, so the branch must fork from an event recorded when it starts
+            bst["refork"] = True
             return
         _lib.wait_stream(torch.cuda.current_stream(), bst["stream"])
         bst["pend"].clear()
