@@ -25,6 +25,9 @@ CAPTURE_MODE = "thread_local"
 LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
 # config 4 as two independent per-network chains with one join (TDE_C4_CHAINS=0: the two-join schedule, A/B)
 C4_CHAINS = os.environ.get("TDE_C4_CHAINS", "1") != "0"
+# config 4 chains: the compute stream's chain (disp_net) issued BEFORE the second stream's (depth_net), which then
+# waits only for the inputs piece (TDE_C4_MAIN_FIRST=1; A/B of the launch order)
+C4_MAIN_FIRST = os.environ.get("TDE_C4_MAIN_FIRST", "0") == "1"
 
 
 def _halves(a, b):
@@ -822,6 +825,8 @@ class DepthThenCamTrainer(Trainer):
             # of a join before the loss, and the depth_net-dependent loss runs beside disp_net's backward.  The
             # second stream waits only for the inputs (concat + image area pyramids)
             chain = {"pair": self._chain_pair, "single": self._chain_single}
+            if C4_MAIN_FIRST:
+                return [("main", self._p_inputs), ("fork", None), ("main", chain[m]), ("ov", chain[o]), ("join", None)]
             return [("main", self._p_inputs), ("ov", chain[o]), ("main", chain[m]), ("join", None)]
         return [("main", self._p_inputs), ("ov", fwd[o]), ("main", fwd[m]), ("join", None),
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
@@ -956,13 +961,21 @@ class DepthThenCamTrainer(Trainer):
         self._out = {}
         ov = self._overlap_stream()
         cur = torch.cuda.current_stream()
+        fork = None
         for where, fn in self._pieces():
             if where == "join":
                 if ov is not None:
                     _lib.wait_stream(cur, ov)
+            elif where == "fork":
+                if ov is not None:
+                    fork = torch.cuda.Event()
+                    fork.record(cur)
             elif where == "ov" and ov is not None:
                 # depth_net on both pairs on the second stream, beside disp_net on both images
-                _lib.wait_stream(ov, cur)
+                if fork is not None:
+                    _lib.wait_event(ov, fork)
+                else:
+                    _lib.wait_stream(ov, cur)
                 with torch.cuda.stream(ov):
                     fn()
             else:
@@ -995,7 +1008,7 @@ class DepthThenCamTrainer(Trainer):
             gs.begin_step()
         try:
             for where, fn in pieces:
-                if where == "join":
+                if where in ("join", "fork"):
                     seq.append((where, None))
                     continue
                 stream = ov if where == "ov" else main
@@ -1046,12 +1059,20 @@ class DepthThenCamTrainer(Trainer):
         seg = gs is not None and hasattr(gs, "begin_step")
         if seg:
             gs.begin_step()
+        fork = None
         for where, segs in self.ov_seq:
             if where == "join":
                 cur.wait_stream(ov)
                 continue
+            if where == "fork":
+                fork = torch.cuda.Event()
+                fork.record(cur)
+                continue
             if where == "ov":
-                ov.wait_stream(cur)
+                if fork is not None:
+                    ov.wait_event(fork)
+                else:
+                    ov.wait_stream(cur)
             with torch.cuda.stream(ov if where == "ov" else cur):
                 for g, buckets in segs:
                     if g is not None:
