@@ -295,7 +295,7 @@ def build_trainer(args, name, N, world, rank):
         tr.enable_deferred_adam()
     if net_overlap:
         tr.enable_net_overlap()
-    branch = getattr(args, "branch_overlap", "on") == "on" and args.adam_overlap == "off" and not deferred
+    branch = getattr(args, "branch_overlap", "off") == "on" and args.adam_overlap == "off" and not deferred
     if branch:
         tr.enable_branch_overlap()
     branch = branch and tr._branch_on()
@@ -438,9 +438,10 @@ def main():
                     help="config 4: depth_net's calls on a second stream beside disp_net's (independent "
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
                          "Measured config 4 605 -> 665 samples/s")
-    ap.add_argument("--branch-overlap", default="on", choices=["on", "off"],
+    ap.add_argument("--branch-overlap", default="off", choices=["on", "off"],
                     help="depth_net's pose and explainability-mask branches on a stream of their own beside the decoder, "
-                         "forward and backward (bit-identical to the same calls on one stream)")
+                         "forward and backward (bit-identical to the same calls on one stream).  Measured slower: config 4 "
+                         "1074-1082 -> 901-912 pairs/s (a third concurrent queue delays disp_net's chain; DESIGN.md)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce of every row group's sums per BN layer "
                          "and direction, on a communicator of its own, captured into the step's graphs)")

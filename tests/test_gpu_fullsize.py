@@ -167,11 +167,9 @@ def test_config4_forward_benched_batch():
     tr = train.DepthThenCamTrainer(B, H, W)
     assert tr.twin and tr.runs["s"].groups == 2 and tr.runs["p"].groups == 2 and tr.runs["s"].N == 2 * B
     # bench.py's schedule at N = 1: depth_net's filter gradients on their side stream, the two networks on two
-    # streams, depth_net's pose / mask branches on a third
+    # streams
     tr.enable_wgrad_overlap(only=["pair"])
     tr.enable_net_overlap()
-    tr.enable_branch_overlap()
-    assert tr._branch_on()
     il, ir = texture(B, H, W, 51), texture(B, H, W, 52)
     g = np.random.default_rng(53)
     lab = g.uniform(0.1, 2.0, (B, H, W, 1))
