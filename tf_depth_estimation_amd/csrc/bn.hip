@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float
         const float v = (zv[j] - mu[j]) * is[j] + bt[j];
         o[j] = (relu && v < 0.f) ? 0.f : v;
       }
-      *reinterpret_cast<f4*>(y + (long)r * ycs + yco + c) = o;
+      tde_st(reinterpret_cast<f4*>(y + (long)r * ycs + yco + c), o);
     }
   }
 }
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
         o[j] = is[j] * (g - mg[j] - xh * mgx[j]);
         mx = fmaxf(mx, fabsf(o[j]));
       }
-      *reinterpret_cast<f4*>(dz + (long)r * C + c) = o;
+      tde_st(reinterpret_cast<f4*>(dz + (long)r * C + c), o);
     }
   }
   block_absmax_to(mx, amax);
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const f
           const float t = (v[i][j] - s_mu[j]) * s_is[j] + bt[j];
           o[j] = (relu && t < 0.f) ? 0.f : t;
         }
-        *reinterpret_cast<f4*>(yg + (long)r * ycs + yco + c) = o;
+        tde_st(reinterpret_cast<f4*>(yg + (long)r * ycs + yco + c), o);
       }
     }
   }
@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const f
           o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
           mx = fmaxf(mx, fabsf(o[j]));
         }
-        *reinterpret_cast<f4*>(dz + (row0 + r) * C + c) = o;
+        tde_st(reinterpret_cast<f4*>(dz + (row0 + r) * C + c), o);
       }
     }
   }

@@ -891,7 +891,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int n = n0 + wcol0 + b * 16 + r16;
-        if (rowaddr[a][r] >= 0 && n < Nn) base[rowaddr[a][r] + coff[b]] = acc[a][b][r];
+        if (rowaddr[a][r] >= 0 && n < Nn) tde_st(base + rowaddr[a][r] + coff[b], acc[a][b][r]);
       }
 }
 
@@ -1116,7 +1116,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
         for (int j = 0; j < 4; ++j) s[j] = bias_act(s[j], p.bias, col + j, p.relu);
       }
     }
-    *reinterpret_cast<f4*>(dst) = s;
+    tde_st(reinterpret_cast<f4*>(dst), s);
   }
 }
 
@@ -1147,7 +1147,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_bn_kernel(const float* ws, 
       }
       for (int u = 0; zi < splits; ++zi, ++u) a[u] += ld4(src + zi * stride);
       const f4 v = (a[0] + a[1]) + (a[2] + a[3]);
-      *reinterpret_cast<f4*>(z + (long)r * cols + c) = v;
+      tde_st(reinterpret_cast<f4*>(z + (long)r * cols + c), v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { f0[j] += v[j]; f1[j] += v[j] * v[j]; }
     }

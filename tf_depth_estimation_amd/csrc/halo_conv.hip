@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
         const int col = col0 + b * 16 + r16;
-        if (rowok[a][r] && col < p.Ncols) p.out[rowaddr[a][r] + col] = acc[a][b][r];
+        if (rowok[a][r] && col < p.Ncols) tde_st(p.out + rowaddr[a][r] + col, acc[a][b][r]);
       }
 }
 
