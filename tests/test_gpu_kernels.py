@@ -460,14 +460,16 @@ def test_conv_fused_bn_grouped(L, case):
     L.check(lib.tde_bn_bwd(M, Kc, G, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(gdy), ycs, yco,
                            L.ptr(dz), L.ptr(dbeta), 0, 1, None, L.ptr(wsb), wsb.numel() * 4, st))
     zr_ = zr.double().reshape(M, Kc).clone().requires_grad_(True)
+    # the ReLU mask the GPU applied (y > 0): at millions of elements a pre-activation within rounding of zero flips
+    # between the fp32 and fp64 evaluations, and dz is discontinuous there (dy vs 0)
+    ym = (y[:, yco:yco + Kc] > 0).double().cpu()
     outs = []
     for g in range(G):
         zg = zr_[g * Mg:(g + 1) * Mg]
         mean, var = zg.mean(0), zg.var(0, unbiased=False)
-        outs.append(torch.relu((zg - mean) / torch.sqrt(var + 1e-3) + beta.double().cpu()))
+        outs.append(((zg - mean) / torch.sqrt(var + 1e-3) + beta.double().cpu()) * ym[g * Mg:(g + 1) * Mg])
     torch.cat(outs).backward(dy)
     close(dz, zr_.grad, tol=5e-5, what="grouped bn dz")
-    ym = torch.cat(outs).detach() > 0
     close(dbeta, (dy * ym).sum(0), tol=5e-5, what="grouped dbeta")
 
 
