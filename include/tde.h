@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 7
+#define TDE_ABI_VERSION 8
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
@@ -142,6 +142,9 @@ typedef struct {
   float* y; int y_cstride, y_coff;
   int relu;
   int groups;              /* row groups (0 or 1: one), see tde_bn_fwd_train */
+  double* sums;            /* SyncBN phase 1 (non-NULL): write the per-group fp64 (sum z, sum z^2) [groups][2][C]
+                              from the conv's own statistics partials and stop -- no statistics, moving averages
+                              or y (see tde_bn_sums / tde_bn_fwd_from_sums) */
 } tde_bn_train_t;
 /* z dense [N*OH*OW][K] (y_cstride == K, y_coff == 0 in d).  Workspace: tde_conv2d_workspace_size(d, 3). */
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z,
@@ -248,26 +251,30 @@ int tde_bias_relu_bwd(int M, int C, const float* y, int y_cstride, int y_coff, c
                       void* ws, size_t ws_bytes, void* stream);
 
 /* SyncBN (BatchNorm over the batch of ALL data-parallel replicas), in two phases around
- * the caller's all-reduce of `sums` (fp64 [2][C]):
- *   forward : tde_bn_sums(mode 0) -> sums = (sum z, sum z^2) over this replica's M rows; all-reduce;
- *             tde_bn_fwd_from_sums(M, C, M_total, ...) = tde_bn_fwd_train semantics over M_total rows.
- *   backward: tde_bn_sums(mode 1) -> (sum g, sum g*xhat), g = dy * relu'(y); keep a copy (local), all-reduce
- *             (global); tde_bn_bwd_from_sums: dz from the global means, dbeta from the LOCAL sum g (the
- *             data-parallel gradient average divides the summed dbeta by the replica count).
+ * the caller's ONE all-reduce of `sums` (fp64 [groups][2][C]; M rows = `groups` equal row groups, each its own
+ * BatchNorm batch as in tde_bn_fwd_train):
+ *   forward : tde_bn_sums(mode 0), or the conv itself (tde_conv2d_fwd_bn / tde_deconv2d_fwd_bn with
+ *             tde_bn_train_t.sums) -> sums = (sum z, sum z^2) per group over this replica's rows; all-reduce;
+ *             tde_bn_fwd_from_sums(M, C, groups, M_total, ...) = tde_bn_fwd_train semantics over M_total rows per
+ *             group, in ONE launch (statistics computed from the sums in the apply pass; block 0 publishes them
+ *             and the moving averages, groups in order).
+ *   backward: tde_bn_sums(mode 1) -> (sum g, sum g*xhat), g = dy * relu'(y), into `sums` and (optional) the same
+ *             values into `sums_copy` (the local copy); all-reduce `sums` (global); tde_bn_bwd_from_sums: dz from
+ *             the global means, dbeta from the LOCAL sum g (the data-parallel gradient average divides the summed
+ *             dbeta by the replica count), one launch.
  * Replaces slim.batch_norm's moments over the single-device batch (nets_optflow_depth.py:82-87) with
  * moments over the global batch (the reference's own semantics at global batch 64 on one device). */
-int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, int dy_coff,
+int tde_bn_sums(int M, int C, int groups, const float* z, const float* dy, int dy_cstride, int dy_coff,
                 const float* save_mean, const float* save_invstd, const float* beta, int relu, int mode,
-                double* sums, void* ws, size_t ws_bytes, void* stream);
-int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const double* sums, const float* beta,
-                         float eps, float decay, int bessel, float* moving_mean, float* moving_var,
+                double* sums, double* sums_copy, void* ws, size_t ws_bytes, void* stream);
+int tde_bn_fwd_from_sums(int M, int C, int groups, long M_total, const float* z, const double* sums,
+                         const float* beta, float eps, float decay, int bessel, float* moving_mean, float* moving_var,
                          float* save_mean, float* save_invstd, float* y, int y_cstride, int y_coff, int relu,
                          void* stream);
-int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean,
+int tde_bn_bwd_from_sums(int M, int C, int groups, long M_total, const float* z, const float* save_mean,
                          const float* save_invstd, const float* beta, const float* dy, int dy_cstride, int dy_coff,
                          const double* global_sums, const double* local_sums, float* dz, float* dbeta,
-                         int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes,
-                         void* stream);
+                         int accumulate_dbeta, int relu, float* dz_absmax, void* stream);
 
 /* ---------------------------------------------------------------- legacy resizes
  * resize_like -> tf.image.resize_nearest_neighbor (nets_optflow_depth.py:11-16),

@@ -15,7 +15,7 @@ ParamChunk, and asserts on every rank; a non-zero exit fails the test.
   syncbn      : the SyncBN protocol of Trainer.enable_sync_bn / NetProgram (per-layer fp64 (sum z, sum z^2) and, in
                 backward, (sum g, sum g*xhat) all-reduced with SUM; statistics and coefficients from the global
                 sums over M x world rows; dbeta from the LOCAL sum, averaged by the gradient exchange), restated
-                with the formulas of bn.hip's bn_from_sums_kernel / bn_bwd_apply_kernel: every rank's normalised
+                with the formulas of bn.hip's stats_from_sums / bn_bwd_apply_kernel: every rank's normalised
                 output, dz, dbeta and moving averages equal whole-batch BatchNorm + ReLU (oracle tf_ops.batch_norm
                 and its fp64 autograd) on the concatenated batch, the reference's one-device semantics
                 (train_depth_then_cam_lr.py:130-136).  The kernels themselves run on the GPU in

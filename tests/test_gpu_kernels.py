@@ -471,6 +471,36 @@ def test_conv_fused_bn_grouped(L, case):
     torch.cat(outs).backward(dy)
     close(dz, zr_.grad, tol=5e-5, what="grouped bn dz")
     close(dbeta, (dy * ym).sum(0), tol=5e-5, what="grouped dbeta")
+    # SyncBN phases on one replica (M_total = the group's rows): the conv's phase-1 sums (tde_bn_train_t.sums, from
+    # the same statistics partials) then ONE tde_bn_fwd_from_sums launch == the fused call; backward: one tde_bn_sums
+    # (+ local copy) then ONE tde_bn_bwd_from_sums launch == tde_bn_bwd
+    sums = torch.full((G, 2 * Kc), float("nan"), dtype=torch.float64, device="cuda")
+    z3, y3 = torch.empty_like(z), torch.zeros_like(y)
+    sm3 = torch.empty_like(sm)
+    mm3, mv3 = torch.zeros(Kc, device="cuda"), torch.ones(Kc, device="cuda")
+    bn3 = L.BnTrain(L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm3), L.ptr(mv3), L.ptr(sm3[0]), L.ptr(sm3[1]), L.ptr(y3), ycs,
+                    yco, 1, G, L.ptr(sums))
+    L.check(fn(ctypes.byref(d), L.ptr(dev(x)), L.ptr(dev(w)), L.ptr(z3), ctypes.byref(bn3), L.ptr(ws), ws.numel() * 4,
+               st))
+    assert torch.equal(z3, z) and float(y3.abs().sum()) == 0.0, "phase 1 writes z and the sums only"
+    zz = z64.reshape(G, Mg, Kc)
+    close(sums[:, :Kc], zz.sum(1), tol=1e-9, what="phase-1 sum z")
+    close(sums[:, Kc:], (zz * zz).sum(1), tol=1e-9, what="phase-1 sum z^2")
+    L.check(lib.tde_bn_fwd_from_sums(M, Kc, G, Mg, L.ptr(z3), L.ptr(sums), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm3),
+                                     L.ptr(mv3), L.ptr(sm3[0]), L.ptr(sm3[1]), L.ptr(y3), ycs, yco, 1, st))
+    close(sm3, sm, tol=1e-6, what="from-sums statistics")
+    close(mm3, mm, tol=1e-6, what="from-sums moving mean")
+    close(mv3, mv, tol=1e-6, what="from-sums moving var")
+    close(y3, y, tol=1e-5, what="from-sums y")
+    gs, ls = (torch.empty(G, 2 * Kc, dtype=torch.float64, device="cuda") for _ in range(2))
+    L.check(lib.tde_bn_sums(M, Kc, G, L.ptr(z), L.ptr(gdy), ycs, yco, L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), 1, 1,
+                            L.ptr(gs), L.ptr(ls), L.ptr(wsb), wsb.numel() * 4, st))
+    assert torch.equal(gs, ls), "local copy"
+    dz3, db3 = torch.empty_like(dz), torch.full_like(dbeta, 7.0)
+    L.check(lib.tde_bn_bwd_from_sums(M, Kc, G, Mg, L.ptr(z), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), L.ptr(gdy), ycs,
+                                     yco, L.ptr(gs), L.ptr(ls), L.ptr(dz3), L.ptr(db3), 0, 1, None, st))
+    close(dz3, dz, tol=1e-5, what="from-sums dz")
+    close(db3, dbeta, tol=1e-6, what="from-sums dbeta (groups added, not accumulated)")
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -829,16 +859,16 @@ def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
     parts = [(0, M1), (M1, M2)]
     sums = [torch.empty(2 * C, dtype=torch.float64, device="cuda") for _ in parts]
     for (r0, m), s in zip(parts, sums):
-        L.check(lib.tde_bn_sums(m, C, L.ptr(z[r0:]), None, 0, 0, None, None, None, 0, 0, L.ptr(s), L.ptr(ws),
+        L.check(lib.tde_bn_sums(m, C, 1, L.ptr(z[r0:]), None, 0, 0, None, None, None, 0, 0, L.ptr(s), None, L.ptr(ws),
                                 ws.numel() * 4, st))
     g = sums[0] + sums[1]                                        # the all-reduce
     y2 = torch.empty(M, C, device="cuda")
     sm2 = torch.empty(2, 2, C, device="cuda")
     mm2, mv2 = torch.zeros(2, C, device="cuda"), torch.ones(2, C, device="cuda")
     for k, (r0, m) in enumerate(parts):
-        L.check(lib.tde_bn_fwd_from_sums(m, C, M, L.ptr(z[r0:]), L.ptr(g), L.ptr(beta), 1e-3, 0.99, 1, L.ptr(mm2[k]),
-                                         L.ptr(mv2[k]), L.ptr(sm2[k, 0]), L.ptr(sm2[k, 1]), L.ptr(y2[r0:]), C, 0, 1,
-                                         st))
+        L.check(lib.tde_bn_fwd_from_sums(m, C, 1, M, L.ptr(z[r0:]), L.ptr(g), L.ptr(beta), 1e-3, 0.99, 1,
+                                         L.ptr(mm2[k]), L.ptr(mv2[k]), L.ptr(sm2[k, 0]), L.ptr(sm2[k, 1]),
+                                         L.ptr(y2[r0:]), C, 0, 1, st))
     for k in range(2):
         close(sm2[k], sm, tol=1e-6, what="global statistics")
         close(mm2[k], mm, tol=1e-6, what="moving mean")
@@ -846,16 +876,16 @@ def test_syncbn_two_replicas_equal_global_bn(L, M1, M2, C):
     close(y2, y, what="y")
     ls = [torch.empty(2 * C, dtype=torch.float64, device="cuda") for _ in parts]
     for (r0, m), s in zip(parts, ls):
-        L.check(lib.tde_bn_sums(m, C, L.ptr(z[r0:]), L.ptr(dy[r0:]), C, 0, L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta), 1,
-                                1, L.ptr(s), L.ptr(ws), ws.numel() * 4, st))
+        L.check(lib.tde_bn_sums(m, C, 1, L.ptr(z[r0:]), L.ptr(dy[r0:]), C, 0, L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta),
+                                1, 1, L.ptr(s), None, L.ptr(ws), ws.numel() * 4, st))
     gb = ls[0] + ls[1]
     dz2 = torch.empty(M, C, device="cuda")
     db2 = torch.empty(2, C, device="cuda")
     amax2 = torch.zeros(L.BOUND_SLOTS, device="cuda")
     for k, (r0, m) in enumerate(parts):
-        L.check(lib.tde_bn_bwd_from_sums(m, C, M, L.ptr(z[r0:]), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta),
+        L.check(lib.tde_bn_bwd_from_sums(m, C, 1, M, L.ptr(z[r0:]), L.ptr(sm[0]), L.ptr(sm[1]), L.ptr(beta),
                                          L.ptr(dy[r0:]), C, 0, L.ptr(gb), L.ptr(ls[k]), L.ptr(dz2[r0:]), L.ptr(db2[k]),
-                                         0, 1, L.ptr(amax2), L.ptr(ws), ws.numel() * 4, st))
+                                         0, 1, L.ptr(amax2), st))
     close(dz2, dz, what="dz")
     assert amax2.max().item() == dz2.abs().max().item(), "dz_absmax over both replicas' calls"
     close(db2[0] + db2[1], db, tol=1e-6, what="dbeta")

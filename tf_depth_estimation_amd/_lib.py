@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
@@ -37,7 +37,7 @@ class BnTrain(ctypes.Structure):
     """Mirror of tde_bn_train_t (include/tde.h): batch norm + ReLU fused behind a conv."""
     _fields_ = [("beta", P), ("eps", c_float), ("decay", c_float), ("bessel", c_int), ("moving_mean", P),
                 ("moving_var", P), ("save_mean", P), ("save_invstd", P), ("y", P), ("y_cstride", c_int),
-                ("y_coff", c_int), ("relu", c_int), ("groups", c_int)]
+                ("y_coff", c_int), ("relu", c_int), ("groups", c_int), ("sums", P)]
 
 
 class WarpLossArgs(ctypes.Structure):
@@ -140,11 +140,11 @@ _SIGS = {
                            P]),
     "tde_bias_relu_bwd": (c_int, [c_int, c_int, P, c_int, c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_size_t,
                                   P]),
-    "tde_bn_sums": (c_int, [c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, c_size_t, P]),
-    "tde_bn_fwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, c_float, c_float, c_int, P, P, P, P, P,
-                                     c_int, c_int, c_int, P]),
-    "tde_bn_bwd_from_sums": (c_int, [c_int, c_int, ctypes.c_long, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int,
-                                     c_int, P, P, c_size_t, P]),
+    "tde_bn_sums": (c_int, [c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, c_int, c_int, P, P, P, c_size_t, P]),
+    "tde_bn_fwd_from_sums": (c_int, [c_int, c_int, c_int, ctypes.c_long, P, P, P, c_float, c_float, c_int, P, P, P,
+                                     P, P, c_int, c_int, c_int, P]),
+    "tde_bn_bwd_from_sums": (c_int, [c_int, c_int, c_int, ctypes.c_long, P, P, P, P, P, c_int, c_int, P, P, P, P,
+                                     c_int, c_int, P, P]),
     "tde_resize_nearest_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_nearest_bwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "tde_resize_bilinear_fwd": (c_int, [c_int] * 4 + [P, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),

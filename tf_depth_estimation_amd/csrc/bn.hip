@@ -107,7 +107,8 @@ template <int MODE, int NT>
 __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int nparts, const double* part, float eps,
                                                          float decay, int bessel, float* mm, float* mv,
                                                          float* save_mean, float* save_invstd, float* dbeta,
-                                                         int acc, float* coef, double* sums = nullptr, int G = 1) {
+                                                         int acc, float* coef, double* sums = nullptr, int G = 1,
+                                                         double* sums2 = nullptr) {
   constexpr int FIN_ST = NT / 4, NWV = NT / 64;
   __shared__ double sh[2][NWV][4];
   const int cl = threadIdx.x & 3, st = threadIdx.x >> 2;
@@ -153,6 +154,7 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int npart
       if (MODE == 2) {   // raw per-channel sums (SyncBN: all-reduced by the caller, then *_from_sums)
         sums[(long)g * 2 * C + c] = s;
         sums[(long)g * 2 * C + C + c] = s2;
+        if (sums2) { sums2[(long)g * 2 * C + c] = s; sums2[(long)g * 2 * C + C + c] = s2; }
       } else if (MODE == 0) {
         const double mean = s / M;
         double var = s2 / M - mean * mean;
@@ -178,13 +180,84 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(int M, int C, int npart
   }
 }
 
+// SyncBN statistics of channels c..c+3 of row group g from the (all-reduced) sums [G][2][C] over Mt rows: fp64
+// mean / variance, rounded to fp32 once (the expressions publish_fwd stores, so every block applies the statistics
+// block 0 publishes).
+__device__ __forceinline__ void stats_from_sums(const double* sums, int C, int g, int c, double Mt, float eps,
+                                                f4& mu, f4& is) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double sv = sums[(long)g * 2 * C + c + j], s2 = sums[(long)g * 2 * C + C + c + j];
+    const double mean = sv / Mt;
+    double var = s2 / Mt - mean * mean;
+    if (var < 0) var = 0;
+    mu[j] = (float)mean;
+    is[j] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+}
+
+// What the SyncBN one-launch apply passes publish from block 0 (per row group, in group order): forward the batch
+// statistics and the moving averages, backward dbeta from this replica's own sums.
+struct SumsPub {
+  const double* sums;        // all-reduced [G][2][C]
+  const double* lsums;       // backward: this replica's [G][2][C] (dbeta)
+  double Mt;                 // rows per group over all replicas
+  float eps, decay;
+  int bessel, G, acc;
+  float *mm, *mv, *save_mean, *save_invstd, *dbeta;
+};
+
+__device__ __forceinline__ void publish_fwd(const SumsPub& P, int C, int c) {
+  float mm0[4] = {0, 0, 0, 0}, mv0[4] = {0, 0, 0, 0};
+  if (P.mm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { mm0[j] = P.mm[c + j]; mv0[j] = P.mv[c + j]; }
+  }
+  for (int g = 0; g < P.G; ++g) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double sv = P.sums[(long)g * 2 * C + c + j], s2 = P.sums[(long)g * 2 * C + C + c + j];
+      const double mean = sv / P.Mt;
+      double var = s2 / P.Mt - mean * mean;
+      if (var < 0) var = 0;
+      P.save_mean[(long)g * C + c + j] = (float)mean;
+      P.save_invstd[(long)g * C + c + j] = (float)(1.0 / sqrt(var + (double)P.eps));
+      if (P.mm) {
+        const double vu = (P.bessel && P.Mt > 1) ? var * P.Mt / (P.Mt - 1) : var;
+        mm0[j] -= (mm0[j] - (float)mean) * (1.f - P.decay);
+        mv0[j] -= (mv0[j] - (float)vu) * (1.f - P.decay);
+      }
+    }
+  }
+  if (P.mm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { P.mm[c + j] = mm0[j]; P.mv[c + j] = mv0[j]; }
+  }
+}
+
+__device__ __forceinline__ void publish_bwd(const SumsPub& P, int C, int c) {
+  if (!P.dbeta) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float db = P.acc ? P.dbeta[c + j] : 0.f;
+    for (int g = 0; g < P.G; ++g) {
+      const float l = (float)P.lsums[(long)g * 2 * C + c + j];
+      db = (g == 0 && !P.acc) ? l : db + l;
+    }
+    P.dbeta[c + j] = db;
+  }
+}
+
 // y = relu((z - mean) * invstd + beta): rows split over blocks, a thread owns one channel quad of a row
 // lane (no 64-bit division in the index math).
 // Row groups: rows [g*Mg, (g+1)*Mg) use the statistics at [g][C] (a thread moves to the next group's
 // statistics when its row walk crosses a group boundary).
+// SUMS (SyncBN, one launch instead of from-sums + apply): the statistics come from the all-reduced sums (P), and
+// block 0 publishes them and the moving averages.
+template <bool SUMS>
 __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float* z, const float* mean,
                                                        const float* invstd, const float* beta, int relu, float* y,
-                                                       int ycs, int yco, int rows_per_block, int Mg) {
+                                                       int ycs, int yco, int rows_per_block, int Mg, SumsPub P) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
   if (cq < 256 && threadIdx.x >= rstep * cq) return;
@@ -192,17 +265,27 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); qq < cq; qq += (cq >= 256 ? 256 : cq)) {
     const int c = 4 * qq;
+    if (SUMS && blockIdx.x == 0 && rl == 0) publish_fwd(P, C, c);
     int g = (r0 + rl) / Mg, gend = (g + 1) * Mg;
-    f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
-    f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+    f4 mu, is;
+    if (SUMS) {
+      stats_from_sums(P.sums, C, g, c, P.Mt, P.eps, mu, is);
+    } else {
+      mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+      is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+    }
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
 #pragma unroll 4
     for (int r = r0 + rl; r < r1; r += rstep) {
       if (r >= gend) {
         g = r / Mg;
         gend = (g + 1) * Mg;
-        mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
-        is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+        if (SUMS) {
+          stats_from_sums(P.sums, C, g, c, P.Mt, P.eps, mu, is);
+        } else {
+          mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+          is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+        }
       }
       const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
       f4 o;
@@ -233,10 +316,28 @@ __device__ __forceinline__ void block_absmax_to(float m, float* amax) {
   }
 }
 
+// coef = (mean g, mean g*xhat) of row group g: from the finalize's coef, or (SUMS) from the all-reduced sums over
+// P.Mt rows (fp64 quotient, one fp32 rounding)
+template <bool SUMS>
+__device__ __forceinline__ void bwd_coef(const float* coef, const SumsPub& P, int C, int g, int c, f4& mg, f4& mgx) {
+  if (SUMS) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mg[j] = (float)(P.sums[(long)g * 2 * C + c + j] / P.Mt);
+      mgx[j] = (float)(P.sums[(long)g * 2 * C + C + c + j] / P.Mt);
+    }
+  } else {
+    mg = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + c);
+    mgx = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + C + c);
+  }
+}
+
+template <bool SUMS>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const float* z, const float* dy, int dycs,
                                                            int dyco, const float* mean, const float* invstd,
                                                            const float* beta, const float* coef, int relu,
-                                                           float* dz, int rows_per_block, float* amax, int Mg) {
+                                                           float* dz, int rows_per_block, float* amax, int Mg,
+                                                           SumsPub P) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
   const bool active = cq >= 256 || threadIdx.x < rstep * cq;
@@ -245,12 +346,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
   float mx = 0.f;
   for (int qq = (cq >= 256 ? threadIdx.x : threadIdx.x % cq); active && qq < cq; qq += (cq >= 256 ? 256 : cq)) {
     const int c = 4 * qq;
+    if (SUMS && blockIdx.x == 0 && rl == 0) publish_bwd(P, C, c);
     int g = (r0 + rl) / Mg, gend = (g + 1) * Mg;
     f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
     f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
-    f4 mg = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + c);
-    f4 mgx = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + C + c);
+    f4 mg, mgx;
+    bwd_coef<SUMS>(coef, P, C, g, c, mg, mgx);
 #pragma unroll 4
     for (int r = r0 + rl; r < r1; r += rstep) {
       if (r >= gend) {
@@ -258,8 +360,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
         gend = (g + 1) * Mg;
         mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
         is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
-        mg = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + c);
-        mgx = *reinterpret_cast<const f4*>(coef + (long)g * 2 * C + C + c);
+        bwd_coef<SUMS>(coef, P, C, g, c, mg, mgx);
       }
       const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
       const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
@@ -275,36 +376,6 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
     }
   }
   block_absmax_to(mx, amax);
-}
-
-// SyncBN second phase: batch statistics from per-channel sums over ALL replicas (count Mt).
-// MODE 0: mean / invstd (+ moving averages) from (sum z, sum z^2).  MODE 1: coef = global (mean g,
-// mean g*xhat) from the all-reduced sums, dbeta from this replica's own sum g (the data-parallel gradient
-// average then divides the summed dbeta by the replica count, as for every other parameter).
-template <int MODE>
-__global__ void __launch_bounds__(256) bn_from_sums_kernel(int C, double Mt, const double* gsum, const double* lsum,
-                                                           float eps, float decay, int bessel, float* mm, float* mv,
-                                                           float* save_mean, float* save_invstd, float* dbeta,
-                                                           int acc, float* coef) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  const double s = gsum[c], s2 = gsum[C + c];
-  if (MODE == 0) {
-    const double mean = s / Mt;
-    double var = s2 / Mt - mean * mean;
-    if (var < 0) var = 0;
-    save_mean[c] = (float)mean;
-    save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (mm) {
-      const double vu = (bessel && Mt > 1) ? var * Mt / (Mt - 1) : var;
-      mm[c] -= (mm[c] - (float)mean) * (1.f - decay);
-      mv[c] -= (mv[c] - (float)vu) * (1.f - decay);
-    }
-  } else {
-    if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)lsum[c] : (float)lsum[c];
-    coef[c] = (float)(s / Mt);
-    coef[C + c] = (float)(s2 / Mt);
-  }
 }
 
 // ------------------------------------------------------------------ M <= 2048: one kernel
@@ -567,13 +638,13 @@ int finalize_blocks(int C) { return C / 4; }
 template <int MODE>
 void finalize_launch(int nparts, int C, hipStream_t st, int M, const double* part, float eps, float decay, int bessel,
                      float* mm, float* mv, float* save_mean, float* save_invstd, float* dbeta, int acc, float* coef,
-                     double* sums, int G = 1) {
+                     double* sums, int G = 1, double* sums2 = nullptr) {
   if (nparts / G <= 512)
     hipLaunchKernelGGL((bn_finalize_kernel<MODE, 256>), dim3(finalize_blocks(C)), dim3(256), 0, st, M, C, nparts, part,
-                       eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G);
+                       eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G, sums2);
   else
     hipLaunchKernelGGL((bn_finalize_kernel<MODE, 1024>), dim3(finalize_blocks(C)), dim3(1024), 0, st, M, C, nparts,
-                       part, eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G);
+                       part, eps, decay, bessel, mm, mv, save_mean, save_invstd, dbeta, acc, coef, sums, G, sums2);
 }
 
 }  // namespace
@@ -620,8 +691,15 @@ size_t bn_part_bytes(long M, int C) {
   return (size_t)n * 2 * C * sizeof(double);
 }
 
-void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream_t st) {
+void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, double* part, hipStream_t st) {
   const int G = o.groups > 1 ? o.groups : 1;
+  if (o.sums) {   // SyncBN phase 1: the grouped sums only
+    const BnChunks pp = bn_chunk_plan(M, C, 1, G);
+    hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0,
+                       nullptr, nullptr, nullptr, 0, pp, part);
+    bn_fwd_from_partials_launch(M, C, z, pp.chunks, part, o, st);
+    return;
+  }
   hipLaunchKernelGGL(bn_fwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay, o.bessel,
                      o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
 }
@@ -629,17 +707,22 @@ void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
                                  hipStream_t st) {
   const int G = o.groups > 1 ? o.groups : 1;
+  if (o.sums) {   // SyncBN phase 1: the per-group (sum z, sum z^2) for the caller's all-reduce; nothing applied
+    finalize_launch<2>(nparts, C, st, M / G, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                       nullptr, o.sums, G);
+    return;
+  }
   finalize_launch<0>(nparts, C, st, M / G, part, o.eps, o.decay, o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd,
                      nullptr, 0, nullptr, nullptr, G);
   const int rpb = apply_rows_per_block(M, C);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, o.save_mean,
-                     o.save_invstd, o.beta, o.relu, o.y, o.ycs, o.yco, rpb, M / G);
+  hipLaunchKernelGGL(bn_apply_kernel<false>, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, o.save_mean,
+                     o.save_invstd, o.beta, o.relu, o.y, o.ycs, o.yco, rpb, M / G, SumsPub{});
 }
 
 void bn_fwd_standalone_launch(int M, int C, const float* z, const BnOut& o, double* part, hipStream_t st) {
   const int G = o.groups > 1 ? o.groups : 1;
   if (M / G <= BN_SMALL_M) {
-    bn_fwd_small_launch(M, C, z, o, st);
+    bn_fwd_small_launch(M, C, z, o, part, st);
     return;
   }
   const BnChunks pp = bn_chunk_plan(M, C, 1, G);
@@ -712,21 +795,22 @@ int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean,
   finalize_launch<1>(pp.chunks, C, st, Mg, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta,
                      coef, nullptr, G);
   const int rpb = apply_rows_per_block(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax, Mg);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy,
+                     dy_cstride, dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax, Mg, SumsPub{});
   return tde_launch_status();
 }
 
 
-int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, int dy_coff, const float* save_mean,
-                const float* save_invstd, const float* beta, int relu, int mode, double* sums, void* ws,
-                size_t ws_bytes, void* stream) {
+int tde_bn_sums(int M, int C, int groups, const float* z, const float* dy, int dy_cstride, int dy_coff,
+                const float* save_mean, const float* save_invstd, const float* beta, int relu, int mode, double* sums,
+                double* sums_copy, void* ws, size_t ws_bytes, void* stream) {
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && sums && (mode == 0 || mode == 1));
+  TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(tde_aligned16(z) && (mode == 0 || (dy && save_mean && save_invstd && beta && tde_aligned16(dy) &&
                                                    dy_cstride % 4 == 0 && dy_coff % 4 == 0)));
   if (ws_bytes < tde_bn_workspace_size(M, C) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const BnChunks pp = bn_chunk_plan(M, C, 1);
+  const BnChunks pp = bn_chunk_plan(M, C, 1, groups);
   double* part = reinterpret_cast<double*>(tde_ws_body(ws));
   if (mode == 0)
     hipLaunchKernelGGL(bn_part_kernel<0>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, nullptr, 0, 0,
@@ -734,41 +818,43 @@ int tde_bn_sums(int M, int C, const float* z, const float* dy, int dy_cstride, i
   else
     hipLaunchKernelGGL(bn_part_kernel<1>, dim3(pp.chunks, pp.groups), dim3(256), 0, st, M, C, z, dy, dy_cstride,
                        dy_coff, save_mean, save_invstd, beta, relu, pp, part);
-  finalize_launch<2>(pp.chunks, C, st, M, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
-                     sums);
+  finalize_launch<2>(pp.chunks, C, st, M / groups, part, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                     nullptr, sums, groups, sums_copy);
   return tde_launch_status();
 }
 
-int tde_bn_fwd_from_sums(int M, int C, long M_total, const float* z, const double* sums, const float* beta, float eps,
-                         float decay, int bessel, float* moving_mean, float* moving_var, float* save_mean,
+int tde_bn_fwd_from_sums(int M, int C, int groups, long M_total, const float* z, const double* sums, const float* beta,
+                         float eps, float decay, int bessel, float* moving_mean, float* moving_var, float* save_mean,
                          float* save_invstd, float* y, int y_cstride, int y_coff, int relu, void* stream) {
-  TDE_CHECK_ARG(M > 0 && M_total >= M && C > 0 && C % 4 == 0 && z && sums && beta && save_mean && save_invstd && y);
+  TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0 && M_total >= M / groups);
+  TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && sums && beta && save_mean && save_invstd && y);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) &&
                 tde_aligned16(y) && (moving_mean == nullptr) == (moving_var == nullptr));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(bn_from_sums_kernel<0>, dim3((C + 255) / 256), dim3(256), 0, st, C, (double)M_total, sums,
-                     nullptr, eps, decay, bessel, moving_mean, moving_var, save_mean, save_invstd, nullptr, 0, nullptr);
+  SumsPub P{};
+  P.sums = sums; P.Mt = (double)M_total; P.eps = eps; P.decay = decay; P.bessel = bessel; P.G = groups;
+  P.mm = moving_mean; P.mv = moving_var; P.save_mean = save_mean; P.save_invstd = save_invstd;
   const int rpb = apply_rows_per_block(M, C);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, save_mean, save_invstd,
-                     beta, relu, y, y_cstride, y_coff, rpb, M);
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, nullptr, nullptr,
+                     beta, relu, y, y_cstride, y_coff, rpb, M / groups, P);
   return tde_launch_status();
 }
 
-int tde_bn_bwd_from_sums(int M, int C, long M_total, const float* z, const float* save_mean, const float* save_invstd,
-                         const float* beta, const float* dy, int dy_cstride, int dy_coff, const double* global_sums,
-                         const double* local_sums, float* dz, float* dbeta, int accumulate_dbeta, int relu,
-                         float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
-  TDE_CHECK_ARG(M > 0 && M_total >= M && C > 0 && C % 4 == 0 && z && save_mean && save_invstd && beta && dy && dz &&
+int tde_bn_bwd_from_sums(int M, int C, int groups, long M_total, const float* z, const float* save_mean,
+                         const float* save_invstd, const float* beta, const float* dy, int dy_cstride, int dy_coff,
+                         const double* global_sums, const double* local_sums, float* dz, float* dbeta,
+                         int accumulate_dbeta, int relu, float* dz_absmax, void* stream) {
+  TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0 && M_total >= M / groups);
+  TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && save_mean && save_invstd && beta && dy && dz &&
                 global_sums && local_sums);
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
-  if (ws_bytes < (size_t)2 * C * sizeof(float) || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  float* coef = reinterpret_cast<float*>(tde_ws_body(ws));
-  hipLaunchKernelGGL(bn_from_sums_kernel<1>, dim3((C + 255) / 256), dim3(256), 0, st, C, (double)M_total, global_sums,
-                     local_sums, 0.f, 0.f, 0, nullptr, nullptr, nullptr, nullptr, dbeta, accumulate_dbeta, coef);
+  SumsPub P{};
+  P.sums = global_sums; P.lsums = local_sums; P.Mt = (double)M_total; P.G = groups; P.acc = accumulate_dbeta;
+  P.dbeta = dbeta;
   const int rpb = apply_rows_per_block(M, C);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
-                     dy_coff, save_mean, save_invstd, beta, coef, relu, dz, rpb, dz_absmax, M);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3((M + rpb - 1) / rpb), dim3(256), 0, st, M, C, z, dy, dy_cstride,
+                     dy_coff, save_mean, save_invstd, beta, nullptr, relu, dz, rpb, dz_absmax, M / groups, P);
   return tde_launch_status();
 }
 

@@ -19,6 +19,7 @@ struct BnOut {
   float* y;
   int ycs, yco, relu;
   int groups;
+  double* sums = nullptr;   // SyncBN phase 1 (tde_bn_train_t.sums): the per-group sums only, nothing applied
 };
 
 // Row-chunk x 64-channel-group grid of the partial-statistics passes (bn.hip and the conv's split-K
@@ -39,7 +40,7 @@ __device__ __forceinline__ void bn_chunk_rows(const BnChunks& p, int k, int& r0,
 size_t bn_part_bytes(long M, int C);
 
 // Mg <= BN_SMALL_M: statistics + finalize + apply in one launch.
-void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, hipStream_t st);
+void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, double* part, hipStream_t st);
 // From `nparts` fp64 partials [part][2][C] of z (G | nparts, group-aligned): finalize (one small launch) + apply
 // (one launch).
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,

@@ -1637,9 +1637,9 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   span_mark(1, st);
   if (bn) {
-    const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
-                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
-    if (rows / G <= BN_SMALL_M) bn_fwd_small_launch((int)rows, d->C, a.y, o, st);
+    BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G, bn->sums};
+    if (rows / G <= BN_SMALL_M) bn_fwd_small_launch((int)rows, d->C, a.y, o, part, st);
     else if (epi) bn_fwd_from_partials_launch((int)rows, d->C, a.y, (int)(grid.x * grid.y), part, o, st);
     else bn_fwd_standalone_launch((int)rows, d->C, a.y, o, part, st);
   }
@@ -1683,8 +1683,8 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     if (!skip) halo_launch(hp, *d, in, a.w, z, accumulate, body, grouped_sa ? nullptr : part, st, a.bias, a.relu);
     span_mark(1, st);
     if (bn) {
-      const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
-                    bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
+      BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                    bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G, bn->sums};
       if (grouped_sa) bn_fwd_standalone_launch((int)Mz, hp.Ncols, z, o, part, st);
       else bn_fwd_from_partials_launch((int)Mz, hp.Ncols, z, hp.nparts, part, o, st);
     }
@@ -1716,10 +1716,10 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   span_mark(1, st);
   if (bn) {
     // slim.batch_norm + ReLU of z (nets_optflow_depth.py:82-87)
-    const BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
-                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G};
+    BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
+                  bn->save_invstd, bn->y, bn->y_cstride, bn->y_coff, bn->relu, G, bn->sums};
     if (bp.path == BN_SMALL) {
-      bn_fwd_small_launch(pl.rows, pl.cols, z, o, st);
+      bn_fwd_small_launch(pl.rows, pl.cols, z, o, part, st);
     } else if (bp.path == BN_STANDALONE) {
       bn_fwd_standalone_launch(pl.rows, pl.cols, z, o, part, st);
     } else {

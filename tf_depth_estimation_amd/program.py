@@ -702,26 +702,23 @@ class NetProgram:
                         _lib.check(fn(ctypes_ref(fd), run.vptr(op.src), ptr(wf), ptr(bf), 1, run.vptr(op.dst), ptr(ws),
                                       wsb, st), op.layer)
                 elif is_training and self.bn_sync is not None:
-                    # SyncBN: conv, local (sum z, sum z^2) per row group, ONE all-reduce of all groups' sums, then
-                    # each group normalised over its rows of all replicas (a twin run's left / right halves stay
-                    # separate BatchNorm batches, as the reference's two calls, train_depth_then_cam_lr.py:130-136)
-                    fn = lib.tde_deconv2d_fwd if op.deconv else lib.tde_conv2d_fwd
-                    _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), 0, ptr(ws), wsb, st), op.layer)
+                    # SyncBN: the conv writes its local (sum z, sum z^2) per row group from its own statistics
+                    # partials, ONE all-reduce of all groups' sums, then one apply launch normalises each group over its
+                    # rows of all replicas (a twin run's left / right halves stay separate BatchNorm batches, as the
+                    # reference's two calls, train_depth_then_cam_lr.py:130-136)
                     G = run.groups
                     Mg = M // G
                     sums = self._sums(i, op.K, 0, G)
-                    for g in range(G):
-                        _lib.check(lib.tde_bn_sums(Mg, op.K, ptr(z[g * (N // G):]), None, 0, 0, None, None, None, 0, 0,
-                                                   ptr(sums[g]), ptr(ws), wsb, st), op.layer + " bn sums")
+                    bn = _lib.BnTrain(ptr(beta), 1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
+                                      ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, G, ptr(sums))
+                    fn = lib.tde_deconv2d_fwd_bn if op.deconv else lib.tde_conv2d_fwd_bn
+                    _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb, st),
+                               op.layer + " bn sums")
                     (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(sums)
-                    ystride = Mg * op.dst.buf.cs * 4
-                    for g in range(G):
-                        _lib.check(lib.tde_bn_fwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(z[g * (N // G):]),
-                                                            ptr(sums[g]), ptr(beta), 1e-3, op.decay, int(self.bessel),
-                                                            ptr(mm), ptr(mv), ptr(sm[0][g * op.K:]),
-                                                            ptr(sm[1][g * op.K:]),
-                                                            ctypes.c_void_p(run.vptr(op.dst).value + g * ystride),
-                                                            op.dst.buf.cs, op.dst.coff, 1, st), op.layer + " syncbn")
+                    _lib.check(lib.tde_bn_fwd_from_sums(M, op.K, G, Mg * self.bn_world, ptr(z), ptr(sums), ptr(beta),
+                                                        1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
+                                                        ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st),
+                               op.layer + " syncbn")
                 elif is_training and self._production():
                     # conv + batch norm (batch statistics, moving averages) + ReLU: one ABI call; the BN pass
                     # consumes the conv's split-K partials directly (a GraphTimer times its conv kernels only)
@@ -910,32 +907,24 @@ class NetProgram:
                                                          ptr(self.G(f"{op.layer}/biases")), pacc, run.absmax_ptr(i),
                                                          ptr(ws), wsb, st), op.layer + " bias_relu_bwd")
                 elif self.bn_sync is not None:
-                    # SyncBN backward: local (sum g, sum g*xhat) per row group -> all-reduced copy -> dz from the global
-                    # means; dbeta from the local sums, groups added in order (the gradient all-reduce averages it like
-                    # every parameter)
+                    # SyncBN backward: local (sum g, sum g*xhat) per row group (one launch writes the copy to be
+                    # all-reduced and the local one) -> all-reduce -> dz from the global means in one launch; dbeta
+                    # from the local sums, groups added in order (the gradient all-reduce averages it like every
+                    # parameter)
                     G = run.groups
                     Mg = M // G
                     ls, gs = self._sums(i, op.K, 1, G), self._sums(i, op.K, 2, G)
                     beta = self.P(f"{op.layer}/BatchNorm/beta")
                     zi = run.z[i]
-                    dystride = Mg * op.dst.buf.cs * 4
-                    dyp = run.vptr(op.dst, True).value
-                    for g in range(G):
-                        _lib.check(lib.tde_bn_sums(Mg, op.K, ptr(zi[g * (N // G):]), ctypes.c_void_p(dyp + g * dystride),
-                                                   op.dst.buf.cs, op.dst.coff, ptr(sm[0][g * op.K:]),
-                                                   ptr(sm[1][g * op.K:]), ptr(beta), 1, 1, ptr(ls[g]), ptr(ws), wsb, st),
-                                   op.layer + " bn sums")
-                    gs.copy_(ls)
+                    dy = run.vptr(op.dst, True)
+                    _lib.check(lib.tde_bn_sums(M, op.K, G, ptr(zi), dy, op.dst.buf.cs, op.dst.coff, ptr(sm[0]),
+                                               ptr(sm[1]), ptr(beta), 1, 1, ptr(gs), ptr(ls), ptr(ws), wsb, st),
+                               op.layer + " bn sums")
                     (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(gs)
-                    for g in range(G):
-                        _lib.check(lib.tde_bn_bwd_from_sums(Mg, op.K, Mg * self.bn_world, ptr(zi[g * (N // G):]),
-                                                            ptr(sm[0][g * op.K:]), ptr(sm[1][g * op.K:]), ptr(beta),
-                                                            ctypes.c_void_p(dyp + g * dystride), op.dst.buf.cs,
-                                                            op.dst.coff, ptr(gs[g]), ptr(ls[g]),
-                                                            ptr(dz[g * Mg * op.K:]),
-                                                            ptr(self.G(f"{op.layer}/BatchNorm/beta")),
-                                                            pacc if g == 0 else 1, 1, run.absmax_ptr(i), ptr(ws), wsb,
-                                                            st), op.layer + " syncbn bwd")
+                    _lib.check(lib.tde_bn_bwd_from_sums(M, op.K, G, Mg * self.bn_world, ptr(zi), ptr(sm[0]), ptr(sm[1]),
+                                                        ptr(beta), dy, op.dst.buf.cs, op.dst.coff, ptr(gs), ptr(ls),
+                                                        ptr(dz), ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,
+                                                        run.absmax_ptr(i), st), op.layer + " syncbn bwd")
                 else:
                     with self._span("bn_bwd"):
                         _lib.check(lib.tde_bn_bwd(M, op.K, run.groups, ptr(run.z[i]), ptr(sm[0]), ptr(sm[1]),
