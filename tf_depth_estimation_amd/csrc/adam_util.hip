@@ -1,6 +1,8 @@
 // TF Adam over one flat parameter buffer (tf.train.AdamOptimizer, train_depth_then_cam_lr.py:413-417;
 // TF ApplyAdam kernel: m += (g-m)(1-b1); v += (g*g-v)(1-b2); var -= lr_t*m/(sqrt(v)+eps)) plus small
 // utilities.  Adam is HBM-bound: 4 reads + 3 writes of 4 B per parameter, 16-byte vectors.
+#include <cstdio>
+
 #include "tde_common.h"
 
 namespace {
@@ -84,6 +86,8 @@ int ew_grid(long n) {
 
 }  // namespace
 
+thread_local int tde_g_last_hip = 0;
+
 extern "C" {
 
 int tde_abi_version(void) { return TDE_ABI_VERSION; }
@@ -93,7 +97,12 @@ const char* tde_status_string(int s) {
     case TDE_OK: return "ok";
     case TDE_ERR_ARG: return "invalid argument (pointer, alignment or shape)";
     case TDE_ERR_WORKSPACE: return "workspace too small";
-    case TDE_ERR_HIP: return "HIP launch error";
+    case TDE_ERR_HIP: {
+      static thread_local char buf[160];
+      snprintf(buf, sizeof(buf), "HIP launch error: %s",
+               hipGetErrorName(static_cast<hipError_t>(tde_g_last_hip)));
+      return buf;
+    }
     case TDE_ERR_UNSUPPORTED: return "unsupported configuration";
     default: return "unknown status";
   }

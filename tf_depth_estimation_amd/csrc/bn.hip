@@ -379,141 +379,179 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
 }
 
 // ------------------------------------------------------------------ M <= 2048: one kernel
-// Block = one channel quad; each lane keeps its <= 8 rows in registers between the statistics and the
-// apply (fp32 per lane, fp64 across lanes, fixed-order wave/LDS combine).
+// Block = one channel quad; each lane keeps its <= 8 rows per group in registers between the statistics and the
+// apply (fp32 per lane, fp64 across lanes, fixed-order wave/LDS combine).  GT row groups are in flight at once (all
+// their loads issued before the first reduction, one barrier round for all of them): a twin run's two groups cost
+// one load -> reduce -> apply latency chain instead of two.  The moving averages and dbeta still take the groups'
+// values in group order (one thread per channel walks them).
 constexpr int SMALL_R = BN_SMALL_M / 256;
 
+template <int GT>
 __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const float* z, const float* beta, float eps,
                                                            float decay, int bessel, float* mm, float* mv,
                                                            float* save_mean, float* save_invstd, float* y, int ycs,
                                                            int yco, int relu, int G) {
-  // M = rows per group (<= BN_SMALL_M); the G groups run one after the other in the block
-  __shared__ double sh[2][4][4];
-  __shared__ float s_mu[4], s_is[4];
+  // M = rows per group (<= BN_SMALL_M); groups g0 .. g0+GT-1 together, G / GT rounds one after the other
+  __shared__ double sh[GT][2][4][4];
+  __shared__ float s_mu[GT][4], s_is[GT][4];
   const int c = bn_quad_block() * 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // beta and the moving averages loaded up front (off the reduce -> publish -> apply chain)
   const f4 bt = *reinterpret_cast<const f4*>(beta + c);
   float mm0 = 0.f, mv0 = 0.f;
   if (threadIdx.x < 4 && mm) { mm0 = mm[c + threadIdx.x]; mv0 = mv[c + threadIdx.x]; }
-  for (int g = 0; g < G; ++g) {
-    const float* zg = z + (long)g * M * C;
-    f4 v[SMALL_R];
-    float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
+  for (int g0 = 0; g0 < G; g0 += GT) {
+    f4 v[GT][SMALL_R];
+    float fa[GT][4], fb[GT][4];
 #pragma unroll
-    for (int i = 0; i < SMALL_R; ++i) {
-      const int r = threadIdx.x + 256 * i;
-      v[i] = r < M ? *reinterpret_cast<const f4*>(zg + (long)r * C + c) : f4{0, 0, 0, 0};
+    for (int k = 0; k < GT; ++k) {
+      const float* zg = z + (long)(g0 + k) * M * C;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { fa[j] += v[i][j]; fb[j] += v[i][j] * v[i][j]; }
+      for (int j = 0; j < 4; ++j) fa[k][j] = fb[k][j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < SMALL_R; ++i) {
+        const int r = threadIdx.x + 256 * i;
+        v[k][i] = r < M ? *reinterpret_cast<const f4*>(zg + (long)r * C + c) : f4{0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { fa[k][j] += v[k][i][j]; fb[k][j] += v[k][i][j] * v[k][i][j]; }
+      }
     }
-    if (g > 0) __syncthreads();          // the previous group's apply has read s_mu / s_is
+    if (g0 > 0) __syncthreads();          // the previous round's apply has read s_mu / s_is
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
-      if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
+    for (int k = 0; k < GT; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double a = wave_sum_d((double)fa[k][j]), b = wave_sum_d((double)fb[k][j]);
+        if (lane == 0) { sh[k][0][wv][j] = a; sh[k][1][wv][j] = b; }
+      }
     }
     __syncthreads();
     if (threadIdx.x < 4) {
       const int j = threadIdx.x, cc = c + j;
-      const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
-      const double s2 = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
-      const double mean = s / M;
-      double var = s2 / M - mean * mean;
-      if (var < 0) var = 0;
-      const float mu = (float)mean, is = (float)(1.0 / sqrt(var + (double)eps));
-      s_mu[j] = mu; s_is[j] = is;
-      save_mean[(long)g * C + cc] = mu;
-      save_invstd[(long)g * C + cc] = is;
-      if (mm) {
-        const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
-        mm0 = mm0 - (mm0 - mu) * (1.f - decay);
-        mv0 = mv0 - (mv0 - (float)vu) * (1.f - decay);
+#pragma unroll
+      for (int k = 0; k < GT; ++k) {
+        const double s = ((sh[k][0][0][j] + sh[k][0][1][j]) + sh[k][0][2][j]) + sh[k][0][3][j];
+        const double s2 = ((sh[k][1][0][j] + sh[k][1][1][j]) + sh[k][1][2][j]) + sh[k][1][3][j];
+        const double mean = s / M;
+        double var = s2 / M - mean * mean;
+        if (var < 0) var = 0;
+        const float mu = (float)mean, is = (float)(1.0 / sqrt(var + (double)eps));
+        s_mu[k][j] = mu; s_is[k][j] = is;
+        save_mean[(long)(g0 + k) * C + cc] = mu;
+        save_invstd[(long)(g0 + k) * C + cc] = is;
+        if (mm) {
+          const double vu = (bessel && M > 1) ? var * M / (M - 1) : var;
+          mm0 = mm0 - (mm0 - mu) * (1.f - decay);
+          mv0 = mv0 - (mv0 - (float)vu) * (1.f - decay);
+        }
       }
     }
     __syncthreads();
-    float* yg = y + (long)g * M * ycs;
 #pragma unroll
-    for (int i = 0; i < SMALL_R; ++i) {
-      const int r = threadIdx.x + 256 * i;
-      if (r < M) {
-        f4 o;
+    for (int k = 0; k < GT; ++k) {
+      float* yg = y + (long)(g0 + k) * M * ycs;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float t = (v[i][j] - s_mu[j]) * s_is[j] + bt[j];
-          o[j] = (relu && t < 0.f) ? 0.f : t;
+      for (int i = 0; i < SMALL_R; ++i) {
+        const int r = threadIdx.x + 256 * i;
+        if (r < M) {
+          f4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float t = (v[k][i][j] - s_mu[k][j]) * s_is[k][j] + bt[j];
+            o[j] = (relu && t < 0.f) ? 0.f : t;
+          }
+          tde_st(reinterpret_cast<f4*>(yg + (long)r * ycs + yco + c), o);
         }
-        tde_st(reinterpret_cast<f4*>(yg + (long)r * ycs + yco + c), o);
       }
     }
   }
   if (threadIdx.x < 4 && mm) { mm[c + threadIdx.x] = mm0; mv[c + threadIdx.x] = mv0; }
 }
 
+template <int GT>
 __global__ void __launch_bounds__(256) bn_bwd_small_kernel(int M, int C, const float* z, const float* mean,
                                                            const float* invstd, const float* beta, const float* dy,
                                                            int dycs, int dyco, float* dz, float* dbeta, int acc,
                                                            int relu, float* amax, int G) {
-  // M = rows per group (<= BN_SMALL_M); the G groups run one after the other in the block; dbeta takes the
-  // groups' sums in group order (the first overwrites unless accumulating)
-  __shared__ double sh[2][4][4];
-  __shared__ float s_mg[4], s_mgx[4];
+  // M = rows per group (<= BN_SMALL_M); groups g0 .. g0+GT-1 together; dbeta takes the groups' sums in group
+  // order (the first overwrites unless accumulating)
+  __shared__ double sh[GT][2][4][4];
+  __shared__ float s_mg[GT][4], s_mgx[GT][4];
   const int c = bn_quad_block() * 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const f4 bt = *reinterpret_cast<const f4*>(beta + c);
   float db = (threadIdx.x < 4 && dbeta && acc) ? dbeta[c + threadIdx.x] : 0.f;
   bool first = !acc;
   float mx = 0.f;
-  for (int g = 0; g < G; ++g) {
-    const f4 mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
-    const f4 is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
-    const long row0 = (long)g * M;
-    f4 xr[SMALL_R], gr[SMALL_R];
-    float fa[4] = {0, 0, 0, 0}, fb[4] = {0, 0, 0, 0};
+  for (int g0 = 0; g0 < G; g0 += GT) {
+    f4 mu[GT], is[GT];
+    f4 xr[GT][SMALL_R], gr[GT][SMALL_R];
+    float fa[GT][4], fb[GT][4];
 #pragma unroll
-    for (int i = 0; i < SMALL_R; ++i) {
-      const int r = threadIdx.x + 256 * i;
-      xr[i] = f4{0, 0, 0, 0}; gr[i] = f4{0, 0, 0, 0};
-      if (r < M) {
-        const f4 v = *reinterpret_cast<const f4*>(z + (row0 + r) * C + c);
-        const f4 gv = *reinterpret_cast<const f4*>(dy + (row0 + r) * dycs + dyco + c);
+    for (int k = 0; k < GT; ++k) {
+      mu[k] = *reinterpret_cast<const f4*>(mean + (long)(g0 + k) * C + c);
+      is[k] = *reinterpret_cast<const f4*>(invstd + (long)(g0 + k) * C + c);
+    }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xh = (v[j] - mu[j]) * is[j];
-          const float gg = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
-          xr[i][j] = xh; gr[i][j] = gg;
-          fa[j] += gg; fb[j] += gg * xh;
+    for (int k = 0; k < GT; ++k) {
+      const long row0 = (long)(g0 + k) * M;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fa[k][j] = fb[k][j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < SMALL_R; ++i) {
+        const int r = threadIdx.x + 256 * i;
+        xr[k][i] = f4{0, 0, 0, 0}; gr[k][i] = f4{0, 0, 0, 0};
+        if (r < M) {
+          const f4 v = *reinterpret_cast<const f4*>(z + (row0 + r) * C + c);
+          const f4 gv = *reinterpret_cast<const f4*>(dy + (row0 + r) * dycs + dyco + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xh = (v[j] - mu[k][j]) * is[k][j];
+            const float gg = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
+            xr[k][i][j] = xh; gr[k][i][j] = gg;
+            fa[k][j] += gg; fb[k][j] += gg * xh;
+          }
         }
       }
     }
-    if (g > 0) __syncthreads();          // the previous group's apply has read s_mg / s_mgx
+    if (g0 > 0) __syncthreads();          // the previous round's apply has read s_mg / s_mgx
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double a = wave_sum_d((double)fa[j]), b = wave_sum_d((double)fb[j]);
-      if (lane == 0) { sh[0][wv][j] = a; sh[1][wv][j] = b; }
+    for (int k = 0; k < GT; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double a = wave_sum_d((double)fa[k][j]), b = wave_sum_d((double)fb[k][j]);
+        if (lane == 0) { sh[k][0][wv][j] = a; sh[k][1][wv][j] = b; }
+      }
     }
     __syncthreads();
     if (threadIdx.x < 4) {
       const int j = threadIdx.x;
-      const double s = ((sh[0][0][j] + sh[0][1][j]) + sh[0][2][j]) + sh[0][3][j];
-      const double sx = ((sh[1][0][j] + sh[1][1][j]) + sh[1][2][j]) + sh[1][3][j];
-      s_mg[j] = (float)(s / M);
-      s_mgx[j] = (float)(sx / M);
-      db = first ? (float)s : db + (float)s;
-      first = false;
+#pragma unroll
+      for (int k = 0; k < GT; ++k) {
+        const double s = ((sh[k][0][0][j] + sh[k][0][1][j]) + sh[k][0][2][j]) + sh[k][0][3][j];
+        const double sx = ((sh[k][1][0][j] + sh[k][1][1][j]) + sh[k][1][2][j]) + sh[k][1][3][j];
+        s_mg[k][j] = (float)(s / M);
+        s_mgx[k][j] = (float)(sx / M);
+        db = first ? (float)s : db + (float)s;
+        first = false;
+      }
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < SMALL_R; ++i) {
-      const int r = threadIdx.x + 256 * i;
-      if (r < M) {
-        f4 o;
+    for (int k = 0; k < GT; ++k) {
+      const long row0 = (long)(g0 + k) * M;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          o[j] = is[j] * (gr[i][j] - s_mg[j] - xr[i][j] * s_mgx[j]);
-          mx = fmaxf(mx, fabsf(o[j]));
+      for (int i = 0; i < SMALL_R; ++i) {
+        const int r = threadIdx.x + 256 * i;
+        if (r < M) {
+          f4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            o[j] = is[k][j] * (gr[k][i][j] - s_mg[k][j] - xr[k][i][j] * s_mgx[k][j]);
+            mx = fmaxf(mx, fabsf(o[j]));
+          }
+          tde_st(reinterpret_cast<f4*>(dz + (row0 + r) * C + c), o);
         }
-        tde_st(reinterpret_cast<f4*>(dz + (row0 + r) * C + c), o);
       }
     }
   }
@@ -700,8 +738,12 @@ void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, double* p
     bn_fwd_from_partials_launch(M, C, z, pp.chunks, part, o, st);
     return;
   }
-  hipLaunchKernelGGL(bn_fwd_small_kernel, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay, o.bessel,
-                     o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
+  if (G % 2 == 0)
+    hipLaunchKernelGGL(bn_fwd_small_kernel<2>, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay,
+                       o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
+  else
+    hipLaunchKernelGGL(bn_fwd_small_kernel<1>, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay,
+                       o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
 }
 
 void bn_fwd_from_partials_launch(int M, int C, const float* z, int nparts, const double* part, const BnOut& o,
@@ -783,8 +825,12 @@ int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean,
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int G = groups, Mg = M / groups;
   if (Mg <= BN_SMALL_M) {
-    hipLaunchKernelGGL(bn_bwd_small_kernel, dim3(C / 4), dim3(256), 0, st, Mg, C, z, save_mean, save_invstd, beta, dy,
-                       dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax, G);
+    if (G % 2 == 0)
+      hipLaunchKernelGGL(bn_bwd_small_kernel<2>, dim3(C / 4), dim3(256), 0, st, Mg, C, z, save_mean, save_invstd, beta,
+                         dy, dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax, G);
+    else
+      hipLaunchKernelGGL(bn_bwd_small_kernel<1>, dim3(C / 4), dim3(256), 0, st, Mg, C, z, save_mean, save_invstd, beta,
+                         dy, dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax, G);
     return tde_launch_status();
   }
   const BnChunks pp = bn_chunk_plan(M, C, 1, G);

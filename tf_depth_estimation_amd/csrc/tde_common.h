@@ -12,9 +12,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
     if (!(cond)) return TDE_ERR_ARG;   \
   } while (0)
 
+// the HIP error behind the calling thread's last TDE_ERR_HIP (named by tde_status_string)
+extern thread_local int tde_g_last_hip;
+
+// hipErrorNotReady is not a launch failure: HIP records it as the thread's last error when another library in the
+// same thread (the framework's allocator, the collective layer) queries an event that has not completed yet.
 static inline int tde_launch_status() {
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? TDE_OK : TDE_ERR_HIP;
+  if (e == hipSuccess || e == hipErrorNotReady) return TDE_OK;
+  tde_g_last_hip = (int)e;
+  return TDE_ERR_HIP;
 }
 
 static inline bool tde_aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
