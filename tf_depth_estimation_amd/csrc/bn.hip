@@ -4,8 +4,9 @@
 //
 // At the shapes of the reference nets these passes are launch-latency bound (~5 us per kernel on
 // MI355X) or per-CU-bandwidth bound, so:
-//   M <= 2048 rows (the deep levels): ONE kernel per direction; a block owns one channel quad over all
-//     rows (row values held in registers), statistics, finalize, moving averages and apply in place.
+//   M <= BN_SMALL_M = 512 rows per group (the deepest levels): ONE kernel per direction; a block owns one channel
+//     quad over all rows (row values held in registers), statistics, finalize, moving averages and apply in place.
+//     (512, not 2048: the partial-sum path's wider grids measured +0.5 % on the config-4 step, round 4.)
 //   larger M, forward: the statistics partials come from the producing conv (its epilogue or its
 //     split-K reduce, conv_igemm.hip) -- or from bn_part_kernel for the standalone entry point -- then a
 //     finalize launch and an apply launch.
@@ -23,7 +24,7 @@
 
 namespace {
 
-// channel-quad block of the M <= 2048 forward / backward kernels: XCD-contiguous, so the 8 quads of one 128-byte
+// channel-quad block of the M <= BN_SMALL_M forward / backward kernels: XCD-contiguous, so the 8 quads of one 128-byte
 // row line share an L2 (rocprofv3, config 2: bn_fwd_small 6.41 -> 5.27 us, bn_bwd_small 8.90 -> 7.67 us; the
 // finalize kernel, 32-byte fp64 pieces, was neutral-to-slower and keeps hardware order).  TDE_BN_XCD=0: hardware
 // order everywhere, for A/B builds.
@@ -378,13 +379,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
   block_absmax_to(mx, amax);
 }
 
-// ------------------------------------------------------------------ M <= 2048: one kernel
-// Block = one channel quad; each lane keeps its <= 8 rows per group in registers between the statistics and the
+// ------------------------------------------------------------------ M <= BN_SMALL_M (512): one kernel
+// Block = one channel quad; each lane keeps its <= BN_SMALL_M / 256 rows per group in registers between the statistics and the
 // apply (fp32 per lane, fp64 across lanes, fixed-order wave/LDS combine).  GT row groups are in flight at once (all
 // their loads issued before the first reduction, one barrier round for all of them): a twin run's two groups cost
 // one load -> reduce -> apply latency chain instead of two.  The moving averages and dbeta still take the groups'
 // values in group order (one thread per channel walks them).
 constexpr int SMALL_R = BN_SMALL_M / 256;
+#ifndef TDE_SMALL_GT2   // diagnostic A/B build flag: 0 = one row group in flight (the round-3 kernels)
+#define TDE_SMALL_GT2 1
+#endif
 
 template <int GT>
 __global__ void __launch_bounds__(256) bn_fwd_small_kernel(int M, int C, const float* z, const float* beta, float eps,
@@ -738,7 +742,7 @@ void bn_fwd_small_launch(int M, int C, const float* z, const BnOut& o, double* p
     bn_fwd_from_partials_launch(M, C, z, pp.chunks, part, o, st);
     return;
   }
-  if (G % 2 == 0)
+  if (G % 2 == 0 && TDE_SMALL_GT2)
     hipLaunchKernelGGL(bn_fwd_small_kernel<2>, dim3(C / 4), dim3(256), 0, st, M / G, C, z, o.beta, o.eps, o.decay,
                        o.bessel, o.mm, o.mv, o.save_mean, o.save_invstd, o.y, o.ycs, o.yco, o.relu, G);
   else
@@ -825,7 +829,7 @@ int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean,
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int G = groups, Mg = M / groups;
   if (Mg <= BN_SMALL_M) {
-    if (G % 2 == 0)
+    if (G % 2 == 0 && TDE_SMALL_GT2)
       hipLaunchKernelGGL(bn_bwd_small_kernel<2>, dim3(C / 4), dim3(256), 0, st, Mg, C, z, save_mean, save_invstd, beta,
                          dy, dy_cstride, dy_coff, dz, dbeta, accumulate_dbeta, relu, dz_absmax, G);
     else

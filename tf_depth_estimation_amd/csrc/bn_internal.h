@@ -4,7 +4,10 @@
 #pragma once
 #include "tde_common.h"
 
-constexpr int BN_SMALL_M = 2048;   // rows (per row group) of the single-kernel BN path
+#ifndef TDE_BN_SMALL_M   // diagnostic A/B build flag
+#define TDE_BN_SMALL_M 512
+#endif
+constexpr int BN_SMALL_M = TDE_BN_SMALL_M;   // rows (per row group) of the single-kernel BN path
 constexpr int BN_MAX_GROUPS = 8;   // row groups of a grouped BN (tde_bn_train_t.groups)
 
 // What a training-mode BN forward writes: statistics, moving averages (mm/mv null: no update) and
