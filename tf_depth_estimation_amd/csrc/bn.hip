@@ -664,12 +664,18 @@ int ew_grid(long n) {
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
 
-// apply grid: ~8 rows per row lane, <= 2048 blocks
+// apply grid: ~8 rows per row lane, <= 2048 blocks (diagnostic A/B build flags TDE_APPLY_RPL / TDE_APPLY_MAXB)
+#ifndef TDE_APPLY_RPL
+#define TDE_APPLY_RPL 8
+#endif
+#ifndef TDE_APPLY_MAXB
+#define TDE_APPLY_MAXB 2048
+#endif
 int apply_rows_per_block(int M, int C) {
   const int cq = C / 4;
   const int rstep = cq >= 256 ? 1 : 256 / cq;
-  long rpb = (long)rstep * 8;
-  if ((M + rpb - 1) / rpb > 2048) rpb = (M + 2047) / 2048;
+  long rpb = (long)rstep * TDE_APPLY_RPL;
+  if ((M + rpb - 1) / rpb > TDE_APPLY_MAXB) rpb = (M + TDE_APPLY_MAXB - 1) / TDE_APPLY_MAXB;
   rpb = (rpb + rstep - 1) / rstep * rstep;
   return (int)rpb;
 }
