@@ -404,7 +404,7 @@ long env_l(const char* name, long dflt) {
   return v ? atol(v) : dflt;
 }
 const long g_halo = env_l("TDE_HALO", 1);                 // 0: never take the halo path (A/B)
-const long g_halo_min_m = tde_env_pos("TDE_HALO_MIN_M", 16384); // output pixels (N*H*W) from which it pays
+const long g_halo_min_m = tde_env_pos("TDE_HALO_MIN_M", 8192);  // output pixels (N*H*W) from which it pays (r04: 16384 -> 8192, +0.5 %)
 const long g_halo_nw = env_l("TDE_HALO_NW", 0);           // force 4 or 8 waves per block
 const long g_halo_lds = tde_env_pos("TDE_HALO_LDS_KB", 150) << 10;
 const long g_halo_minch = tde_env_pos("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
