@@ -213,6 +213,68 @@ def test_config4_forward_benched_batch():
     assert abs(parts["consist"] - val(rparts["consist"])) <= 1e-4 * val(rparts["consist"]) + 1e-9
 
 
+@pytest.mark.timeout(900)
+def test_config4_step_benched_batch():
+    """The benched step's BACKWARD at its exact shape: config 4 at per-GPU batch 8, 192x256,
+    twin-batched (disp_net once over [left; right], depth_net once over [concat(L,R); concat(R,L)], grouped BN),
+    bench.py's N = 1 schedule (depth_net's filter gradients on their side stream, the two networks on two streams),
+    against the fp64 oracle's four separate calls (train_depth_then_cam_lr.py:123-154,355,413-417): the whole
+    gradient vector within max(1e-3, 8 x the fp32 oracle's error), and per tensor the heads (disp*, exp/mask*),
+    pose/pred and pose/cam_cnv7 within max(1e-3, 8 x fp32 error, 8 x the conditioning probe)."""
+    from tf_depth_estimation_amd import train
+    B, H, W = 8, 192, 256
+    tr = train.DepthThenCamTrainer(B, H, W)
+    assert tr.twin and tr.runs["s"].groups == 2 and tr.runs["p"].groups == 2
+    tr.enable_wgrad_overlap(only=["pair"])
+    tr.enable_net_overlap()
+    il, ir = texture(B, H, W, 61), texture(B, H, W, 62)
+    g = np.random.default_rng(63)
+    lab = g.uniform(0.1, 2.0, (B, H, W, 1))
+    lab[g.uniform(size=lab.shape) < 0.05] = np.nan
+    lab = torch.tensor(lab, dtype=torch.float32)
+    K = intrinsics(B, H, W)
+    gt = small_pose(B, 64)
+    tr.set_batch(il.cuda(), ir.cuda(), lab.cuda(), K.cuda(), gt.cuda())
+    chunks = {"s": tr.single.chunk, "p": tr.pair.chunk}
+    Ps = {dt: (oracle_params_from(chunks["s"], "", dt), oracle_params_from(chunks["p"], "", dt))
+          for dt in (torch.float64, torch.float32)}
+    Ps["pert"] = (perturbed(oracle_params_from(chunks["s"], "", torch.float64)),
+                  perturbed(oracle_params_from(chunks["p"], "", torch.float64), 78))
+    tr.phase_compute()
+    torch.cuda.synchronize()
+    parts = tr.loss_parts()
+    gpu = {}
+    for c in chunks.values():
+        gpu.update({k: c.grad_view(k).detach().cpu().clone() for k in c.names()})
+    grads = {}
+    for key, (Pss, Ppp) in Ps.items():
+        dt = torch.float64 if key == "pert" else key
+        x = {k: v.to(dt) for k, v in dict(il=il, ir=ir).items()}
+        dsl = ON.disp_net(Pss, x["il"], True, scope="model_singledepth/depth_net")
+        dsr = ON.disp_net(Pss, x["ir"], True, scope="model_singledepth/depth_net")
+        dpl, pr, ml = ON.depth_net(Ppp, torch.cat([x["il"], x["ir"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        dpr, pl, mr = ON.depth_net(Ppp, torch.cat([x["ir"], x["il"]], -1), True,
+                                   scope="model_pairdepth/depth_cam_net", levels=4)
+        total, rparts = OL.loss_depth_then_cam_lr(dsl, dsr, dpl, dpr, pr, pl, ml, mr, x["il"], x["ir"], lab.to(dt),
+                                                  K.to(dt), gt.to(dt))
+        if key is torch.float64:
+            def val(t):
+                return t.item() if torch.is_tensor(t) else float(t)
+            for k in ("smooth", "depth", "exp", "cam"):
+                assert abs(parts[k] - val(rparts[k])) <= 1e-5 * abs(val(rparts[k])) + 1e-9, k
+            assert abs(parts["photo"] - val(rparts["pixel"])) <= 1e-5 * val(rparts["pixel"]) + 1e-9
+            assert abs(parts["consist"] - val(rparts["consist"])) <= 1e-4 * val(rparts["consist"]) + 1e-9
+        total.backward()
+        grads[key] = {k: v.grad for P in (Pss, Ppp) for k, v in P.vars.items()}
+        del dsl, dsr, dpl, dpr, pr, pl, ml, mr, total
+    check_grads_global(gpu, grads[torch.float64], grads[torch.float32], FACTOR)
+    names = check_per_tensor(gpu, grads[torch.float64], grads[torch.float32],
+                             ["model_singledepth/depth_net/disp", "model_pairdepth/depth_cam_net/disp",
+                              "pose/pred", "pose/cam_cnv7/weights", "exp/mask"], grads["pert"])
+    assert len(names) >= 26
+
+
 def test_config3_step_full_resolution():
     """Config 3 (train_optflow_combine.py:97-240) at 192x256, batch 4 of the per-GPU 32."""
     from tf_depth_estimation_amd import train

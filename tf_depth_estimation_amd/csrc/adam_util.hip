@@ -109,6 +109,7 @@ const char* tde_status_string(int s) {
 }
 
 int tde_adam_step_begin(float* step, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(step != nullptr);
   hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), step);
   return tde_launch_status();
@@ -116,6 +117,7 @@ int tde_adam_step_begin(float* step, void* stream) {
 
 int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* v, const float* step, float lr,
                     float beta1, float beta2, float eps, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(n % 4 == 0 && param && grad && m && v && step);
   TDE_CHECK_ARG(tde_aligned16(param) && tde_aligned16(grad) && tde_aligned16(m) && tde_aligned16(v));
   const long n4 = (long)(n / 4);
@@ -126,6 +128,7 @@ int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* 
 }
 
 int tde_zero_bytes(size_t bytes, void* p, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(p != nullptr);
   if (bytes == 0) return TDE_OK;
   // a kernel of our own, not hipMemsetAsync: a captured step then holds kernel nodes only (the runtime's
@@ -139,6 +142,7 @@ int tde_zero_bytes(size_t bytes, void* p, void* stream) {
 }
 
 int tde_spatial_mean_fwd(int N, int HW, int C, const float* x, int x_cstride, float* y, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && HW > 0 && C > 0 && x && y);
   hipLaunchKernelGGL(spatial_mean_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, HW, C, x, x_cstride, y);
@@ -147,6 +151,7 @@ int tde_spatial_mean_fwd(int N, int HW, int C, const float* x, int x_cstride, fl
 
 int tde_spatial_mean_bwd(int N, int HW, int C, float* dx, int dx_cstride, int accumulate, const float* dy,
                          void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && HW > 0 && C > 0 && dx && dy);
   hipLaunchKernelGGL(spatial_mean_bwd_kernel, dim3(ew_grid((long)N * HW * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, HW, C, dx, dx_cstride, accumulate, dy);
@@ -154,6 +159,7 @@ int tde_spatial_mean_bwd(int N, int HW, int C, float* dx, int dx_cstride, int ac
 }
 
 int tde_scale(size_t n, float* x, float alpha, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(x != nullptr);
   hipLaunchKernelGGL(scale_kernel, dim3(ew_grid((long)n)), dim3(256), 0, static_cast<hipStream_t>(stream), (long)n, x,
                      alpha);
@@ -161,6 +167,7 @@ int tde_scale(size_t n, float* x, float alpha, void* stream) {
 }
 
 int tde_fill(size_t n, float* x, float value, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(x != nullptr);
   hipLaunchKernelGGL(fill_kernel, dim3(ew_grid((long)n)), dim3(256), 0, static_cast<hipStream_t>(stream), (long)n, x,
                      value);
@@ -169,6 +176,7 @@ int tde_fill(size_t n, float* x, float value, void* stream) {
 
 int tde_copy_view(int M, int C, const float* src, int s_cstride, int s_coff, float* dst, int d_cstride, int d_coff,
                   int accumulate, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && src && dst);
   TDE_CHECK_ARG(s_cstride >= C && d_cstride >= C && s_coff >= 0 && d_coff >= 0);
   const long span = (long)M * (s_cstride > d_cstride ? s_cstride : d_cstride) + (s_coff > d_coff ? s_coff : d_coff);

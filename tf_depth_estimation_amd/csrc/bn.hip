@@ -793,6 +793,7 @@ size_t tde_bn_workspace_size(int M, int C) {
 int tde_bn_fwd_train(int M, int C, int groups, const float* z, const float* beta, float eps, float decay, int bessel,
                      float* moving_mean, float* moving_var, float* save_mean, float* save_invstd, float* y,
                      int y_cstride, int y_coff, int relu, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && beta && save_mean && save_invstd && y);
   TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) && tde_aligned16(y));
@@ -807,6 +808,7 @@ int tde_bn_fwd_train(int M, int C, int groups, const float* z, const float* beta
 
 int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps, const float* moving_mean,
                      const float* moving_var, float* y, int y_cstride, int y_coff, int relu, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && z && beta && moving_mean && moving_var && y);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride);
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -817,6 +819,7 @@ int tde_bn_fwd_infer(int M, int C, const float* z, const float* beta, float eps,
 
 int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const float* moving_mean,
                 const float* moving_var, const float* beta, float eps, float* w_out, float* bias_out, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(taps > 0 && cin > 0 && K > 0 && (layout == 0 || layout == 1) && w && moving_mean && moving_var &&
                 beta && w_out && bias_out && w != w_out);
   const long total = (long)taps * cin * K;
@@ -828,6 +831,7 @@ int tde_bn_fold(int taps, int cin, int K, int layout, const float* w, const floa
 int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean, const float* save_invstd,
                const float* beta, const float* dy, int dy_cstride, int dy_coff, float* dz, float* dbeta,
                int accumulate_dbeta, int relu, float* dz_absmax, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && save_mean && save_invstd && beta && dy && dz);
   TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(dy_cstride % 4 == 0 && dy_coff % 4 == 0 && tde_aligned16(dy) && tde_aligned16(dz));
@@ -860,6 +864,7 @@ int tde_bn_bwd(int M, int C, int groups, const float* z, const float* save_mean,
 int tde_bn_sums(int M, int C, int groups, const float* z, const float* dy, int dy_cstride, int dy_coff,
                 const float* save_mean, const float* save_invstd, const float* beta, int relu, int mode, double* sums,
                 double* sums_copy, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && sums && (mode == 0 || mode == 1));
   TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0);
   TDE_CHECK_ARG(tde_aligned16(z) && (mode == 0 || (dy && save_mean && save_invstd && beta && tde_aligned16(dy) &&
@@ -882,6 +887,7 @@ int tde_bn_sums(int M, int C, int groups, const float* z, const float* dy, int d
 int tde_bn_fwd_from_sums(int M, int C, int groups, long M_total, const float* z, const double* sums, const float* beta,
                          float eps, float decay, int bessel, float* moving_mean, float* moving_var, float* save_mean,
                          float* save_invstd, float* y, int y_cstride, int y_coff, int relu, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0 && M_total >= M / groups);
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && sums && beta && save_mean && save_invstd && y);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && tde_aligned16(z) &&
@@ -900,6 +906,7 @@ int tde_bn_bwd_from_sums(int M, int C, int groups, long M_total, const float* z,
                          const float* save_invstd, const float* beta, const float* dy, int dy_cstride, int dy_coff,
                          const double* global_sums, const double* local_sums, float* dz, float* dbeta,
                          int accumulate_dbeta, int relu, float* dz_absmax, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(groups >= 1 && groups <= BN_MAX_GROUPS && M % groups == 0 && M_total >= M / groups);
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && z && save_mean && save_invstd && beta && dy && dz &&
                 global_sums && local_sums);
@@ -917,6 +924,7 @@ int tde_bn_bwd_from_sums(int M, int C, int groups, long M_total, const float* z,
 int tde_bias_relu_bwd(int M, int C, const float* y, int y_cstride, int y_coff, const float* dy, int dy_cstride,
                       int dy_coff, int relu, float* dz, float* dbias, int accumulate_dbias, float* dz_absmax, void* ws,
                       size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(M > 0 && C > 0 && C % 4 == 0 && C <= 1024 && y && dy && dz && dbias);
   TDE_CHECK_ARG(y_cstride % 4 == 0 && y_coff % 4 == 0 && y_coff + C <= y_cstride && dy_cstride % 4 == 0 &&
                 dy_coff % 4 == 0 && dy_coff + C <= dy_cstride);

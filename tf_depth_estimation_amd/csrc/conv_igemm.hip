@@ -1358,6 +1358,15 @@ static BnPlan bn_plan(const tde_conv_desc_t& d, int mode, const Plan& pl, int G 
     b.nparts = b.ch.chunks;
   }
   b.part_bytes = (size_t)b.nparts * 2 * pl.cols * sizeof(double);
+  if (pl.splits > 1) {
+    // the workspace query does not know G: a grouped split-K reduce may cut up to G - 1 more row chunks than the
+    // G = 1 plan (per_g is a ceiling per group), so size for the worst G
+    for (int g = 1; g <= BN_MAX_GROUPS; ++g) {
+      if (pl.rows % g != 0) continue;
+      const size_t pb = (size_t)bn_chunk_plan(pl.rows, pl.cols, pl.splits, g).chunks * 2 * pl.cols * sizeof(double);
+      if (pb > b.part_bytes) b.part_bytes = pb;
+    }
+  }
   // room for the grouped standalone statistics pass (any G: the workspace query does not know it)
   const size_t sa = bn_part_bytes(pl.rows, pl.cols);
   if (sa > b.part_bytes) b.part_bytes = sa;
@@ -1914,6 +1923,7 @@ static int bound_grad_operand(const tde_conv_desc_t* d, tde_conv_desc_t& db, int
 extern "C" {
 
 int tde_set_conv_math(int mode) {
+  tde_clear_error();
   if (mode < 0 || mode > 4) return TDE_ERR_ARG;
   g_conv_math = mode;
   return TDE_OK;
@@ -1929,6 +1939,7 @@ size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op) {
 
 int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const int* ops, const float* const* weights,
                              void* const* outs, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(n >= 0 && (n == 0 || (descs && ops && weights && outs)));
   std::vector<HaloPlan> hps(n);
   for (int i = 0; i < n; ++i) {
@@ -1956,6 +1967,7 @@ size_t tde_deconv2d_workspace_size(const tde_conv_desc_t* d, int op) {
 
 int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, float* y, int accumulate,
                    void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y;
@@ -1964,6 +1976,7 @@ int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, flo
 
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z, const tde_bn_train_t* bn,
                       void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(z) && bn_ok(bn, d->K));
   TDE_CHECK_ARG(d->y_cstride == d->K && d->y_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
@@ -1973,6 +1986,7 @@ int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, 
 
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
                         void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx));
   tde_conv_desc_t db;
   const int rc = bound_grad_operand(d, db, 1, dy, ws, ws_bytes, stream);
@@ -1984,6 +1998,7 @@ int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* 
 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
                           void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(dw));
   tde_conv_desc_t db;
   const int rc = bound_grad_operand(d, db, 1, dy, ws, ws_bytes, stream);
@@ -1995,6 +2010,7 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
 
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
                      int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   // the deconv input is an activation (no gradient-operand bound needed): the virtual DGRAD directly
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big));
   ConvArgs a = make_args(*d);
@@ -2005,6 +2021,7 @@ int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float
 // Folded-BN inference conv: y = relu?(conv(x, w_folded) + bias) into the y view of d.
 int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, int relu,
                             float* y, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y) && (relu == 0 || relu == 1));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y; a.bias = bias; a.relu = relu;
@@ -2013,6 +2030,7 @@ int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const floa
 
 int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, const float* w, const float* bias,
                               int relu, float* y_big, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big) &&
                 (relu == 0 || relu == 1) && d->w_cin == d->C);
   ConvArgs a = make_args(*d);
@@ -2022,6 +2040,7 @@ int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, co
 
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
                         const tde_bn_train_t* bn, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(z_big) && bn_ok(bn, d->C));
   TDE_CHECK_ARG(d->x_cstride == d->C && d->x_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
@@ -2039,6 +2058,7 @@ size_t tde_deconv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
 
 int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, const float* w, float* dx,
                    int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(dy) && tde_aligned16(w) && tde_aligned16(dx) &&
                 tde_aligned16(dw));
   tde_conv_desc_t db;
@@ -2056,6 +2076,7 @@ int tde_conv2d_bwd(const tde_conv_desc_t* d, const float* x, const float* dy, co
 int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, const float* w,
                      float* dx_small, int accumulate_dx, float* dw, int accumulate_dw, void* ws, size_t ws_bytes,
                      void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(x_small) && tde_aligned16(w) &&
                 tde_aligned16(dx_small) && tde_aligned16(dw));
   tde_conv_desc_t db;
@@ -2072,6 +2093,7 @@ int tde_deconv2d_bwd(const tde_conv_desc_t* d, const float* dy_big, const float*
 
 int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const float* w, float* dx_small,
                           int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(w) && tde_aligned16(dx_small));
   tde_conv_desc_t db;
   const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
@@ -2081,6 +2103,7 @@ int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const f
 
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, float* dw,
                             int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(dy_big) && tde_aligned16(x_small) && tde_aligned16(dw));
   tde_conv_desc_t db;
   const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
@@ -2091,6 +2114,7 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
 }
 
 int tde_stamp(unsigned long long* slot, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(slot != nullptr);
   hipLaunchKernelGGL(span_stamp_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), slot);
   return tde_launch_status();
@@ -2099,6 +2123,7 @@ int tde_stamp(unsigned long long* slot, void* stream) {
 // bench.py's graph-timed roofline: arm the calling thread's conv-kernel span stamp slots (device uint64, 8-byte
 // aligned; null, null disarms).  Returns how many stamps the previous arming launched (2 after one conv entry call).
 int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp_end) {
+  tde_clear_error();
   const int n = g_span_marks;
   g_span_slot[0] = stamp_begin;
   g_span_slot[1] = stamp_end;

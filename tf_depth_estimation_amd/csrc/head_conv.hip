@@ -1168,6 +1168,7 @@ size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
 
 int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* bias, float* y,
                  int act, float scale, float offset, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(head_desc_ok(d) && x && w && bias && y && tde_aligned16(x) && d->x_cstride % 4 == 0 && d->x_coff % 4 == 0);
   HeadArgs a = make_head_args(d);
   a.x = x; a.w = w; a.b = bias; a.y = y; a.act = act; a.scale = scale; a.offset = offset;
@@ -1199,6 +1200,7 @@ int tde_head_fwd(const tde_conv_desc_t* d, const float* x, const float* w, const
 int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const float* y, const float* dy,
                  float* dx, int accumulate_dx, float* dw, float* dbias, int accumulate_dw, int act, float scale,
                  float offset, void* ws, size_t ws_bytes, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(head_desc_ok(d) && d->stride == 1 && x && w && y && dy && tde_aligned16(x));
   TDE_CHECK_ARG(d->x_cstride % 4 == 0 && d->x_coff % 4 == 0);
   TDE_CHECK_ARG(d->K == 1 || d->K == 2 || d->K == 3 || d->K == 6);

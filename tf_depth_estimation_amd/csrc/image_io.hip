@@ -73,6 +73,7 @@ __global__ void __launch_bounds__(256) resize_unpack_kernel(const tde_image_batc
 extern "C" {
 
 int tde_image_resize_unpack(const tde_image_batch_t* a, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(a && a->B > 0 && a->out_h > 0 && a->out_w > 0 && a->nframes >= 1 && a->nframes <= TDE_MAX_FRAMES);
   TDE_CHECK_ARG(a->src && a->src_off && a->src_hw);
   for (int f = 0; f < a->nframes; ++f)

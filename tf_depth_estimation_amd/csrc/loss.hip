@@ -349,6 +349,7 @@ extern "C" {
 
 int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int coff, int recip, float weight,
                      double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H >= 3 && W >= 3 && pred && loss && grad);
   Map f{pred, H, W, cstride, coff, recip};
   hipLaunchKernelGGL(smooth2_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0, static_cast<hipStream_t>(stream),
@@ -358,6 +359,7 @@ int tde_loss_smooth2(int N, int H, int W, const float* pred, int cstride, int co
 
 int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, const float* label, int nonfinite,
                 float weight, double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && pred && label && loss && grad);
   const long total = (long)N * H * W;
   hipLaunchKernelGGL(l1_kernel, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, pred,
@@ -368,6 +370,7 @@ int tde_loss_l1(int N, int H, int W, const float* pred, int cstride, int coff, c
 int tde_loss_sig_l2(int N, int H, int W, const float* pred, int cstride, int coff, const float* label, int ndeltas,
                     const int* deltas, const float* weights, float sig_epsilon, float epsilon, float weight,
                     double* loss, float* grad, int g_cstride, int g_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && pred && label && loss && grad && ndeltas >= 1 && ndeltas <= SIG_MAXD &&
                 deltas && weights && cstride > coff && g_cstride > g_coff);
   SigArgs a{};
@@ -428,6 +431,7 @@ static int pyr_setup(const tde_depth_loss_t* a, PyrArgs& P) {
 }
 
 int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
+  tde_clear_error();
   PyrArgs P;
   const int rc = pyr_setup(a, P);
   if (rc != TDE_OK) return rc;
@@ -437,6 +441,7 @@ int tde_loss_depth_pyramid(const tde_depth_loss_t* a, void* stream) {
 }
 
 int tde_loss_depth_pyramid_multi(const tde_depth_loss_t* args, int n, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(args && n > 0 && n <= TDE_PYR_MULTI_MAX);
   PyrMulti M;
   M.n = n;

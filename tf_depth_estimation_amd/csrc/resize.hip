@@ -217,6 +217,7 @@ extern "C" {
 
 int tde_resize_nearest_fwd(int N, int H, int W, int C, const float* x, int x_cstride, int x_coff, int OH, int OW,
                            float* y, int y_cstride, int y_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && x && y);
   hipLaunchKernelGGL(nearest_fwd_kernel, dim3(ew_grid((long)N * OH * OW * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, H, W, C, x, x_cstride, x_coff, OH, OW, y, y_cstride, y_coff);
@@ -225,6 +226,7 @@ int tde_resize_nearest_fwd(int N, int H, int W, int C, const float* x, int x_cst
 
 int tde_resize_nearest_bwd(int N, int H, int W, int C, float* dx, int dx_cstride, int dx_coff, int accumulate, int OH,
                            int OW, const float* dy, int dy_cstride, int dy_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && dx && dy);
   hipLaunchKernelGGL(nearest_bwd_kernel, dim3(ew_grid((long)N * H * W * C)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), N, H, W, C, dx, dx_cstride, dx_coff, accumulate, OH, OW, dy,
@@ -234,6 +236,7 @@ int tde_resize_nearest_bwd(int N, int H, int W, int C, float* dx, int dx_cstride
 
 int tde_resize_bilinear_fwd(int N, int H, int W, int C, const float* x, int x_cstride, int x_coff, int OH, int OW,
                             float* y, int y_cstride, int y_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && x && y);
   if (OH == 2 * H && OW == 2 * W && (long)N * OH * OW * (y_cstride > x_cstride ? y_cstride : x_cstride) < (1L << 31)) {
     hipLaunchKernelGGL(bilinear_up2_fwd_kernel, dim3(ew_grid((long)N * OH * OW)), dim3(256), 0,
@@ -247,6 +250,7 @@ int tde_resize_bilinear_fwd(int N, int H, int W, int C, const float* x, int x_cs
 
 int tde_resize_bilinear_bwd(int N, int H, int W, int C, float* dx, int dx_cstride, int dx_coff, int accumulate, int OH,
                             int OW, const float* dy, int dy_cstride, int dy_coff, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && dx && dy);
   if (OH == 2 * H && OW == 2 * W && (long)N * OH * OW * (dy_cstride > dx_cstride ? dy_cstride : dx_cstride) < (1L << 31)) {
     hipLaunchKernelGGL(bilinear_up2_bwd_kernel, dim3(ew_grid((long)N * H * W)), dim3(256), 0,
@@ -261,6 +265,7 @@ int tde_resize_bilinear_bwd(int N, int H, int W, int C, float* dx, int dx_cstrid
 }
 
 int tde_resize_area_fwd(int N, int H, int W, int C, const float* x, int OH, int OW, float* y, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(N > 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0 && x && y);
   TDE_CHECK_ARG(H % OH == 0 && W % OW == 0);
   hipLaunchKernelGGL(area_fwd_kernel, dim3(ew_grid((long)N * OH * OW * C)), dim3(256), 0,

@@ -15,11 +15,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // the HIP error behind the calling thread's last TDE_ERR_HIP (named by tde_status_string)
 extern thread_local int tde_g_last_hip;
 
-// hipErrorNotReady is not a launch failure: HIP records it as the thread's last error when another library in the
-// same thread (the framework's allocator, the collective layer) queries an event that has not completed yet.
+// Launch status of an ABI entry: every entry point that launches starts with tde_clear_error(), which drops
+// whatever another library left in the calling thread's last-error slot (an event query's hipErrorNotReady from
+// the framework's allocator or the collective layer, any other stale code), so tde_launch_status() at its end
+// reports exactly the launches of this call.  (Round 4 whitelisted hipErrorNotReady after the fact instead: any
+// other stale code still failed a capture, and a real failure could be read as someone else's.)
+static inline void tde_clear_error() { (void)hipGetLastError(); }
 static inline int tde_launch_status() {
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess || e == hipErrorNotReady) return TDE_OK;
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return TDE_OK;
   tde_g_last_hip = (int)e;
   return TDE_ERR_HIP;
 }

@@ -743,6 +743,7 @@ __global__ void dP_to_dT_kernel(int B, const float* K, const double* gP, float* 
 extern "C" {
 
 int tde_pose_vec2mat(int B, const float* vec, int format, float* T, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && vec && T && format >= 0 && format <= 2);
   hipLaunchKernelGGL(pose_vec2mat_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B, vec,
                      format, T);
@@ -751,6 +752,7 @@ int tde_pose_vec2mat(int B, const float* vec, int format, float* T, void* stream
 
 int tde_pose_vec2mat_bwd(int B, const float* vec, int format, const float* dT, float* dvec, int accumulate,
                          void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && vec && dT && dvec && format >= 0 && format <= 2);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (format == 0)
@@ -766,6 +768,7 @@ int tde_pose_vec2mat_bwd(int B, const float* vec, int format, const float* dT, f
 
 int tde_sampler_bwd(int B, int H, int W, int C, const float* coords, const float* img, int Hs, int Ws,
                     const float* d_out, const float* d_wmask, float* d_img, float* d_coords, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0 && Hs > 0 && Ws > 0 && coords && img);
   TDE_CHECK_ARG(!d_img || d_out);
   dim3 grid((H * W + 255) / 256, B);
@@ -777,6 +780,7 @@ int tde_sampler_bwd(int B, int H, int W, int C, const float* coords, const float
 int tde_cam_coords_bwd(int B, int H, int W, const float* depth, const float* P, const float* Kinv,
                        const float* d_coords, const float* d_z, float* d_depth, int accumulate, double* gP,
                        void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && H > 0 && W > 0 && depth && P && Kinv && (d_coords || d_z));
   dim3 grid((H * W + 255) / 256, B);
   hipLaunchKernelGGL(cam_coords_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream), B, H, W, depth, P,
@@ -785,6 +789,7 @@ int tde_cam_coords_bwd(int B, int H, int W, const float* depth, const float* P, 
 }
 
 int tde_pose_dp_to_dt(int B, const float* K, const double* gP, float* dT, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && K && gP && dT);
   hipLaunchKernelGGL(dP_to_dT_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B, K, gP,
                      dT);
@@ -794,6 +799,7 @@ int tde_pose_dp_to_dt(int B, const float* K, const double* gP, float* dT, void* 
 int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_disp, const float* P, const float* Kinv,
                  const float* coords_in, const float* img, int Hs, int Ws, float* out, float* coords, float* flow_x,
                  float* flow_y, float* wmask, float* z, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && H > 0 && W > 0 && (depth || coords_in) && (!depth || (P && Kinv)));
   TDE_CHECK_ARG(!out || (img && C > 0 && Hs > 0 && Ws > 0));
   dim3 grid((H * W + 255) / 256, B);
@@ -804,6 +810,7 @@ int tde_warp_fwd(int B, int H, int W, int C, const float* depth, int depth_is_di
 }
 
 int tde_warp_loss(const tde_warp_loss_t* a, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(a && a->B > 0 && a->H > 0 && a->W > 0 && a->img_src && a->img_tgt && a->loss);
   TDE_CHECK_ARG((a->disp != nullptr) != (a->flow != nullptr));
   TDE_CHECK_ARG(!a->disp || (a->P && a->Kinv));
@@ -841,6 +848,7 @@ int tde_warp_loss(const tde_warp_loss_t* a, void* stream) {
 }
 
 int tde_warp_loss_multi(const tde_warp_loss_t* args, int n, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(args && n > 0 && n <= TDE_WARP_MULTI_MAX);
   static const long maxb = tde_env_pos("TDE_WARP_MAXB", 512);
   WarpMulti m;
@@ -879,6 +887,7 @@ size_t tde_warp_loss_det_workspace_size(int B, int H, int W) {
 
 int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const float* K, float* T, float* P,
                   float* Kinv, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && (pose_vec || pose_mat) && K && P && Kinv);
   hipLaunchKernelGGL(pose_prep_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B,
                      pose_vec, pose_mat, K, T, P, Kinv);
@@ -886,6 +895,7 @@ int tde_pose_prep(int B, const float* pose_vec, const float* pose_mat, const flo
 }
 
 int tde_pose_prep_multi(const tde_pose_prep_t* jobs, int n, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(jobs && n > 0 && n <= TDE_WARP_MULTI_MAX);
   PoseMulti m;
   int bmax = 0;
@@ -902,6 +912,7 @@ int tde_pose_prep_multi(const tde_pose_prep_t* jobs, int n, void* stream) {
 
 int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, long k_stride_b, const double* gP,
                   const float* gT_extra, float* g_pose_vec, int accumulate, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && nscales > 0 && pose_vec && K && gP && g_pose_vec);
   hipLaunchKernelGGL(pose_grad_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B,
                      nscales, pose_vec, K, k_stride_b, gP, gT_extra, g_pose_vec, accumulate);
@@ -909,6 +920,7 @@ int tde_pose_grad(int B, int nscales, const float* pose_vec, const float* K, lon
 }
 
 int tde_pose_grad_spread(const tde_pose_grad_t* jobs, int n, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(jobs && n > 0 && n <= TDE_WARP_MULTI_MAX);
   PoseGradMulti m;
   int bmax = 0;
@@ -926,6 +938,7 @@ int tde_pose_grad_spread(const tde_pose_grad_t* jobs, int n, void* stream) {
 
 int tde_cam_loss(int B, const float* gt_vec, const float* T_lr, const float* T_rl, float weight, double* loss,
                  float* gT_lr, float* gT_rl, void* stream) {
+  tde_clear_error();
   TDE_CHECK_ARG(B > 0 && gt_vec && T_lr && T_rl && loss && gT_lr && gT_rl);
   hipLaunchKernelGGL(cam_loss_kernel, dim3((B + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), B, gt_vec,
                      T_lr, T_rl, weight, loss, gT_lr, gT_rl);

@@ -294,6 +294,8 @@ class Trainer:
         if on and (self.adam_ov is not None or self.dadam is not None or
                    (getattr(self, "sync_bn", False) and not getattr(self, "sync_bn_capturable", False))):
             raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / host-side SyncBN")
+        if on:
+            self._check_sync_bn_streams(net=True)
         self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
@@ -378,9 +380,29 @@ class Trainer:
         deferred Adam."""
         if on and (self.adam_ov is not None or self.dadam is not None):
             raise ValueError("branch overlap and the Adam overlap / deferred Adam are exclusive")
+        if on and not serial:
+            self._check_sync_bn_streams(branch=True)
         for p in self.programs():
             p.enable_branch_overlap(on, serial)
         return self
+
+    def _check_sync_bn_streams(self, net=False, branch=False):
+        """RCCL SyncBN across replicas issues its all-reduces from every stream that runs a BatchNorm.  Per-program
+        (and per-branch) communicators keep each communicator on one stream, but with GPU_MAX_HW_QUEUES = 4 the
+        kernels of different communicators may share a hardware queue in a different order on different GPUs,
+        which no world > 1 run has checked: refuse SyncBN over more than one replica combined with the
+        net or branch overlap, and an explicit shared group with any overlap or the gradient exchange."""
+        if not getattr(self, "sync_bn", False):
+            return
+        world = max((getattr(p, "bn_world", 1) for p in self.programs()), default=1)
+        net = net or self.net_stream is not None
+        branch = branch or self._branch_on()
+        if world > 1 and (net or branch):
+            raise ValueError("SyncBN over RCCL at world > 1 runs its collectives from one stream: no net or branch "
+                             "overlap with it")
+        if getattr(self, "_sync_bn_group", None) is not None and (net or branch or self.grad_sync is not None):
+            raise ValueError("SyncBN with an explicit process group shares one communicator over several streams: "
+                             "no overlap or bucketed exchange with it")
 
     timeline = None           # program.StepTimeline (diagnostic, probe/step_timeline.py)
 
@@ -446,6 +468,7 @@ class Trainer:
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
                                   pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams)
+        self._check_sync_bn_streams()
         return self.grad_sync
 
     def enable_sync_bn(self, world, group=None):
@@ -479,6 +502,8 @@ class Trainer:
                 p.bn_sync_branch = make_sync(dist.new_group(backend="nccl"))
         self.sync_bn = True
         self.sync_bn_capturable = nccl
+        self._sync_bn_group = group
+        self._check_sync_bn_streams()
 
     def programs(self):
         return [p for p in (getattr(self, "prog", None), getattr(self, "single", None), getattr(self, "pair", None))
@@ -519,6 +544,10 @@ class Trainer:
         if getattr(self, "sync_bn", False) and not getattr(self, "sync_bn_capturable", False):
             raise NotImplementedError("SyncBN over gloo all-reduces on the host inside forward/backward: run step() "
                                       "eagerly")
+        if self.dadam is not None and not self.dadam.pending:
+            # the captured step must begin with an owed update, or step() would never replay it: one
+            # eager warm-up step makes one owed
+            warmup = max(warmup, 1)
         s = _lib.owned_stream(self, "capture_warmup")
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
