@@ -264,9 +264,10 @@ def build_trainer(args, name, N, world, rank):
     from tf_depth_estimation_amd import train
     tr = make_trainer(name, N)
     tr.set_batch(*[t.cuda() for t in make_batch(name, N, seed=1000 + rank)])
-    if world > 1:
+    if world > 1 or args.exchange == "on":
+        # (--exchange on at N = 1: a world-1 RCCL group, so the N > 1 exchange path is timed on one GPU)
         if args.ddp == "overlap":
-            tr.enable_ddp(world, bucket_mb=args.bucket_mb)
+            tr.enable_ddp(world, bucket_mb=args.bucket_mb, mode=args.exchange_mode)
         else:
             tr.grad_sync = train.MultiAllReduce(tr.chunks, world)
     if args.sync_bn:
@@ -447,6 +448,12 @@ def main():
                          "and direction, on a communicator of its own, captured into the step's graphs)")
     ap.add_argument("--ddp", default="overlap", choices=["overlap", "after"],
                     help="N > 1: bucketed all-reduce overlapped with backward, or one all-reduce after it")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "on"],
+                    help="gradient exchange: auto = with N > 1; on = also at N = 1 over a world-1 RCCL group (times the "
+                         "multi-GPU code path on one GPU)")
+    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "segments"],
+                    help="bucket all-reduces captured into the step's graphs (graph) or issued eagerly between graph "
+                         "segments cut at each bucket launch point (segments, rounds 2-4)")
     args = ap.parse_args()
     knobs = env_knobs()
 
@@ -454,7 +461,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1 or args.sync_bn:
+    if world > 1 or args.sync_bn or args.exchange == "on":
         # (--sync-bn at N = 1: a world-1 RCCL group, so the SyncBN step -- sums kernels and the captured
         # all-reduce nodes -- runs as it does at N > 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -524,7 +531,8 @@ def main():
             "data": "synthetic (SURVEY.md §8d shapes/distributions); random-init Glorot weights",
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
-                       "grad_exchange": None if world == 1 else f"{args.ddp}, {args.bucket_mb} MB buckets",
+                       "grad_exchange": (None if world == 1 and args.exchange != "on" else
+                                         f"{args.ddp}, {args.bucket_mb} MB buckets, {args.exchange_mode}"),
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",
                        "wgrad_overlap": args.wgrad_overlap == "on", "wgrad_progs": opts.get("wgrad_progs"),
                        "adam_overlap": args.adam_overlap if world == 1 else "off",

@@ -27,7 +27,7 @@ def pg():
     dist.destroy_process_group()
 
 
-def _trainer(ddp, graph, steps, wgrad=None):
+def _trainer(ddp, graph, steps, wgrad=None, mode="graph"):
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
     _api.clear_programs()
@@ -39,34 +39,43 @@ def _trainer(ddp, graph, steps, wgrad=None):
     if wgrad is not None:
         tr.enable_wgrad_overlap(serial=(wgrad == "serial"))
     if ddp:
-        gs = tr.enable_ddp(1, bucket_mb=0.5)
+        gs = tr.enable_ddp(1, bucket_mb=0.5, mode=mode)
         assert len(gs.buckets) > 8
     if graph:
         tr.capture(warmup=1)
-        if ddp:
+        if ddp and mode == "segments":
             assert len(tr.segments) > 4, "expected the backward to be cut at bucket launches"
+        if ddp and mode == "graph":
+            assert tr.segments is None and len(tr.graphs) == 1, "graph mode: one graph, all-reduces captured"
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
     return tr.chunk.flat.clone(), tr.chunk.grad.clone()
 
 
+MODES = pytest.mark.parametrize("mode", ["graph", "segments"])
+
+
+@MODES
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_overlapped_exchange_world1_matches_plain(pg, graph):
+def test_overlapped_exchange_world1_matches_plain(pg, graph, mode):
+    """World-1 RCCL exchange == no exchange, bit for bit, eager and captured, in both exchange modes (graph: the
+    bucket all-reduces captured on a forked comm branch; segments: graphs cut at launch points)."""
     p0, g0 = _trainer(False, graph, 3)
-    p1, g1 = _trainer(True, graph, 3)
+    p1, g1 = _trainer(True, graph, 3, mode=mode)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
 
 
+@MODES
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_overlapped_exchange_with_wgrad_side_stream(pg, graph):
+def test_overlapped_exchange_with_wgrad_side_stream(pg, graph, mode):
     """Filter gradients on a side stream (enable_wgrad_overlap) under the bucketed exchange: every launch
     point first joins the side stream (a bucket's last parameters come from it), and under capture the
     segments close with the side branch joined.  Bit-identical to the same split backward calls run
     serially on one stream without an exchange."""
     p0, g0 = _trainer(False, graph, 3, wgrad="serial")
-    p1, g1 = _trainer(True, graph, 3, wgrad="overlap")
+    p1, g1 = _trainer(True, graph, 3, wgrad="overlap", mode=mode)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
 
@@ -106,7 +115,7 @@ def test_sync_bn_world1_step_parity(pg):
     _api.clear_programs()
 
 
-def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False):
+def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False, mode="graph"):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
@@ -118,7 +127,7 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False):
                  torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(), small_pose(B, 4).cuda())
     tr.enable_wgrad_overlap()
     if ddp:
-        gs = tr.enable_ddp(1, bucket_mb=4.0)
+        gs = tr.enable_ddp(1, bucket_mb=4.0, mode=mode)
         assert len(gs.buckets) > 4
     if net_overlap:
         tr.enable_net_overlap()
@@ -126,7 +135,7 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False):
         tr.enable_branch_overlap(serial=branch == "serial")
     if graph:
         tr.capture(warmup=1)
-        if ddp and net_overlap:
+        if ddp and net_overlap and mode == "segments":
             nseg = sum(len(segs) for w, segs in tr.ov_seq if segs is not None)
             assert nseg > len([w for w, s in tr.ov_seq if s is not None]), "backward pieces were not cut"
     for _ in range(steps):
@@ -135,22 +144,24 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False):
     return [(c.flat.clone(), c.grad.clone(), c.adam_m.clone()) for c in tr.chunks]
 
 
+@MODES
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_config4_exchange_with_net_overlap(pg, graph):
+def test_config4_exchange_with_net_overlap(pg, graph, mode):
     """Config 4 (twin-batched programs, filter gradients on their side streams, depth_net on the second stream)
     under the bucketed exchange (world-1 RCCL group): each program's bucket launch points cut its own piece's
     graphs (only that program's filter-gradient branch is joined), the comm stream waits on events -- the
     parameters, gradients and moments equal the same step without an exchange bit for bit (deterministic
     warp-loss mode; world 1: the all-reduce is the identity)."""
     ref = _c4_trainer(False, graph, True)
-    for a, b in zip(ref, _c4_trainer(True, graph, True)):
+    for a, b in zip(ref, _c4_trainer(True, graph, True, mode=mode)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
-    for a, b in zip(ref, _c4_trainer(True, graph, False)):
+    for a, b in zip(ref, _c4_trainer(True, graph, False, mode=mode)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
+@MODES
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_config4_exchange_with_branch_overlap(pg, graph):
+def test_config4_exchange_with_branch_overlap(pg, graph, mode):
     """The benched config-4 schedule with depth_net's pose / mask branches on their own stream (enable_branch_overlap)
     under the bucketed exchange: a branch's parameters are reported from the main stream, a bucket launch point joins
     the branch before it cuts the graph, the comm stream waits on the branch's tail eagerly -- parameters, gradients
@@ -158,7 +169,7 @@ def test_config4_exchange_with_branch_overlap(pg, graph):
     ref = _c4_trainer(False, graph, True, branch="serial")
     for a, b in zip(ref, _c4_trainer(False, graph, True, branch=True)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
-    for a, b in zip(ref, _c4_trainer(True, graph, True, branch=True)):
+    for a, b in zip(ref, _c4_trainer(True, graph, True, branch=True, mode=mode)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 

@@ -27,6 +27,8 @@
 #include <vector>
 #include "bn_internal.h"
 #include "split_math.h"
+#include "conv_common.h"
+using namespace tdeconv;
 
 #include <utility>
 #include "halo_conv.h"
@@ -35,14 +37,6 @@
 
 namespace {
 
-constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
-// MODE_PS: the forward of a 3x3 stride-2 deconv (slim.conv2d_transpose, nets_optflow_depth.py:103-140) as ONE
-// pixel-shuffle GEMM instead of 4 parity-class DGRAD GEMMs: rows = input pixels (n, a, b), columns = the 2x2 output
-// block (py, px) x Cout, K = the 2x2 input neighbourhood (a - 1 + th, b - 1 + tw) x Cin -- a stride-1 2x2 forward
-// conv whose B operand is the deconv weight w[kh][kw][c][k] gathered at kh = 2 (1 - th) + py, kw = 2 (1 - tw) + px
-// (zero past the 3x3 kernel: 9 of the 16 taps x class pairs), and whose epilogue scatters column (py, px, c) to
-// output pixel (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes.
-constexpr int MODE_PS = 3;
 // TDE_DBG_PHASE (timing-diagnostic BUILDS only, -DTDE_DBG_PHASE=..., wrong results; never a runtime switch), a
 // bit mask: 1 no k-loop global loads, 2 no MFMAs, 4 no staging (split + LDS stores), 8 no B-operand loads or
 // staging (its fragments read whatever LDS holds), 16 the same for the A operand.  (Round 3's row-of-4 WGRAD
@@ -52,60 +46,6 @@ constexpr int MODE_PS = 3;
 #define TDE_DBG_PHASE 0
 #endif
 constexpr int NT = 256;
-
-struct ConvArgs {
-  int N, H, W, C, OH, OW, K, KH, KW, S, PT, PL, wcin;
-  const float* x; float* dx; int xcs, xco;
-  const float* dy; float* y; int ycs, yco;
-  const float* w; float* dw;
-  float* ws; int splits; int accumulate;
-  int kt_per;  // k-tiles per split
-  FDiv fC, fK, fKW, fOW, fOHW;
-  double* bnp;  // BN statistics partials [row tile][2][Nn] from the epilogue (FWD/DGRAD/PS, splits == 1)
-  int bn_gx;    // row tiles per DGRAD class (grid x)
-  int bn_G;     // BN row groups (DGRAD: partials ordered group-major over the parity classes; the host checks that
-                // every class's rows per group are whole row tiles)
-  int bn_gy;    // MODE_PS: column tiles (one partial record [2][ps_C] per (row tile, column tile))
-  // inference epilogue (FWD / DGRAD outputs only; accumulate == 0): v = conv + bias[col], then ReLU
-  // (BN folded into the weights, tde_conv2d_fwd_bias_act); bias null and relu 0 = plain conv
-  const float* bias; int relu;
-  // fp16x3 (math 4) operand bounds |x| <= *bound of the x view, the y view and the weights (null: unscaled
-  // x / y, fixed weight scale; split_math.h)
-  const float* xmax; const float* ymax; const float* wmax;
-  // MODE_PS: deconv output channels / height / width, weight input channels (w[3][3][ps_C][ps_K])
-  int ps_C, ps_H, ps_W, ps_K;
-  FDiv fpsC;
-};
-
-// The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
-__device__ __forceinline__ float bias_act(float v, const float* bias, int col, int relu) {
-  if (bias) v += bias[col];
-  return (relu && v < 0.f) ? 0.f : v;
-}
-
-// Per-class geometry of the DGRAD sub-pixel decomposition.
-struct DgClass {
-  int py, px, khs, kws, dh, dw, nth, ntw, HH, WW, M, Kd;
-};
-
-__device__ __forceinline__ DgClass dg_class(const ConvArgs& p, int cls) {
-  DgClass g;
-  g.py = cls / p.S;
-  g.px = cls - g.py * p.S;
-  g.khs = (g.py + p.PT) % p.S;
-  g.kws = (g.px + p.PL) % p.S;
-  g.dh = (g.py + p.PT - g.khs) / p.S;
-  g.dw = (g.px + p.PL - g.kws) / p.S;
-  g.nth = (p.KH - g.khs + p.S - 1) / p.S;
-  g.ntw = (p.KW - g.kws + p.S - 1) / p.S;
-  g.HH = (p.H - g.py + p.S - 1) / p.S;
-  g.WW = (p.W - g.px + p.S - 1) / p.S;
-  g.M = p.N * g.HH * g.WW;
-  g.Kd = g.nth * g.ntw * p.K;
-  return g;
-}
-
-__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
 
 // ------------------------------------------------------------------ bf16x3 split-precision variant
@@ -735,164 +675,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
       for (int b = 0; b < TN; ++b) acc[a][b] *= inv;
   }
 
-  // ---- batch-norm statistics of the output tile (slim.batch_norm after this conv, bn.hip): per-channel
-  // sum and sum of squares over the tile's rows (rows past M hold exact zeros: their operand rows loaded
-  // as zero), lanes -> waves in a fixed order, one fp64 partial per row tile.  Workgroup-local: the
-  // cross-tile reduction is the next kernel's (a launch costs what an in-kernel hand-off costs).
-  if constexpr (MODE != MODE_WGRAD) {
-    if (p.bnp != nullptr) {
-      float cs[TN], cq[TN];
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        cs[b] = 0.f; cq[b] = 0.f;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) { const float v = acc[a][b][r]; cs[b] += v; cq[b] += v * v; }
-        cs[b] += __shfl_xor(cs[b], 16, 64); cq[b] += __shfl_xor(cq[b], 16, 64);
-        cs[b] += __shfl_xor(cs[b], 32, 64); cq[b] += __shfl_xor(cq[b], 32, 64);
-      }
-      float* red = reinterpret_cast<float*>(smem);   // [2][WM][BN]; the main loop ended with a barrier
-      if (lane < 16) {
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          red[wm * BN + wcol0 + b * 16 + lane] = cs[b];
-          red[(WM + wm) * BN + wcol0 + b * 16 + lane] = cq[b];
-        }
-      }
-      __syncthreads();
-      if constexpr (MODE == MODE_PS) {
-        // column (py, px, c) is channel c of output-pixel class (py, px): a tile of BN columns covers whole classes
-        // (the host checks BN % ps_C == 0), so channel c's record sums its classes' columns in class order
-        const int Cc = p.ps_C;
-        if (tid < Cc) {
-          double sv = 0.0, sq = 0.0;
-          for (int k = 0; k * Cc < BN; ++k) {
-            const int col = k * Cc + tid;
-            if (n0 + col >= Nn) break;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) { sv += red[w * BN + col]; sq += red[(WM + w) * BN + col]; }
-          }
-          const size_t j = (size_t)bx * p.bn_gy + by;
-          p.bnp[j * 2 * Cc + tid] = sv;
-          p.bnp[j * 2 * Cc + Cc + tid] = sq;
-        }
-      } else if (tid < BN && n0 + tid < Nn) {
-        // dense row-tile index (class-major for DGRAD: classes own disjoint pixel sets; with row groups group-major,
-        // each group's tiles of every class before the next group's)
-        int j = bx;
-        if constexpr (MODE == MODE_DGRAD) {
-          const int ncls = p.S * p.S, cls = bz % ncls;
-          if (p.bn_G > 1) {
-            int off = 0, tot = 0, tg = 1;
-            for (int c = 0; c < ncls; ++c) {
-              const int t = dg_class(p, c).M / p.bn_G / BM;
-              if (c < cls) off += t;
-              if (c == cls) tg = t;
-              tot += t;
-            }
-            const int gi = bx / tg;
-            j = gi * tot + off + (bx - gi * tg);
-          } else {
-            for (int c = 0; c < cls; ++c) j += (dg_class(p, c).M + BM - 1) / BM;
-          }
-        }
-        double sv = 0.0, sq = 0.0;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) { sv += red[w * BN + tid]; sq += red[(WM + w) * BN + tid]; }
-        p.bnp[(size_t)j * 2 * Nn + n0 + tid] = sv;
-        p.bnp[(size_t)j * 2 * Nn + Nn + n0 + tid] = sq;
-      }
-    }
-  }
-
-  // ---- epilogue (16x16 C/D map is dtype-independent on gfx950).  Row addresses first; when
-  // accumulating into the destination, ALL old values are loaded before any store (a store may alias a
-  // later load, so an interleaved read-modify-write would serialise one memory latency per element).
-  const bool direct = (p.splits == 1);
-  float* base;
-  if constexpr (FWDLIKE) base = direct ? p.y : p.ws;
-  else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
-  else base = direct ? p.dw : p.ws;
-  long rowaddr[TM][4];
-#pragma unroll
-  for (int a = 0; a < TM; ++a) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wrow0 + a * 16 + 4 * q + r;
-      long ra_ = -1;
-      if (m < M) {
-        if constexpr (MODE == MODE_FWD) {
-          ra_ = direct ? (long)m * p.ycs + p.yco : ((long)zsplit * M + m) * Nn;
-        } else if constexpr (MODE == MODE_PS) {
-          // output pixel (2a, 2b) of row (n, a, b); split-K never runs in this mode (the host keeps splits 1)
-          const int ohw = p.OH * p.OW;
-          const int ni = m / ohw, rr = m - ni * ohw, aa = rr / p.OW, bb = rr - aa * p.OW;
-          ra_ = ((long)(ni * p.ps_H + 2 * aa) * p.ps_W + 2 * bb) * p.ycs + p.yco;
-        } else if constexpr (MODE == MODE_DGRAD) {
-          const int hw = g.HH * g.WW;
-          const int n = m / hw, rr = m - n * hw, ihh = rr / g.WW, iww = rr - ihh * g.WW;
-          const long P = ((long)n * p.H + (ihh * p.S + g.py)) * p.W + (iww * p.S + g.px);
-          ra_ = direct ? P * p.xcs + p.xco : ((long)zsplit * p.N * p.H * p.W + P) * Nn;
-        } else {
-          if (direct) {
-            const int tap = m / p.C, c = m - tap * p.C;
-            if (c < p.wcin) ra_ = (long)(tap * p.wcin + c) * p.K;
-          } else {
-            ra_ = ((long)zsplit * M + m) * Nn;
-          }
-        }
-      }
-      rowaddr[a][r] = ra_;
-    }
-  }
-  // element offset of column n from its row address, and the channel of n (bias index): n itself, except MODE_PS
-  // (column (py, px, c) -> pixel (2a + py, 2b + px), channel c)
-  long coff[TN];
-  int ccol[TN];
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int n = n0 + wcol0 + b * 16 + r16;
-    coff[b] = n; ccol[b] = n;
-    if constexpr (MODE == MODE_PS) {
-      const int gq = fdiv(n, p.fpsC);
-      ccol[b] = n - gq * p.ps_C;
-      coff[b] = (long)((gq >> 1) * p.ps_W + (gq & 1)) * p.ycs + ccol[b];
-    }
-  }
-  if (direct && p.accumulate) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int n = n0 + wcol0 + b * 16 + r16;
-          if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + coff[b]];
-        }
-  }
-  if constexpr (MODE != MODE_WGRAD) {
-    if (direct && (p.bias || p.relu)) {
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wcol0 + b * 16 + r16;
-        const int nb = n < Nn ? ccol[b] : 0;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[a][b][r] = bias_act(acc[a][b][r], p.bias, nb, p.relu);
-      }
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int n = n0 + wcol0 + b * 16 + r16;
-        if (rowaddr[a][r] >= 0 && n < Nn) tde_st(base + rowaddr[a][r] + coff[b], acc[a][b][r]);
-      }
+  tile_epilogue<MODE, BM, BN, WM, WN>(p, acc, bx, by, bz, M, Nn, zsplit, g, reinterpret_cast<float*>(smem));
 }
 
 // Tile order = hardware order.  (An XCD-contiguous remap -- each XCD walking a run of tiles that
@@ -1404,15 +1187,117 @@ static size_t hwg_ws_bytes(const tde_conv_desc_t& d) {
 
 static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr);
 
+// ---- LDS-DMA ring tiles (conv_ring.hip): every FWD / DGRAD / pixel-shuffle GEMM of the fp16x3 math that takes
+// neither the halo nor the skinny path.  TDE_RING=0: the register-staged tiles everywhere (A/B runs).
+static const long g_ring = env_long("TDE_RING", 1);
+
+// Plan + B-image geometry of the ring GEMM of d in `mode` (MODE_FWD / MODE_DGRAD / MODE_PS); false: not on the ring.
+// The column tile follows make_plan's rule over the ring widths {32, 64, 96, 128}; make_plan picks rows and splits.
+static const long g_ring_wgrad = env_long("TDE_RING_WGRAD", 1);
+static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg) {
+  if (!g_ring || g_conv_math != 4) return false;
+  if (mode == MODE_WGRAD) {
+    // the filter gradient of every layer the halo-tiled WGRAD does not take; no B image (both operands activations)
+    HwgPlan wp;
+    if (!g_ring_wgrad || hwg_plan(d, wp, g_conv_math)) return false;
+    long M, Nn, Kd;
+    int ncls;
+    gemm_dims(d, mode, M, Nn, Kd, ncls);
+    static const int wc[] = {32, 64, 96, 128};
+    int bn = 0;
+    long best = -1;
+    for (int b : wc) {
+      const long t = tde_cdiv(Nn, b), cost = t * b + 24 * t;
+      if (best < 0 || cost < best || (cost == best && b > bn)) { best = cost; bn = b; }
+    }
+    pl = make_plan(d, mode, 0, bn);
+    rg = RingGeom{mode, pl.bm, bn, 1, 0, 0};
+    return true;
+  }
+  if (mode == MODE_PS) {
+    int bm = 0, bn = 0;
+    if (!ps_ok(d, &bm, &bn)) return false;
+    const long M = (long)d.N * d.OH * d.OW;
+    const int Nn = 4 * d.C;
+    pl = Plan{};
+    pl.bm = bm; pl.bn = bn; pl.splits = 1; pl.kt_per = tde_cdiv(4L * d.K, BK3);
+    pl.gx = tde_cdiv(M, bm); pl.gy = Nn / bn; pl.gz = 1;
+    pl.rows = (int)((long)d.N * d.H * d.W); pl.cols = d.C;
+    rg = RingGeom{MODE_PS, bm, bn, 1, tde_cdiv(4L * d.K, BK3), Nn / bn};
+    return true;
+  }
+  if (mode != MODE_FWD && mode != MODE_DGRAD) return false;
+  HaloPlan hp;
+  if (halo_plan(d, mode == MODE_FWD ? 0 : 1, g_conv_math, hp)) return false;
+  if (mode == MODE_DGRAD && ps_ok(d)) return false;      // its GEMM is MODE_PS
+  long M, Nn, Kd;
+  int ncls;
+  gemm_dims(d, mode, M, Nn, Kd, ncls);
+  static const int cands[] = {32, 64, 96, 128};
+  int bn = 0;
+  long best = -1;
+  for (int b : cands) {
+    const long t = tde_cdiv(Nn, b), cost = t * b + 24 * t;
+    if (best < 0 || cost < best || (cost == best && b > bn)) { best = cost; bn = b; }
+  }
+  pl = make_plan(d, mode, 0, bn);
+  if (pl.skinny_tm > 0) return false;
+  rg = RingGeom{mode, pl.bm, bn, ncls, tde_cdiv(Kd, BK3), tde_cdiv(Nn, bn)};
+  return true;
+}
+
+// The pre-split B image job of d's ring GEMM (weights w; out: rg.image_bytes(), 16-byte aligned).
+static RingJob ring_job(const tde_conv_desc_t& d, const RingGeom& rg, const float* w, void* out) {
+  RingJob J{};
+  J.w = w; J.out = static_cast<unsigned short*>(out); J.wmax = d.w_absmax;
+  J.total = (long)(rg.image_bytes() / 2);
+  J.mode = rg.mode;
+  J.KH = d.KH; J.KW = d.KW; J.S = d.stride; J.PT = d.pad_top; J.PL = d.pad_left; J.wcin = d.w_cin;
+  J.ncls = rg.ncls; J.nkt = rg.nkt; J.ncolt = rg.ncolt; J.bn = rg.bn;
+  if (rg.mode == MODE_FWD) {
+    J.C = d.C; J.K = d.K; J.Kd = d.KH * d.KW * d.C; J.Nn = d.K;
+  } else if (rg.mode == MODE_DGRAD) {
+    J.C = d.C; J.K = d.K; J.Nn = d.C;
+  } else {   // MODE_PS: the 2x2 stride-1 virtual conv over the deconv input (K channels) into 4 x C columns
+    J.C = d.K; J.K = 4 * d.C; J.Kd = 4 * d.K; J.Nn = 4 * d.C; J.ps_C = d.C; J.ps_K = d.K;
+  }
+  return J;
+}
+
+// Prep launches for a list of jobs (RING_MAXJ per launch; a block per B tile, <= 2048 blocks per job).
+static void ring_prep(const std::vector<RingJob>& jobs, hipStream_t st) {
+  for (size_t i0 = 0; i0 < jobs.size(); i0 += RING_MAXJ) {
+    RingJobs B{};
+    int blocks = 0;
+    for (size_t i = i0; i < jobs.size() && i < i0 + RING_MAXJ; ++i) {
+      RingJob J = jobs[i];
+      J.nblocks = std::min(2048, std::max(1, J.ncls * J.nkt * J.ncolt));   // one B tile per block
+      J.block0 = blocks;
+      blocks += J.nblocks;
+      B.j[B.njobs++] = J;
+    }
+    ring_wprep_launch(B, blocks, st);
+  }
+}
+
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
-  const Plan pl = make_plan(d, mode);
-  const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
+  Plan pl;
+  RingGeom rg;
+  const bool ring = ring_plan(d, mode, pl, rg);
+  if (!ring) pl = make_plan(d, mode);
+  // ring: + the B image when the caller passes no pre-split weights (the call splits them itself)
+  const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0) + (ring ? rg.image_bytes() : 0);
   const size_t halo = halo_ws_bytes(d, mode, bn);
   size_t b = igemm > halo ? igemm : halo;
   int pbm = 0, pbn = 0;
-  if (mode == MODE_DGRAD && bn && ps_ok(d, &pbm, &pbn)) {
-    // pixel-shuffle path: one partial record [2][C] per (row tile, column tile)
-    const size_t pb = (size_t)tde_cdiv((long)d.N * d.OH * d.OW, pbm) * (4 * d.C / pbn) * 2 * d.C * sizeof(double);
+  if (mode == MODE_DGRAD && ps_ok(d, &pbm, &pbn)) {
+    // pixel-shuffle path: one partial record [2][C] per (row tile, column tile) (+ its ring image)
+    size_t pb = bn ? std::max((size_t)tde_cdiv((long)d.N * d.OH * d.OW, pbm) * (4 * d.C / pbn) * 2 * d.C * sizeof(double),
+                              bn_part_bytes((long)d.N * d.H * d.W, d.C))
+                   : 0;
+    Plan pp;
+    RingGeom rp;
+    if (ring_plan(d, MODE_PS, pp, rp)) pb += rp.image_bytes();
     if (pb > b) b = pb;
   }
   HwgPlan wp;
@@ -1607,9 +1492,9 @@ static bool ps_ok(const tde_conv_desc_t& d, int* bm, int* bn) {
   return true;
 }
 
-static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, const tde_bn_train_t* bn, void* ws,
-                  size_t ws_bytes, void* stream) {
-  // the virtual DGRAD's operands: input = a0.dy (view y of d, K channels), output = a0.dx (view x of d, C channels)
+// The pixel-shuffle GEMM's arguments: the virtual DGRAD's input = a0.dy (view y of d, K channels), its output =
+// a0.dx (view x of d, C channels).
+static ConvArgs ps_args(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate) {
   ConvArgs a{};
   a.N = d->N; a.H = d->OH; a.W = d->OW; a.C = d->K; a.OH = d->OH; a.OW = d->OW; a.K = 4 * d->C;
   a.KH = 2; a.KW = 2; a.S = 1; a.PT = 1; a.PL = 1; a.wcin = d->K;
@@ -1620,6 +1505,33 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   a.x = a0.dy; a.w = a0.w; a.y = a0.dx; a.bias = a0.bias; a.relu = a0.relu;
   a.ps_C = d->C; a.ps_H = d->H; a.ps_W = d->W; a.ps_K = d->K; a.fpsC = make_fdiv(d->C);
   a.splits = 1; a.kt_per = tde_cdiv(4L * d->K, BK3); a.accumulate = accumulate;
+  return a;
+}
+
+// One pixel-shuffle GEMM launch: the ring tile (B image from d->w_split[1], else split into `img_ws`) or the
+// register-staged tile.
+static void launch_ps(const tde_conv_desc_t* d, ConvArgs& a, int BM, int BN, dim3 grid, const Plan* rpl,
+                      const RingGeom* rg, void* img_ws, hipStream_t st) {
+  if (rpl != nullptr) {
+    const void* img = d->w_split[1];
+    if (img == nullptr) {
+      ring_prep({ring_job(*d, *rg, a.w, img_ws)}, st);
+      img = img_ws;
+    }
+    a.wimg = static_cast<const unsigned short*>(img);
+    a.img_nkt = rg->nkt; a.img_ncolt = rg->ncolt;
+    ring_launch(MODE_PS, BM, BN, grid, a, st);
+    return;
+  }
+  if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+}
+
+static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, const tde_bn_train_t* bn, void* ws,
+                  size_t ws_bytes, void* stream) {
+  ConvArgs a = ps_args(d, a0, accumulate);
   const long M = (long)d->N * d->OH * d->OW, rows = (long)d->N * d->H * d->W;
   const int Nn = 4 * d->C;
   const int G = bn && bn->groups > 1 ? bn->groups : 1;
@@ -1627,12 +1539,16 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   int BM = 0, BN = 0;
   ps_ok(*d, &BM, &BN);
   const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
+  Plan rpl;
+  RingGeom rg;
+  const bool ring = ring_plan(*d, MODE_PS, rpl, rg);
   // BN statistics from the epilogue (one record per (row tile, column tile)) when every row group is whole row tiles
   // and a tile covers whole classes; else a grouped partial pass over z
   const bool epi = bn && rows / G > BN_SMALL_M && (M % G == 0) && ((M / G) % BM == 0) && BN % d->C == 0;
   const size_t epi_bytes = (size_t)grid.x * grid.y * 2 * d->C * sizeof(double);
-  if (bn && (!ws || !tde_aligned16(ws) || bn_part_bytes(rows, d->C) > ws_bytes || (epi && epi_bytes > ws_bytes)))
-    return TDE_ERR_WORKSPACE;
+  const size_t part_bytes = bn ? std::max(bn_part_bytes(rows, d->C), epi ? epi_bytes : (size_t)0) : 0;
+  const size_t img_bytes = ring && d->w_split[1] == nullptr ? rg.image_bytes() : 0;
+  if ((bn || img_bytes) && (!ws || !tde_aligned16(ws) || part_bytes + img_bytes > ws_bytes)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
   double* part = bn ? reinterpret_cast<double*>(tde_ws_body(ws)) : nullptr;
   if (epi) {
@@ -1640,10 +1556,8 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
     a.bn_gy = (int)grid.y;
   }
   span_mark(0, st);
-  if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
-  else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
-  else if (BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  launch_ps(d, a, BM, BN, grid, ring ? &rpl : nullptr, ring ? &rg : nullptr,
+            img_bytes ? tde_ws_body(ws) + part_bytes : nullptr, st);
   span_mark(1, st);
   if (bn) {
     BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
@@ -1699,12 +1613,18 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     }
     return tde_launch_status();
   }
-  const Plan pl = make_plan(*d, MODE);
+  Plan pl;
+  RingGeom rg;
+  const bool ring = ring_plan(*d, MODE, pl, rg);
+  if (!ring) pl = make_plan(*d, MODE);
   BnPlan bp{};
   const int G = bn && bn->groups > 1 ? bn->groups : 1;
   if (pl.rows % G != 0) return TDE_ERR_ARG;
   if (bn) bp = bn_plan(*d, MODE, pl, G);
-  if (pl.ws_bytes + bp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  const bool need_img = ring && MODE != MODE_WGRAD;   // (the ring WGRAD reads two activations: no B image)
+  const void* img = need_img ? d->w_split[MODE == MODE_FWD ? 0 : 1] : nullptr;
+  const size_t img_bytes = need_img && img == nullptr ? rg.image_bytes() : 0;
+  if (pl.ws_bytes + bp.part_bytes + img_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   double* part = reinterpret_cast<double*>(body + pl.slab_bytes);
   a.ws = reinterpret_cast<float*>(body);
@@ -1716,7 +1636,17 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   a.bn_G = G;
   hipStream_t st = static_cast<hipStream_t>(stream);
   span_mark(0, st);
-  if (!skip) launch_mode<MODE>(pl, a, st);
+  if (ring && !skip) {
+    if (need_img && img == nullptr) {
+      img = body + pl.slab_bytes + bp.part_bytes;
+      ring_prep({ring_job(*d, rg, a.w, const_cast<void*>(img))}, st);
+    }
+    a.wimg = static_cast<const unsigned short*>(img);
+    a.img_nkt = rg.nkt; a.img_ncolt = rg.ncolt;
+    ring_launch(MODE, pl.bm, pl.bn, dim3(pl.gx, pl.gy, pl.gz), a, st);
+  } else if (!skip) {
+    launch_mode<MODE>(pl, a, st);
+  }
   float* z = MODE == MODE_FWD ? a.y : (MODE == MODE_DGRAD ? a.dx : a.dw);
   if (!skipr && !(bn && bp.path == BN_REDUCE)) launch_reduce<MODE>(pl, a, st);
   if (bn && bp.path == BN_REDUCE && !skipr)
@@ -1773,6 +1703,19 @@ static void launch_bwd2(const Plan& p1, const ConvArgs& a1, const Plan& p2, cons
 static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches (A/B experiments)
 
 
+// The filter-gradient GEMM of run_bwd: its plan (the ring WGRAD where it applies, else the register-staged tile;
+// fix_bm / fix_bn: the fused launch's shared tile) and the launch.
+static Plan wgrad_plan(const tde_conv_desc_t& d, bool& ring, int fix_bm = 0, int fix_bn = 0) {
+  Plan pl;
+  RingGeom rg;
+  ring = !fix_bm && ring_plan(d, MODE_WGRAD, pl, rg);
+  return ring ? pl : make_plan(d, MODE_WGRAD, fix_bm, fix_bn);
+}
+static void launch_wgrad(const Plan& p2, bool ring, const ConvArgs& a2, hipStream_t st) {
+  if (ring) ring_launch(MODE_WGRAD, p2.bm, p2.bn, dim3(p2.gx, p2.gy, p2.gz), a2, st);
+  else launch_mode<MODE_WGRAD>(p2, a2, st);
+}
+
 // Data + filter gradient of one layer.  MODE1 = the data-gradient GEMM of the virtual conv (DGRAD for a
 // conv, FWD for a deconv); the filter gradient is always its WGRAD.  One fused launch when the data
 // gradient's tile fits the filter gradient (re-planned on that tile), then the split-K reduces.
@@ -1804,7 +1747,8 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   }
   if (MODE1 == MODE_DGRAD && halo_plan(*d, 1, g_conv_math, hp)) {
     // data gradient on the halo path, filter gradient on the implicit GEMM (two launches + its reduce)
-    const Plan p2 = make_plan(*d, MODE_WGRAD);
+    bool r2;
+    const Plan p2 = wgrad_plan(*d, r2);
     if (hp.wbytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
     char* body = tde_ws_body(ws);
     a2.ws = reinterpret_cast<float*>(body + hp.wbytes);
@@ -1812,15 +1756,30 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (!skip) {
       halo_launch(hp, *d, a1.dy, a1.w, a1.dx, acc1, body, nullptr, st);
-      if (!g_skip_wgrad) launch_mode<MODE_WGRAD>(p2, a2, st);
+      if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
     }
     if (!skipr && !g_skip_wgrad) launch_reduce<MODE_WGRAD>(p2, a2, st);
     return tde_launch_status();
   }
-  const Plan p1 = make_plan(*d, MODE1);
-  const bool fuse = g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
-  const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : make_plan(*d, MODE_WGRAD);
-  if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  // the data gradient on the ring tiles where they apply (a 3x3 stride-2 conv's as the pixel-shuffle GEMM), then the
+  // filter gradient as its own launch; else the fused data + filter gradient launch
+  Plan p1;
+  RingGeom rg1;
+  int m1 = MODE1;
+  bool ring1 = ring_plan(*d, MODE1, p1, rg1);
+  if (!ring1 && MODE1 == MODE_DGRAD && ring_plan(*d, MODE_PS, p1, rg1)) {
+    ring1 = true;
+    m1 = MODE_PS;
+  }
+  if (!ring1) p1 = make_plan(*d, MODE1);
+  bool r2 = false;
+  const Plan p2w = wgrad_plan(*d, r2);
+  // fused data + filter gradient launch only when neither GEMM is on the ring tiles
+  const bool fuse = !ring1 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
+  const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : p2w;
+  const void* img = ring1 ? d->w_split[MODE1 == MODE_FWD ? 0 : 1] : nullptr;
+  const size_t img_bytes = ring1 && img == nullptr ? rg1.image_bytes() : 0;
+  if (p1.slab_bytes + p2.slab_bytes + img_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   a1.ws = reinterpret_cast<float*>(body);
   a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
@@ -1828,11 +1787,27 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   a2.splits = p2.splits; a2.kt_per = p2.kt_per; a2.accumulate = acc2; a2.bnp = nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (skip) {
+  } else if (ring1) {
+    if (img == nullptr) {
+      img = body + p1.slab_bytes + p2.slab_bytes;
+      ring_prep({ring_job(*d, rg1, a1.w, const_cast<void*>(img))}, st);
+    }
+    if (m1 == MODE_PS) {
+      ConvArgs ap = ps_args(d, a1, acc1);
+      ap.wimg = static_cast<const unsigned short*>(img);
+      ap.img_nkt = rg1.nkt; ap.img_ncolt = rg1.ncolt;
+      ring_launch(MODE_PS, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), ap, st);
+    } else {
+      a1.wimg = static_cast<const unsigned short*>(img);
+      a1.img_nkt = rg1.nkt; a1.img_ncolt = rg1.ncolt;
+      ring_launch(MODE1, p1.bm, p1.bn, dim3(p1.gx, p1.gy, p1.gz), a1, st);
+    }
+    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
   } else if (fuse) {
     launch_bwd2<MODE1>(p1, a1, p2, a2, st);
   } else {
     launch_mode<MODE1>(p1, a1, st);
-    if (!g_skip_wgrad) launch_mode<MODE_WGRAD>(p2, a2, st);
+    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
   }
   if (!skipr) {
     launch_reduce<MODE1>(p1, a1, st);
@@ -1846,9 +1821,23 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   const size_t fused = p1.skinny_tm ? 0 : p1.slab_bytes + make_plan(d, MODE_WGRAD, p1.bm, p1.bn).slab_bytes;
   const size_t split = p1.slab_bytes + make_plan(d, MODE_WGRAD).slab_bytes;
   size_t b = fused > split ? fused : split;
+  {
+    // the ring data gradient: its slab + the filter gradient's + the B image (no pre-split weights)
+    Plan pr;
+    RingGeom rg;
+    bool r2;
+    const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
+    if (ring_plan(d, mode1, pr, rg) || (mode1 == MODE_DGRAD && ring_plan(d, MODE_PS, pr, rg))) {
+      const size_t r = pr.slab_bytes + w2 + rg.image_bytes();
+      if (r > b) b = r;
+    }
+    if (p1.slab_bytes + w2 > b) b = p1.slab_bytes + w2;
+  }
   if (mode1 == MODE_DGRAD) {
     const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
-    if (h && h + make_plan(d, MODE_WGRAD).slab_bytes > b) b = h + make_plan(d, MODE_WGRAD).slab_bytes;
+    bool r2;
+    const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
+    if (h && h + w2 > b) b = h + w2;
     const size_t hw = hwg_ws_bytes(d);
     if (hw) {
       const size_t b1 = h > p1.slab_bytes ? h : p1.slab_bytes;   // halo or igemm data gradient (math-dependent)
@@ -1931,23 +1920,49 @@ int tde_set_conv_math(int mode) {
 
 int tde_get_conv_math(void) { return g_conv_math; }
 
+// The ring GEMM behind op 0 (forward) / op 1 (data gradient) of d, if any (the data gradient of a 3x3 stride-2 conv /
+// the forward of its deconv is the pixel-shuffle GEMM where ps_ok holds).
+static bool ring_for_op(const tde_conv_desc_t& d, int op, Plan& pl, RingGeom& rg) {
+  if (op == 0) return ring_plan(d, MODE_FWD, pl, rg);
+  return ring_plan(d, MODE_DGRAD, pl, rg) || ring_plan(d, MODE_PS, pl, rg);
+}
+
 size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op) {
+  if (!desc_ok(d) || (op != 0 && op != 1)) return 0;
   HaloPlan hp;
-  if (!desc_ok(d) || (op != 0 && op != 1) || !halo_plan(*d, op, g_conv_math, hp)) return 0;
-  return hp.wbytes;
+  if (halo_plan(*d, op, g_conv_math, hp)) return hp.wbytes;
+  Plan pl;
+  RingGeom rg;
+  if (ring_for_op(*d, op, pl, rg)) return rg.image_bytes();
+  return 0;
 }
 
 int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const int* ops, const float* const* weights,
                              void* const* outs, void* stream) {
   tde_clear_error();
   TDE_CHECK_ARG(n >= 0 && (n == 0 || (descs && ops && weights && outs)));
-  std::vector<HaloPlan> hps(n);
+  // halo-path images (halo_wprep_batch) and ring B images (ring_prep), one batched launch per kind
+  std::vector<HaloPlan> hps;
+  std::vector<const tde_conv_desc_t*> hd;
+  std::vector<const float*> hw;
+  std::vector<void*> ho;
+  std::vector<RingJob> rj;
   for (int i = 0; i < n; ++i) {
     TDE_CHECK_ARG(desc_ok(descs[i]) && (ops[i] == 0 || ops[i] == 1) && weights[i] && outs[i] && tde_aligned16(outs[i]));
-    // a layer / op that takes no split (tde_conv2d_split_weights_size == 0) is the caller's error
-    TDE_CHECK_ARG(halo_plan(*descs[i], ops[i], g_conv_math, hps[i]));
+    HaloPlan hp;
+    Plan pl;
+    RingGeom rg;
+    if (halo_plan(*descs[i], ops[i], g_conv_math, hp)) {
+      hps.push_back(hp); hd.push_back(descs[i]); hw.push_back(weights[i]); ho.push_back(outs[i]);
+    } else if (ring_for_op(*descs[i], ops[i], pl, rg)) {
+      rj.push_back(ring_job(*descs[i], rg, weights[i], outs[i]));
+    } else {
+      return TDE_ERR_ARG;   // a layer / op that takes no split (tde_conv2d_split_weights_size == 0): the caller's error
+    }
   }
-  if (n > 0) halo_wprep_batch(n, hps.data(), descs, weights, outs, static_cast<hipStream_t>(stream));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!hps.empty()) halo_wprep_batch((int)hps.size(), hps.data(), hd.data(), hw.data(), ho.data(), st);
+  if (!rj.empty()) ring_prep(rj, st);
   return tde_launch_status();
 }
 

@@ -65,19 +65,11 @@ __device__ __forceinline__ int tde_xcd_block(int b, int nb) {
   return x * q + (x < r ? x : r) + (b >> 3);
 }
 
-// Output stores of the big producer kernels (conv epilogues, split-K slabs and reduces, BatchNorm apply passes):
-// TDE_NT_STORES=1 builds them as non-temporal stores (diagnostic A/B: a dependent kernel boundary writes back the
-// L2's dirty lines, MI355X_MICROARCH "boundary" row, and the next kernel reads across XCDs from MALL anyway).
-#ifndef TDE_NT_STORES
-#define TDE_NT_STORES 0
-#endif
+// Output stores of the big producer kernels (conv epilogues, split-K slabs and reduces, BatchNorm apply passes).
+// (Round 4's TDE_NT_STORES build flag -- non-temporal stores -- measured slower and was removed in round 5.)
 template <typename T>
 __device__ __forceinline__ void tde_st(T* p, T v) {
-#if TDE_NT_STORES
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 __device__ __forceinline__ float tde_sign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }

@@ -16,8 +16,16 @@ contribution of the step (`uses` backward calls per chunk) is launched at once:
 so the exchange of late layers overlaps the backward conv of early ones.  `finish()` launches any
 bucket never reported and makes the compute stream wait for the comm stream before Adam.
 
-Under hipGraph capture (Trainer.capture) a launch point instead closes the current graph segment;
-replay runs segment, launches its buckets eagerly, next segment ... so RCCL stays outside graphs.
+Under hipGraph capture there are two modes:
+  * mode "graph" (the default over RCCL, round 5): the all-reduces are CAPTURED.  A launch point forks the chunk's
+    comm stream off the capture stream (an event; the filter-gradient / branch streams that wrote the bucket's
+    gradients are waited on the same way), the bucket's all-reduce (ReduceOp.AVG: no separate 1/world scale pass)
+    becomes a graph node on that branch, and `join(chunk)` at the end of the program's backward joins it back -- no
+    graph is cut, so each network's forward, loss, backward, exchange and Adam replay as the graph (piece) they are.
+    Each chunk all-reduces on a communicator of its own (created in chunk order on every rank): with config 4's two
+    networks on two streams, each communicator is used from one graph branch in a fixed order;
+  * mode "segments" (rounds 2-4; gloo falls back to it): a launch point closes the current graph segment and replay
+    runs segment, its buckets eagerly, next segment ... so RCCL stays outside the graphs.
 
 On CPU (gloo, device 'cpu') the same bookkeeping runs synchronously; tests/test_ddp.py drives it with
 world_size 2.
@@ -71,7 +79,9 @@ class GradSync:
 
     chunks: ParamChunks updated by the step; uses: {id(chunk): backward calls per step} (default 1)."""
 
-    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None, side_streams=None):
+    def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None, side_streams=None,
+                 mode=None, pre_fork=None):
+        import torch.distributed as dist
         self.world, self.group = world, group
         # pre_launch(chunk): called before a bucket launch point UNDER CAPTURE -- joins the streams that write the
         # chunk's gradients beside the capture stream (its program's filter-gradient branch, NetProgram.join_wgrad),
@@ -95,6 +105,21 @@ class GradSync:
         self.comm = _lib.dedicated_stream() if self.gpu else None
         self.capturing = None       # set by Trainer.capture: callable(buckets) closing a graph segment
         self.log = []               # launch order (names), for tests
+        nccl = self.gpu and dist.is_initialized() and dist.get_backend(group) == "nccl"
+        self.mode = mode or ("graph" if nccl else "segments")
+        if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
+            raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
+        self.captured = self.mode == "graph"
+        # graph mode: per chunk a comm stream and a communicator of its own (same creation order on every rank)
+        # pre_fork(chunk): issue whatever the chunk's program still holds back for its side streams (the deferred
+        # filter-gradient calls) before a launch point records events on them
+        self.pre_fork = pre_fork
+        self.comm_of, self.group_of = {}, {}
+        if self.captured:
+            for c in self.chunks:
+                self.comm_of[id(c)] = _lib.dedicated_stream()
+                self.group_of[id(c)] = dist.new_group(backend="nccl") if group is None else group
+        self.forked = set()         # chunks whose comm stream has work not yet joined (graph mode)
         self.begin_step()
 
     # ---- per-step bookkeeping
@@ -128,7 +153,9 @@ class GradSync:
     def _ready(self, buckets, chunk=None):
         for b in buckets:
             b.launched = True
-        if self.capturing is not None:
+        if self.captured:
+            self.launch_forked(buckets, chunk)
+        elif self.capturing is not None:
             if self.pre_launch is not None:
                 self.pre_launch(chunk)
             self.capturing(buckets)      # graph segment boundary; launched at replay
@@ -162,12 +189,49 @@ class GradSync:
                 dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
                 _lib.check(lib.tde_scale(v.numel(), _lib.ptr(v), 1.0 / self.world, st), "grad scale")
 
+    def launch_forked(self, buckets, chunk):
+        """Graph mode: all-reduce (average) `buckets` on the chunk's comm stream, forked from the current stream (and
+        after the chunk's side streams' tails) by events -- capture-legal, so under capture the all-reduces are graph
+        nodes of a branch that join(chunk) merges back; eagerly the same stream order."""
+        import torch.distributed as dist
+        self.log.extend(list(b.names) for b in buckets)
+        if chunk is None:
+            chunk = buckets[0].chunk
+        if self.pre_fork is not None:
+            self.pre_fork(chunk)
+        comm = self.comm_of[id(chunk)]
+        _lib.wait_stream(comm, torch.cuda.current_stream())
+        for sd in (self.side_streams(chunk) if self.side_streams else ()):
+            _lib.wait_stream(comm, sd)
+        with torch.cuda.stream(comm):
+            for b in buckets:
+                dist.all_reduce(b.view(), op=dist.ReduceOp.AVG, group=self.group_of[id(chunk)])
+        self.forked.add(id(chunk))
+
+    def join(self, chunk):
+        """Graph mode: launch the chunk's buckets never reported, then order the current stream after its comm stream
+        (the end of the program's backward: its Adam may follow)."""
+        if not self.captured:
+            return
+        rest = [b for b in self.buckets if b.chunk is chunk and not b.launched]
+        if rest:
+            for b in rest:
+                b.launched = True
+            self.launch_forked(rest, chunk)
+        if id(chunk) in self.forked:
+            _lib.wait_stream(torch.cuda.current_stream(), self.comm_of[id(chunk)])
+            self.forked.discard(id(chunk))
+
     def leftovers(self):
         return [b for b in self.buckets if not b.launched]
 
     def finish(self, streams=()):
         """Launch what was never reported (after `streams` too), then order the compute stream after the comm
         stream."""
+        if self.captured:
+            for c in self.chunks:
+                self.join(c)
+            return
         rest = self.leftovers()
         if rest:
             for b in rest:

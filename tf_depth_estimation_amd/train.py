@@ -25,9 +25,6 @@ CAPTURE_MODE = "thread_local"
 LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
 # config 4 as two independent per-network chains with one join (TDE_C4_CHAINS=0: the two-join schedule, A/B)
 C4_CHAINS = os.environ.get("TDE_C4_CHAINS", "1") != "0"
-# config 4 chains: the compute stream's chain (disp_net) issued BEFORE the second stream's (depth_net), which then
-# waits only for the inputs piece (TDE_C4_MAIN_FIRST=1; A/B of the launch order)
-C4_MAIN_FIRST = os.environ.get("TDE_C4_MAIN_FIRST", "0") == "1"
 
 
 def _halves(a, b):
@@ -461,13 +458,26 @@ class Trainer:
         wg = () if p.wgrad_stream is None or isinstance(p.wgrad_stream, str) else tuple(p.wgrad_streams)
         return wg + p.branch_streams()
 
-    def enable_ddp(self, world, bucket_mb=32.0, group=None):
+    def _flush_chunk_wgrad(self, chunk):
+        """Issue the deferred filter-gradient calls of the program owning `chunk` on its side stream (a captured
+        exchange launch point then waits on that stream's tail)."""
+        p = self._program_of(chunk)
+        for q in ([p] if p is not None else self.programs()):
+            if q.wgrad_stream is not None:
+                q._flush_wgrad()
+
+    def enable_ddp(self, world, bucket_mb=32.0, group=None, mode=None):
+        """Bucketed gradient all-reduce overlapped with backward (ddp.GradSync).  mode "graph" (default over RCCL):
+        the all-reduces are captured into the step's graphs on a per-network comm branch, joined at the end of that
+        network's backward (its Adam then runs inline, as in the single-GPU step); "segments": the round-2 scheme,
+        graphs cut at every bucket launch point and RCCL issued eagerly between segment replays."""
         from .ddp import GradSync
         if self.adam_ov is not None:
             raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
         uses = {id(c): self.BACKWARD_USES for c in self.chunks}
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
-                                  pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams)
+                                  pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams, mode=mode,
+                                  pre_fork=self._flush_chunk_wgrad)
         self._check_sync_bn_streams()
         return self.grad_sync
 
@@ -555,14 +565,18 @@ class Trainer:
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(s)
         gs = self.grad_sync
-        if gs is None:
+        if gs is None or getattr(gs, "captured", False):
             g = torch.cuda.CUDAGraph()
             # deferred Adam: whether the captured step begins with an owed update (it is recorded only if one
             # is owed at capture time); step() replays only when that matches the owed state
             self._graph_owes = self.dadam is not None and self.dadam.pending
+            if gs is not None:
+                gs.begin_step()
             with torch.cuda.graph(g, stream=_lib.owned_stream(self, "capture"), capture_error_mode=CAPTURE_MODE):
                 self._begin()
                 self.phase_compute()
+                if gs is not None:
+                    gs.finish()     # (graph mode: the all-reduces are nodes of this graph)
                 self._update()
             self.graphs = [g]
             return self.graphs
@@ -854,8 +868,6 @@ class DepthThenCamTrainer(Trainer):
             # of a join before the loss, and the depth_net-dependent loss runs beside disp_net's backward.  The
             # second stream waits only for the inputs (concat + image area pyramids)
             chain = {"pair": self._chain_pair, "single": self._chain_single}
-            if C4_MAIN_FIRST:
-                return [("main", self._p_inputs), ("fork", None), ("main", chain[m]), ("ov", chain[o]), ("join", None)]
             return [("main", self._p_inputs), ("ov", chain[o]), ("main", chain[m]), ("join", None)]
         return [("main", self._p_inputs), ("ov", fwd[o]), ("main", fwd[m]), ("join", None),
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
@@ -963,7 +975,8 @@ class DepthThenCamTrainer(Trainer):
         """Plain step (no exchange, no Adam overlap / deferral): each network's Adam runs right after its own
         backward on that backward's stream -- depth_net's update overlaps disp_net's backward tail (and the
         other way round) instead of both updates waiting for the join.  The same update arithmetic."""
-        return (self.grad_sync is None and self.adam_ov is None and self.dadam is None and
+        gs = self.grad_sync
+        return ((gs is None or getattr(gs, "captured", False)) and self.adam_ov is None and self.dadam is None and
                 os.environ.get("TDE_C4_INLINE_ADAM", "1") != "0")
 
     def _p_bwd_pair(self):
@@ -972,6 +985,8 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("pr", self.pair, True)
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
+        if self.grad_sync is not None and getattr(self.grad_sync, "captured", False):
+            self.grad_sync.join(self.pair.chunk)  # depth_net's exchange branch back before its Adam
         if self._inline_adam():
             self.opt.opts[1].step()
             self._tl("pair adam")
@@ -982,6 +997,8 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("sr", self.single, True)
             self._bwd("sl", self.single, False)
+        if self.grad_sync is not None and getattr(self.grad_sync, "captured", False):
+            self.grad_sync.join(self.single.chunk)
         if self._inline_adam():
             self.opt.opts[0].step()
             self._tl("single adam")
@@ -1010,13 +1027,11 @@ class DepthThenCamTrainer(Trainer):
             else:
                 fn()
 
-    def _capture(self, warmup=2, single_graph=None):
+    def _capture(self, warmup=2):
         """With the net overlap: one graph per piece, captured on the piece's stream; step() replays them
-        with the same stream waits as the eager overlapped step.  single_graph=True (or TDE_C4_SINGLE_GRAPH=1,
-        without the bucketed exchange): the whole step as ONE graph, depth_net's calls a forked branch of it."""
-        if single_graph is None:
-            single_graph = os.environ.get("TDE_C4_SINGLE_GRAPH", "0") == "1"
-        if self._overlap_stream() is None or (single_graph and self.grad_sync is None):
+        with the same stream waits as the eager overlapped step.  (The whole step as ONE graph with depth_net's calls
+        a forked branch measured no faster, round 3, and was removed in round 5.)"""
+        if self._overlap_stream() is None:
             self.ov_seq = None
             return super()._capture(warmup)
         s = _lib.owned_stream(self, "capture_warmup")
@@ -1029,11 +1044,11 @@ class DepthThenCamTrainer(Trainer):
         pool = torch.cuda.graph_pool_handle()
         main, ov = _lib.owned_stream(self, "capture"), self.net_stream
         gs = self.grad_sync
-        seg = gs is not None and hasattr(gs, "begin_step")
+        seg = gs is not None and hasattr(gs, "begin_step") and not getattr(gs, "captured", False)
         pieces = self._pieces() + ([] if seg else [("main", self._update)])
         seq = []
         self._out = {}
-        if seg:
+        if gs is not None and hasattr(gs, "begin_step"):
             gs.begin_step()
         try:
             for where, fn in pieces:
@@ -1085,7 +1100,7 @@ class DepthThenCamTrainer(Trainer):
         if os.environ.get("TDE_C4_OV_SERIAL") == "1":
             ov = cur        # diagnostic: the same piece graphs replayed one after another on one stream
         gs = self.grad_sync
-        seg = gs is not None and hasattr(gs, "begin_step")
+        seg = gs is not None and hasattr(gs, "begin_step") and not getattr(gs, "captured", False)
         if seg:
             gs.begin_step()
         fork = None
