@@ -543,6 +543,10 @@ def main():
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,
                          "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "peak_note": peak_note, "traffic": None,
+                         "frac_of_dense_fp16_peak": round(achieved / BF16_MFMA_PEAK, 4),
+                         "frac_of_dense_fp16_peak_note": ("achieved fp32-equivalent conv TFLOP/s / the 2.5 PF dense fp16 MFMA "
+                                                         "peak the north star names (each fp32 product costs 3 fp16 "
+                                                         "MFMAs in fp16x3, so 1/3 is this arithmetic's ceiling)"),
                          "timing": ("conv-busy wall time of the captured production step: a one-wave stamp kernel "
                                     "(device real-time counter) before and after every conv entry call's kernels "
                                     "inside the graphs the timed region replays (less the stamps), the union of the "

@@ -15,7 +15,7 @@ import os
 import re
 
 FAMILIES = [
-    ("conv", re.compile(r"igemm\w*_kernel|splitk_reduce\w*_kernel|skinny_kernel|halo_\w*kernel|hwg_\w*kernel|hwh_\w*kernel")),
+    ("conv", re.compile(r"igemm\w*_kernel|ring_\w*kernel|splitk_reduce\w*_kernel|skinny_kernel|halo_\w*kernel|hwg_\w*kernel|hwh_\w*kernel")),
     ("bn", re.compile(r"bn_\w+_kernel")),
     ("head", re.compile(r"head_\w+_kernel")),
     ("loss", re.compile(r"smooth2_kernel|l1_kernel|warp_\w+kernel|pose_\w+kernel|cam_loss|resize_area")),

@@ -691,6 +691,9 @@ HEAD_CASES = [
     # 3x3, K <= 2, w_cin == C, >= 32768 pixels: the row-walk kernels (head_rw_*; the cases above with C 16/32/64 too)
     (3, 96, 128, 32, 2, 3, 1, 4.0, 0.0, 36, 4),      # two outputs, sigmoid, offset view
     (2, 192, 100, 16, 1, 3, 1, 4.0, 0.0, 16, 0),     # ragged last segment (100 = 6 x 16 + 4)
+    # 5x5 / 7x7 on the halo-tiled kernels: one output, offset views, ragged tiles
+    (2, 130, 140, 64, 1, 5, 1, 4.0, 0.0, 68, 4),
+    (2, 128, 130, 32, 1, 7, 0, 1.0, 0.0, 36, 4),
     # 3-channel LINEAR disparity heads of nets.disp_net (nets.py:122-144: activation_fn=None, no BN, no scaling)
     (2, 24, 32, 128, 3, 3, 0, 1.0, 0.0, 128, 0),     # disp4 at 96x128 input
     (2, 48, 64, 64, 3, 3, 0, 1.0, 0.0, 64, 0),       # disp3

@@ -1242,6 +1242,9 @@ static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg
   }
   pl = make_plan(d, mode, 0, bn);
   if (pl.skinny_tm > 0) return false;
+  // the narrow GEMMs whose column tile would be 16 or 48 in the register-staged planner (16-channel outputs: a 32-wide
+  // ring tile computes twice the columns) stay there
+  if (make_plan(d, mode).bn % 32 != 0) return false;
   rg = RingGeom{mode, pl.bm, bn, ncls, tde_cdiv(Kd, BK3), tde_cdiv(Nn, bn)};
   return true;
 }

@@ -354,6 +354,10 @@ class NetProgram:
         self.pre_op = None
         self.params_ready = None
         self.pre_backward = None    # called first thing in backward (before any gradient is written)
+        # TDE_SPLIT_HEAD=k > 0: weight splits staged on a side stream (_stage_splits: the first k conv layers' forward
+        # images on the compute stream, the rest beside them).  Default 0 (all at the first conv): measured, the extra
+        # stream costs the config-4 step ~25 % (GPU_MAX_HW_QUEUES = 4: another stream's packets queue behind the others)
+        self.split_head = _env_nonneg("TDE_SPLIT_HEAD", 0)
         self.timeline = None        # StepTimeline (diagnostic): a device stamp after every op, under capture only
 
     def _split_plan(self, N):
@@ -638,12 +642,18 @@ class NetProgram:
                 split_todo.setdefault(job[0], []).append(job)
         main = torch.cuda.current_stream()
         bmode = self._branch_mode() if is_training and not fold_bn else None
+        split_wait = split_side = None
+        if split_todo and self.pre_op is None and bmode is None and self.split_head > 0 and self._production():
+            split_todo, split_wait, split_side = self._stage_splits(split_todo, main)
         ws_a, wsb_a = ws, wsb
         forked = False
         tl = self.timeline
         for i, op in enumerate(spec.ops):
             if tl is not None and i > 0:
                 tl.mark(self.prefix, "F", spec.ops[i - 1])
+            if split_wait is not None and i == split_wait[0]:
+                _lib.wait_event(main, split_wait[1])     # the side stream's forward images are written
+                split_wait = None
             br = bmode is not None and getattr(op, "branch", 0) == 1
             if br and bmode is not SERIAL:
                 if not forked:
@@ -767,7 +777,37 @@ class NetProgram:
         torch.cuda.set_stream(main)
         if forked:
             _lib.wait_stream(main, bmode)
+        if split_side is not None:
+            _lib.wait_stream(main, split_side)            # the backward's images (and the join of the side branch)
         return [run.view_tensor(v) for v in spec.outputs]
+
+    def _stage_splits(self, todo, main):
+        """The step's weight splits (halo and ring images, _split_plan) off the forward's critical path: the FORWARD
+        images of the first `split_head` conv layers on the main stream now; on a side stream forked here, the other
+        layers' forward images (the main stream waits for them before the first of those layers) and then every
+        backward image (joined at the end of the forward).  Under capture the side stream is a one-level branch.
+        Returns (empty todo, (op index to wait at, event) or None, side stream)."""
+        ops = self.spec.ops
+
+        def fwd_job(job):      # a conv's forward reads image 0, a deconv's forward (the virtual DGRAD) image 1
+            return job[1] == (1 if ops[job[0]].deconv else 0)
+        idx = sorted(todo)
+        head = set(idx[:self.split_head])
+        now = [j for i in idx if i in head for j in todo[i] if fwd_job(j)]
+        late_f = [j for i in idx if i not in head for j in todo[i] if fwd_job(j)]
+        late_b = [j for i in idx for j in todo[i] if not fwd_job(j)]
+        self._issue_split(now)
+        side = _lib.owned_stream(self, "split")
+        _lib.wait_stream(side, main)
+        wait = None
+        with torch.cuda.stream(side):
+            self._issue_split(late_f)
+            if late_f:
+                ev = torch.cuda.Event()
+                ev.record(side)
+                wait = (min(j[0] for j in late_f), ev)
+            self._issue_split(late_b)
+        return {}, wait, side
 
     # ---------------------------------------------------------------- backward
     def backward(self, run, grad_outputs, need_input_grad=False, on_grads=None, grad_accumulate=True):
