@@ -323,16 +323,20 @@ RING_CASES = [
 ]
 
 
+@pytest.mark.parametrize("roles", [1, 7])
 @pytest.mark.parametrize("case", RING_CASES)
-def test_ring_presplit_weights(L, case):
+def test_ring_presplit_weights(L, case, roles):
     """The ring tiles' B operand pre-split once (tde_conv2d_split_weights: the per-step image every layer's forward
     and backward share, include/tde.h w_split) gives results bit-identical to the same call splitting its own copy into
     the workspace, and both meet the 1e-5 bar against the fp64 oracle: forward, data gradient (single call and the
-    fused data + filter gradient entry)."""
+    fused data + filter gradient entry) and the filter gradient.  roles = tde_set_conv_ring mask: 1 (ring
+    forward calls only; the backward on the register-staged tiles), 7 every GEMM on the ring."""
     deconv, N, H, W, cin, C, K, k, s, xcs, xco = case
     lib = L.load()
     st = L.stream_ptr()
     prev = lib.tde_get_conv_math()
+    prev_ring = lib.tde_set_conv_ring(roles)
+    assert prev_ring >= 0
     L.check(lib.tde_set_conv_math(4))
     try:
         if deconv:
@@ -352,15 +356,22 @@ def test_ring_presplit_weights(L, case):
             d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
                           w_cin=cin, x_cstride=xcs, x_coff=xco, y_cstride=K, y_coff=0)
             w = rnd(k, k, cin, K, seed=72) * 0.2
-        sizes = [lib.tde_conv2d_split_weights_size(ctypes.byref(d), o) for o in (0, 1)]
-        assert all(sz > 0 for sz in sizes), f"ring path not taken: {sizes}"
+        # image op codes: + 2 for a deconv (its forward reads image 1); an image no call of the enabled roles reads
+        # has size 0 and stays NULL
+        codes = [o | (2 if deconv else 0) for o in (0, 1)]
+        sizes = [lib.tde_conv2d_split_weights_size(ctypes.byref(d), oc) for oc in codes]
+        fwd_img = 1 if deconv else 0
+        assert sizes[fwd_img] > 0, f"ring forward not taken: {sizes}"
+        if roles == 1:
+            assert sizes[1 - fwd_img] == 0, f"data-gradient image without the ring data-gradient role: {sizes}"
         gw = dev(w)
-        imgs = [torch.empty(sz // 4 + 64, device="cuda") for sz in sizes]
-        descs = (ctypes.c_void_p * 2)(ctypes.addressof(d), ctypes.addressof(d))
-        ops = (ctypes.c_int * 2)(0, 1)
-        wps = (ctypes.c_void_p * 2)(gw.data_ptr(), gw.data_ptr())
-        outs = (ctypes.c_void_p * 2)(imgs[0].data_ptr(), imgs[1].data_ptr())
-        L.check(lib.tde_conv2d_split_weights(2, descs, ops, wps, outs, st))
+        imgs = [torch.empty(sz // 4 + 64, device="cuda") if sz else None for sz in sizes]
+        todo = [o for o in (0, 1) if sizes[o]]
+        descs = (ctypes.c_void_p * len(todo))(*[ctypes.addressof(d) for _ in todo])
+        ops = (ctypes.c_int * len(todo))(*[codes[o] for o in todo])
+        wps = (ctypes.c_void_p * len(todo))(*[gw.data_ptr() for _ in todo])
+        outs = (ctypes.c_void_p * len(todo))(*[imgs[o].data_ptr() for o in todo])
+        L.check(lib.tde_conv2d_split_weights(len(todo), descs, ops, wps, outs, st))
         ws = ws_for(L, d, deconv=deconv)
         qb = lib.tde_deconv2d_bwd_workspace_size if deconv else lib.tde_conv2d_bwd_workspace_size
         if qb(ctypes.byref(d)) > ws.numel() * 4:
@@ -381,7 +392,7 @@ def test_ring_presplit_weights(L, case):
             gdy = dev(dyb)
         res = []
         for split in (False, True):
-            d.w_split[0], d.w_split[1] = (imgs[0].data_ptr(), imgs[1].data_ptr()) if split else (None, None)
+            d.w_split[0], d.w_split[1] = [im.data_ptr() if split and im is not None else None for im in imgs]
             if deconv:
                 y = torch.zeros(N, 2 * H, 2 * W, K, device="cuda")
                 L.check(lib.tde_deconv2d_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(y), 0, L.ptr(ws), wsb, st))
@@ -401,27 +412,32 @@ def test_ring_presplit_weights(L, case):
                 L.check(lib.tde_conv2d_bwd(ctypes.byref(d), L.ptr(gx), L.ptr(gdy), L.ptr(gw), L.ptr(dx2), 0, L.ptr(dw2),
                                            0, L.ptr(ws), wsb, st))
             torch.cuda.synchronize()
-            res.append((y.cpu(), dx.cpu(), dx2.cpu()))
+            res.append((y.cpu(), dx.cpu(), dx2.cpu(), dw2.cpu()))
         d.w_split[0], d.w_split[1] = None, None
-        for a, b, what in zip(res[0], res[1], ("fwd", "bwd_data", "bwd (fused entry) data")):
+        for a, b, what in zip(res[0], res[1], ("fwd", "bwd_data", "bwd (fused entry) data", "bwd filter")):
             assert torch.equal(a, b), f"{what}: pre-split image differs from the call's own split"
     finally:
         L.check(lib.tde_set_conv_math(prev))
+        lib.tde_set_conv_ring(prev_ring)
     # against the fp64 oracle
     if deconv:
         xr = xin[..., xco:xco + cin].clone().requires_grad_(True)
-        yr = T.conv2d_transpose_same(xr, wt.clone(), 2)
+        wr = wt.clone().requires_grad_(True)
+        yr = T.conv2d_transpose_same(xr, wr, 2)
         yr.backward(dyb)
         close(res[1][0], yr, what="ring deconv fwd")
         close(res[1][1][..., xco:xco + cin], xr.grad, what="ring deconv data grad")
         close(res[1][2][..., xco:xco + cin], xr.grad, what="ring deconv data grad (fused entry)")
+        close(res[1][3][..., :cin], wr.grad, what="ring deconv filter grad")
     else:
         xr = xin[..., xco:xco + cin].clone().requires_grad_(True)
-        yr = T.conv2d_same(xr, w.clone(), s)
+        wr = w.clone().requires_grad_(True)
+        yr = T.conv2d_same(xr, wr, s)
         yr.backward(dyb)
         close(res[1][0], yr, what="ring conv fwd")
         close(res[1][1][..., xco:xco + cin], xr.grad, what="ring conv data grad")
         close(res[1][2][..., xco:xco + cin], xr.grad, what="ring conv data grad (fused entry)")
+        close(res[1][3], wr.grad, what="ring conv filter grad")
 
 
 BN_FUSED_CASES = [

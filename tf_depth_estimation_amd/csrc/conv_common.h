@@ -66,6 +66,8 @@ struct RingJob {
   long total;             // u16 elements of the image
   int block0, nblocks;    // the job's blocks in a batched launch
   int mode, C, K, KH, KW, S, PT, PL, wcin, Kd, Nn, ncls, nkt, ncolt, bn, ps_C, ps_K;
+  long wn;                // floats of w (the buffer-load range: reads past it are zeros)
+  FDiv fC, fK, fpsC;      // divisions of the index decode
 };
 constexpr int RING_MAXJ = 20;
 struct RingJobs {

@@ -1187,19 +1187,26 @@ static size_t hwg_ws_bytes(const tde_conv_desc_t& d) {
 
 static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr);
 
-// ---- LDS-DMA ring tiles (conv_ring.hip): every FWD / DGRAD / pixel-shuffle GEMM of the fp16x3 math that takes
-// neither the halo nor the skinny path.  TDE_RING=0: the register-staged tiles everywhere (A/B runs).
-static const long g_ring = env_long("TDE_RING", 1);
+// ---- LDS-DMA ring tiles (conv_ring.hip) for the fp16x3 GEMMs that take neither the halo nor the skinny path, by
+// the role of the call (TDE_RING / tde_set_conv_ring: a mask of RING_FWD = the forward calls tde_conv2d_fwd* /
+// tde_deconv2d_fwd*, RING_DATA = the data-gradient calls (tde_*_bwd_data, the data half of tde_*_bwd), RING_FILTER =
+// the filter-gradient GEMMs).  Default 0 (opt-in): measured on config 4 (profiles/r05/ring_ab.md), the ring tiles win
+// some forward GEMMs (icnv5 / icnv6 -25 %) but lose the backward ones, whose two GEMMs the register-staged tiles run
+// as ONE fused launch (igemm_bwd2) that fills the chip where neither alone does, and the per-step B images (4 bytes
+// per weight, 384 MB written for the two networks' forward GEMMs) cost ~190 us of prep: 1066 pairs/s with the
+// forward ring vs 1079 without, 994 with every GEMM on it.
+enum { RING_FWD = 1, RING_DATA = 2, RING_FILTER = 4, RING_ALL = 7 };
+static long g_ring = env_long("TDE_RING", 0);
 
-// Plan + B-image geometry of the ring GEMM of d in `mode` (MODE_FWD / MODE_DGRAD / MODE_PS); false: not on the ring.
-// The column tile follows make_plan's rule over the ring widths {32, 64, 96, 128}; make_plan picks rows and splits.
-static const long g_ring_wgrad = env_long("TDE_RING_WGRAD", 1);
-static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg) {
-  if (!g_ring || g_conv_math != 4) return false;
+// Plan + B-image geometry of the ring GEMM of d in `mode` (MODE_FWD / MODE_DGRAD / MODE_PS / MODE_WGRAD) for a call
+// of `role` (RING_ALL: any call -- the workspace queries); false: not on the ring.  The column tile follows
+// make_plan's rule over the ring widths {32, 64, 96, 128}; make_plan picks rows and splits.
+static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg, int role) {
+  if (!(g_ring & role) || g_conv_math != 4) return false;
   if (mode == MODE_WGRAD) {
     // the filter gradient of every layer the halo-tiled WGRAD does not take; no B image (both operands activations)
     HwgPlan wp;
-    if (!g_ring_wgrad || hwg_plan(d, wp, g_conv_math)) return false;
+    if (!(g_ring & role & RING_FILTER) || hwg_plan(d, wp, g_conv_math)) return false;
     long M, Nn, Kd;
     int ncls;
     gemm_dims(d, mode, M, Nn, Kd, ncls);
@@ -1264,6 +1271,8 @@ static RingJob ring_job(const tde_conv_desc_t& d, const RingGeom& rg, const floa
   } else {   // MODE_PS: the 2x2 stride-1 virtual conv over the deconv input (K channels) into 4 x C columns
     J.C = d.K; J.K = 4 * d.C; J.Kd = 4 * d.K; J.Nn = 4 * d.C; J.ps_C = d.C; J.ps_K = d.K;
   }
+  J.wn = rg.mode == MODE_PS ? 9L * d.C * d.K : (long)d.KH * d.KW * d.w_cin * d.K;
+  J.fC = make_fdiv(J.C); J.fK = make_fdiv(J.K); J.fpsC = make_fdiv(J.ps_C > 0 ? J.ps_C : 1);
   return J;
 }
 
@@ -1284,12 +1293,14 @@ static void ring_prep(const std::vector<RingJob>& jobs, hipStream_t st) {
 }
 
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
-  Plan pl;
+  // the register-staged plan, or the ring plan (+ the B image when the caller passes no pre-split weights: the call
+  // splits them itself) of any call role
+  const Plan pl = make_plan(d, mode);
+  size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
+  Plan pr;
   RingGeom rg;
-  const bool ring = ring_plan(d, mode, pl, rg);
-  if (!ring) pl = make_plan(d, mode);
-  // ring: + the B image when the caller passes no pre-split weights (the call splits them itself)
-  const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0) + (ring ? rg.image_bytes() : 0);
+  if (ring_plan(d, mode, pr, rg, RING_ALL))
+    igemm = std::max(igemm, pr.ws_bytes + (bn ? bn_plan(d, mode, pr).part_bytes : 0) + rg.image_bytes());
   const size_t halo = halo_ws_bytes(d, mode, bn);
   size_t b = igemm > halo ? igemm : halo;
   int pbm = 0, pbn = 0;
@@ -1300,7 +1311,7 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
                    : 0;
     Plan pp;
     RingGeom rp;
-    if (ring_plan(d, MODE_PS, pp, rp)) pb += rp.image_bytes();
+    if (ring_plan(d, MODE_PS, pp, rp, RING_ALL)) pb += rp.image_bytes();
     if (pb > b) b = pb;
   }
   HwgPlan wp;
@@ -1533,7 +1544,7 @@ static void launch_ps(const tde_conv_desc_t* d, ConvArgs& a, int BM, int BN, dim
 }
 
 static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, const tde_bn_train_t* bn, void* ws,
-                  size_t ws_bytes, void* stream) {
+                  size_t ws_bytes, void* stream, int role) {
   ConvArgs a = ps_args(d, a0, accumulate);
   const long M = (long)d->N * d->OH * d->OW, rows = (long)d->N * d->H * d->W;
   const int Nn = 4 * d->C;
@@ -1544,7 +1555,7 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
   Plan rpl;
   RingGeom rg;
-  const bool ring = ring_plan(*d, MODE_PS, rpl, rg);
+  const bool ring = ring_plan(*d, MODE_PS, rpl, rg, role);
   // BN statistics from the epilogue (one record per (row tile, column tile)) when every row group is whole row tiles
   // and a tile covers whole classes; else a grouped partial pass over z
   const bool epi = bn && rows / G > BN_SMALL_M && (M % G == 0) && ((M / G) % BM == 0) && BN % d->C == 0;
@@ -1574,9 +1585,9 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
 
 template <int MODE>
 static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
-               size_t ws_bytes, void* stream) {
+               size_t ws_bytes, void* stream, int role) {
   if constexpr (MODE == MODE_DGRAD) {
-    if (ps_ok(*d) && !skip_conv(d)) return run_ps(d, a, accumulate, bn, ws, ws_bytes, stream);
+    if (ps_ok(*d) && !skip_conv(d)) return run_ps(d, a, accumulate, bn, ws, ws_bytes, stream, role);
   }
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
@@ -1618,7 +1629,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   }
   Plan pl;
   RingGeom rg;
-  const bool ring = ring_plan(*d, MODE, pl, rg);
+  const bool ring = ring_plan(*d, MODE, pl, rg, role);
   if (!ring) pl = make_plan(*d, MODE);
   BnPlan bp{};
   const int G = bn && bn->groups > 1 ? bn->groups : 1;
@@ -1711,7 +1722,7 @@ static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches
 static Plan wgrad_plan(const tde_conv_desc_t& d, bool& ring, int fix_bm = 0, int fix_bn = 0) {
   Plan pl;
   RingGeom rg;
-  ring = !fix_bm && ring_plan(d, MODE_WGRAD, pl, rg);
+  ring = !fix_bm && ring_plan(d, MODE_WGRAD, pl, rg, RING_FILTER);
   return ring ? pl : make_plan(d, MODE_WGRAD, fix_bm, fix_bn);
 }
 static void launch_wgrad(const Plan& p2, bool ring, const ConvArgs& a2, hipStream_t st) {
@@ -1769,8 +1780,8 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   Plan p1;
   RingGeom rg1;
   int m1 = MODE1;
-  bool ring1 = ring_plan(*d, MODE1, p1, rg1);
-  if (!ring1 && MODE1 == MODE_DGRAD && ring_plan(*d, MODE_PS, p1, rg1)) {
+  bool ring1 = ring_plan(*d, MODE1, p1, rg1, RING_DATA);
+  if (!ring1 && MODE1 == MODE_DGRAD && ring_plan(*d, MODE_PS, p1, rg1, RING_DATA)) {
     ring1 = true;
     m1 = MODE_PS;
   }
@@ -1830,7 +1841,7 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
     RingGeom rg;
     bool r2;
     const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
-    if (ring_plan(d, mode1, pr, rg) || (mode1 == MODE_DGRAD && ring_plan(d, MODE_PS, pr, rg))) {
+    if (ring_plan(d, mode1, pr, rg, RING_ALL) || (mode1 == MODE_DGRAD && ring_plan(d, MODE_PS, pr, rg, RING_ALL))) {
       const size_t r = pr.slab_bytes + w2 + rg.image_bytes();
       if (r > b) b = r;
     }
@@ -1923,17 +1934,28 @@ int tde_set_conv_math(int mode) {
 
 int tde_get_conv_math(void) { return g_conv_math; }
 
-// The ring GEMM behind op 0 (forward) / op 1 (data gradient) of d, if any (the data gradient of a 3x3 stride-2 conv /
-// the forward of its deconv is the pixel-shuffle GEMM where ps_ok holds).
+int tde_set_conv_ring(int roles) {
+  if (roles < 0 || roles > RING_ALL) return -1;
+  const int prev = (int)g_ring;
+  g_ring = roles;
+  return prev;
+}
+
+int tde_get_conv_ring(void) { return (int)g_ring; }
+
+// The ring GEMM behind split image op & 1 of d (0: the FWD GEMM, 1: the DGRAD GEMM -- the pixel-shuffle GEMM where
+// ps_ok holds), if the call that reads it runs on the ring: op & 2 marks d as a deconv's virtual conv, whose forward
+// call reads image 1 and data-gradient calls image 0 (a conv: the other way round).
 static bool ring_for_op(const tde_conv_desc_t& d, int op, Plan& pl, RingGeom& rg) {
-  if (op == 0) return ring_plan(d, MODE_FWD, pl, rg);
-  return ring_plan(d, MODE_DGRAD, pl, rg) || ring_plan(d, MODE_PS, pl, rg);
+  const int role = ((op & 1) == ((op >> 1) & 1)) ? RING_FWD : RING_DATA;
+  if ((op & 1) == 0) return ring_plan(d, MODE_FWD, pl, rg, role);
+  return ring_plan(d, MODE_DGRAD, pl, rg, role) || ring_plan(d, MODE_PS, pl, rg, role);
 }
 
 size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op) {
-  if (!desc_ok(d) || (op != 0 && op != 1)) return 0;
+  if (!desc_ok(d) || op < 0 || op > 3) return 0;
   HaloPlan hp;
-  if (halo_plan(*d, op, g_conv_math, hp)) return hp.wbytes;
+  if (halo_plan(*d, op & 1, g_conv_math, hp)) return hp.wbytes;
   Plan pl;
   RingGeom rg;
   if (ring_for_op(*d, op, pl, rg)) return rg.image_bytes();
@@ -1951,11 +1973,11 @@ int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const i
   std::vector<void*> ho;
   std::vector<RingJob> rj;
   for (int i = 0; i < n; ++i) {
-    TDE_CHECK_ARG(desc_ok(descs[i]) && (ops[i] == 0 || ops[i] == 1) && weights[i] && outs[i] && tde_aligned16(outs[i]));
+    TDE_CHECK_ARG(desc_ok(descs[i]) && ops[i] >= 0 && ops[i] <= 3 && weights[i] && outs[i] && tde_aligned16(outs[i]));
     HaloPlan hp;
     Plan pl;
     RingGeom rg;
-    if (halo_plan(*descs[i], ops[i], g_conv_math, hp)) {
+    if (halo_plan(*descs[i], ops[i] & 1, g_conv_math, hp)) {
       hps.push_back(hp); hd.push_back(descs[i]); hw.push_back(weights[i]); ho.push_back(outs[i]);
     } else if (ring_for_op(*descs[i], ops[i], pl, rg)) {
       rj.push_back(ring_job(*descs[i], rg, weights[i], outs[i]));
@@ -1989,7 +2011,7 @@ int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, flo
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y;
-  return run<MODE_FWD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_FWD>(d, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FWD);
 }
 
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z, const tde_bn_train_t* bn,
@@ -1999,7 +2021,7 @@ int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, 
   TDE_CHECK_ARG(d->y_cstride == d->K && d->y_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = z;
-  return run<MODE_FWD>(d, a, 0, bn, ws, ws_bytes, stream);
+  return run<MODE_FWD>(d, a, 0, bn, ws, ws_bytes, stream, RING_FWD);
 }
 
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
@@ -2011,7 +2033,7 @@ int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* 
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.dy = dy; a.w = w; a.dx = dx;
-  return run<MODE_DGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_DATA);
 }
 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
@@ -2023,7 +2045,7 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.x = x; a.dy = dy; a.dw = dw;
-  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FILTER);
 }
 
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
@@ -2033,7 +2055,7 @@ int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big));
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = y_big;
-  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FWD);
 }
 
 // Folded-BN inference conv: y = relu?(conv(x, w_folded) + bias) into the y view of d.
@@ -2043,7 +2065,7 @@ int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const floa
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y) && (relu == 0 || relu == 1));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y; a.bias = bias; a.relu = relu;
-  return run<MODE_FWD>(d, a, 0, nullptr, ws, ws_bytes, stream);
+  return run<MODE_FWD>(d, a, 0, nullptr, ws, ws_bytes, stream, RING_FWD);
 }
 
 int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, const float* w, const float* bias,
@@ -2053,7 +2075,7 @@ int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, co
                 (relu == 0 || relu == 1) && d->w_cin == d->C);
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = y_big; a.bias = bias; a.relu = relu;
-  return run<MODE_DGRAD>(d, a, 0, nullptr, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(d, a, 0, nullptr, ws, ws_bytes, stream, RING_FWD);
 }
 
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
@@ -2063,7 +2085,7 @@ int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const fl
   TDE_CHECK_ARG(d->x_cstride == d->C && d->x_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = z_big;
-  return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream);
+  return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream, RING_FWD);
 }
 
 size_t tde_conv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
@@ -2116,7 +2138,9 @@ int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const f
   tde_conv_desc_t db;
   const int rc = bound_grad_operand(d, db, 0, dy_big, ws, ws_bytes, stream);
   if (rc != TDE_OK) return rc;
-  return tde_conv2d_fwd(&db, dy_big, w, dx_small, accumulate, ws, ws_bytes, stream);
+  ConvArgs a = make_args(db);   // the virtual conv's forward, in a data-gradient role
+  a.x = dy_big; a.w = w; a.y = dx_small;
+  return run<MODE_FWD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_DATA);
 }
 
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, float* dw,
@@ -2128,7 +2152,7 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.x = dy_big; a.dy = x_small; a.dw = dw;
-  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FILTER);
 }
 
 int tde_stamp(unsigned long long* slot, void* stream) {

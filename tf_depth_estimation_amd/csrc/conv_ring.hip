@@ -1,6 +1,7 @@
 // LDS-DMA ring implicit-GEMM tiles for gfx950, fp16x3 conv math (round 5).
 //
-// Replaces the register-staged k-loop of conv_igemm.hip (conv_tile) for the FWD / DGRAD / pixel-shuffle GEMMs of
+// Opt-in (tde_set_conv_ring / TDE_RING; measured slower overall, conv_igemm.hip) replacement of the register-staged
+// k-loop of conv_igemm.hip (conv_tile) for the FWD / DGRAD / pixel-shuffle GEMMs of
 // slim.conv2d / slim.conv2d_transpose (nets_optflow_depth.py:88-144) that do not take the
 // halo or skinny paths -- the encoder's strided convs, the deep levels, the decoder's icnv* and the deconvs.  The
 // register-staged tile keeps ONE k-tile in flight: each 32-deep step waits for its global loads (~1-2 us under
@@ -39,54 +40,79 @@ __device__ __forceinline__ void ring_dma16(__amdgpu_buffer_rsrc_t r, void* lds, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, 0, 0, 0);
 }
 
-// B-operand value of the GEMM at reduction index kk, column n (0 past the tensor).
-__device__ __forceinline__ float ring_bval(const RingJob& J, int cls, int kk, int n) {
-  if (n >= J.Nn) return 0.f;
+// Float offset into w of the GEMM's B value at reduction index kk, column n; OOB (a zero read) past the tensor.
+// `g` = the class geometry (DGRAD: khs, kws, ntw, nth * ntw * K) computed once per tile.
+__device__ __forceinline__ int ring_bsrc(const RingJob& J, const int4 g, int kk, int n) {
+  if (n >= J.Nn) return OOB;
   if (J.mode == MODE_FWD) {
     // B[(tap, c)][k] = w[tap][c][k]   (w [KH][KW][wcin][K]; channels c >= wcin of a padded view: 0)
-    if (kk >= J.Kd) return 0.f;
-    const int tap = kk / J.C, c = kk - tap * J.C;
-    return c < J.wcin ? J.w[((long)tap * J.wcin + c) * J.K + n] : 0.f;
+    if (kk >= J.Kd) return OOB;
+    const int tap = fdiv(kk, J.fC), c = kk - tap * J.C;
+    return c < J.wcin ? 4 * ((tap * J.wcin + c) * J.K + n) : OOB;
   }
   if (J.mode == MODE_DGRAD) {
     // class (py, px) of the sub-pixel decomposition: B[(th, tw, kx)][ci] = w[khs + S th][kws + S tw][ci][kx]
-    const int S = J.S, py = cls / S, px = cls - py * S;
-    const int khs = (py + J.PT) % S, kws = (px + J.PL) % S;
-    const int nth = (J.KH - khs + S - 1) / S, ntw = (J.KW - kws + S - 1) / S;
-    if (kk >= nth * ntw * J.K || n >= J.wcin) return 0.f;
-    const int tap = kk / J.K, kx = kk - tap * J.K, th = tap / ntw, tw = tap - th * ntw;
-    return J.w[(((long)(khs + S * th) * J.KW + kws + S * tw) * J.wcin + n) * J.K + kx];
+    if (kk >= g.w || n >= J.wcin) return OOB;
+    const int tap = fdiv(kk, J.fK), kx = kk - tap * J.K;
+    const int th = tap / g.z, tw = tap - th * g.z;   // ntw <= 7: a short division
+    return 4 * ((((g.x + J.S * th) * J.KW + g.y + J.S * tw) * J.wcin + n) * J.K + kx);
   }
   // MODE_PS: column n = (py, px, c), reduction kk = (th, tw, kin): w[2 (1 - th) + py][2 (1 - tw) + px][c][kin]
-  if (kk >= J.Kd) return 0.f;
-  const int gq = n / J.ps_C, c = n - gq * J.ps_C;
-  const int tap = kk / J.C, kin = kk - tap * J.C;
+  if (kk >= J.Kd) return OOB;
+  const int gq = fdiv(n, J.fpsC), c = n - gq * J.ps_C;
+  const int tap = fdiv(kk, J.fC), kin = kk - tap * J.C;
   const int kh = 2 - 2 * (tap >> 1) + (gq >> 1), kw = 2 - 2 * (tap & 1) + (gq & 1);
-  if (kh >= 3 || kw >= 3) return 0.f;
-  return J.w[((long)(kh * 3 + kw) * J.ps_C + c) * J.ps_K + kin];
+  if (kh >= 3 || kw >= 3) return OOB;
+  return 4 * (((kh * 3 + kw) * J.ps_C + c) * J.ps_K + kin);
 }
 
-// One B tile per block: [2 planes][BN][32 u16] of (class, k-tile, column tile) t of job J.  The 32 x BN fp32 values
-// pass through LDS so both sides stay coalesced: read along n where the weights are n-contiguous (FWD: w[tap][c][k]),
-// along k where they are k-contiguous (DGRAD w[tap][ci][kx], PS w[kh][kw][c][kin]); written as whole 16-byte chunks.
+// One B tile per block iteration: [2 planes][BN][32 u16] of (class, k-tile, column tile) t of job J.  The 32 x BN
+// fp32 values pass through LDS so both sides stay coalesced: read along n where the weights are n-contiguous (FWD:
+// w[tap][c][k]), along k where they are k-contiguous (DGRAD w[tap][ci][kx], PS w[kh][kw][c][kin]); written as whole
+// 16-byte chunks.  A lane's BN / 8 reads are all issued before the first is used (the first version read one value
+// per loop trip with the index decode's divisions between: latency-bound, ~100 us per network launch).
 // Row cl's 16-byte slot s holds logical chunk j = s ^ ring_fb(cl), element el of chunk j is k-in-tile 4j + el (el < 4)
 // or 16 + 4j + el - 4; plane 0 = fp16(x s), plane 1 = fp16(x s - hi), s the weights' fp16x3 scale (split_math.h: the
 // same two roundings as split4x2h).
 constexpr int RING_PREP_MAXBN = 128;
+constexpr int RING_PREP_PER = RING_BK * RING_PREP_MAXBN / 256;
 __global__ void __launch_bounds__(256) ring_wprep_kernel(const RingJobs B) {
   __shared__ float T[RING_BK][RING_PREP_MAXBN + 1];
   int k = 0;
   while (k + 1 < B.njobs && (int)blockIdx.x >= B.j[k + 1].block0) ++k;
   const RingJob& J = B.j[k];
   const float ws = f16x3_scale(J.wmax, F16X3_WSCALE);
-  const int BNc = J.bn;
+  const int BNc = J.bn, nel = RING_BK * BNc;
+  const FDiv fbn = make_fdiv(BNc);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(J.w, J.wn);
   for (int t = blockIdx.x - J.block0; t < J.ncls * J.nkt * J.ncolt; t += J.nblocks) {
     const int ct = t % J.ncolt, kt = (t / J.ncolt) % J.nkt, cls = t / (J.ncolt * J.nkt);
-    for (int idx = threadIdx.x; idx < RING_BK * BNc; idx += 256) {
+    int4 g = make_int4(0, 0, 1, 0);
+    if (J.mode == MODE_DGRAD) {
+      const int S = J.S, py = cls / S, px = cls - py * S;
+      const int khs = (py + J.PT) % S, kws = (px + J.PL) % S;
+      const int nth = (J.KH - khs + S - 1) / S, ntw = (J.KW - kws + S - 1) / S;
+      g = make_int4(khs, kws, ntw, nth * ntw * J.K);
+    }
+    float v[RING_PREP_PER];
+#pragma unroll
+    for (int i = 0; i < RING_PREP_PER; ++i) {
+      const int idx = threadIdx.x + 256 * i;
       int kl, n;
-      if (J.mode == MODE_FWD) { kl = idx / BNc; n = idx - kl * BNc; }
+      if (J.mode == MODE_FWD) { kl = fdiv(idx, fbn); n = idx - kl * BNc; }
       else { n = idx >> 5; kl = idx & 31; }
-      T[kl][n] = ring_bval(J, cls, kt * RING_BK + kl, ct * BNc + n) * ws;
+      const int off = idx < nel ? ring_bsrc(J, g, kt * RING_BK + kl, ct * BNc + n) : OOB;
+      v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < RING_PREP_PER; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      if (idx < nel) {
+        int kl, n;
+        if (J.mode == MODE_FWD) { kl = fdiv(idx, fbn); n = idx - kl * BNc; }
+        else { n = idx >> 5; kl = idx & 31; }
+        T[kl][n] = v[i] * ws;
+      }
     }
     __syncthreads();
     u16* out = J.out + (long)t * (2 * BNc * RING_BK);

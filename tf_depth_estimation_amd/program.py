@@ -364,7 +364,7 @@ class NetProgram:
         """The convs whose forward or data-gradient call takes the halo-tiled path (their weights are kept as
         split MFMA tiles, tde_conv2d_split_weights): [(op index, op, desc, buffer)], cached per (N, conv math)."""
         lib = _lib.load()
-        key = (N, lib.tde_get_conv_math())
+        key = (N, lib.tde_get_conv_math(), lib.tde_get_conv_ring())
         plan = self._wsplit.get(key)
         if plan is None:
             plan = []
@@ -373,9 +373,12 @@ class NetProgram:
                     continue
                 d = op.desc(N)
                 for o in (0, 1):
-                    nb = lib.tde_conv2d_split_weights_size(ctypes_ref(d), o)
+                    # op code o + 2 for a deconv: the size of the image the calls of that role read (include/tde.h)
+                    oc = o | (2 if op.deconv else 0)
+                    nb = lib.tde_conv2d_split_weights_size(ctypes_ref(d), oc)
                     if nb:
-                        plan.append((i, o, d, torch.empty((nb + 255) // 256 * 64, dtype=torch.float32, device="cuda")))
+                        plan.append((i, o, d, torch.empty((nb + 255) // 256 * 64, dtype=torch.float32, device="cuda"),
+                                     oc))
             self._wsplit[key] = plan
         return key, plan
 
@@ -386,12 +389,12 @@ class NetProgram:
             return
         lib = _lib.load()
         n = len(jobs)
-        descs = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for _, _, d, _ in jobs])
-        ops = (ctypes.c_int * n)(*[o for _, o, _, _ in jobs])
-        ws = (ctypes.c_void_p * n)(*[self.P(f"{self.spec.ops[i].layer}/weights").data_ptr() for i, _, _, _ in jobs])
-        outs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, _, _, t in jobs])
+        descs = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for _, _, d, _, _ in jobs])
+        ops = (ctypes.c_int * n)(*[oc for _, _, _, _, oc in jobs])
+        ws = (ctypes.c_void_p * n)(*[self.P(f"{self.spec.ops[i].layer}/weights").data_ptr() for i, _, _, _, _ in jobs])
+        outs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, _, _, t, _ in jobs])
         _lib.check(lib.tde_conv2d_split_weights(n, descs, ops, ws, outs, _lib.stream_ptr()), "split weights")
-        for i, o, _, t in jobs:
+        for i, o, _, t, _ in jobs:
             self._cur_split[1].setdefault(i, [None, None])[o] = t.data_ptr()
 
     def op_param_span(self, i):
@@ -409,7 +412,7 @@ class NetProgram:
 
     def _use_split(self, d, i, N):
         cur = getattr(self, "_cur_split", None)
-        if cur is not None and cur[0] == (N, _lib.load().tde_get_conv_math()):
+        if cur is not None and cur[0] == (N, _lib.load().tde_get_conv_math(), _lib.load().tde_get_conv_ring()):
             sp = cur[1].get(i)
             if sp is not None:
                 d.w_split[0], d.w_split[1] = sp[0], sp[1]
