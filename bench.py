@@ -531,6 +531,9 @@ def main():
             "data": "synthetic (SURVEY.md §8d shapes/distributions); random-init Glorot weights",
             "config": {"workload": desc, "global_batch": world * N, "per_gpu_batch": N, "resolution": f"{W}x{H}",
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
+                       # captured graphs of the step and the cuts the exchange forces between them (graph mode: the
+                       # bucket all-reduces are graph nodes, so 0; segments mode: one cut per bucket launch point)
+                       "graph_segment_cuts": (len(getattr(tr, "segments", None) or [1]) - 1) if use_graph else None,
                        "grad_exchange": (None if world == 1 and args.exchange != "on" else
                                          f"{args.ddp}, {args.bucket_mb} MB buckets, {args.exchange_mode}"),
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",

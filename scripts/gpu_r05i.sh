@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T="timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+$T tests/test_gpu_kernels.py > gpurun_out/tests_r05i.log 2>&1 || exit $?
+B="timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 --no-secondary --no-cpu-baseline"
+$B > gpurun_out/bench_r05i_new.json 2> gpurun_out/bench_r05i_new.err || exit $?
+TDE_SLAB_BN=0 $B > gpurun_out/bench_r05i_noslab.json 2> gpurun_out/bench_r05i_noslab.err || exit $?
+$B --exchange on > gpurun_out/bench_r05i_xon.json 2> gpurun_out/bench_r05i_xon.err || exit $?
+$B > gpurun_out/bench_r05i_new2.json 2> gpurun_out/bench_r05i_new2.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r05i -o run --output-format csv -- python3 scripts/layer_profile.py --workload config4 --math fp16x3 --top 5 > gpurun_out/prof_r05i.log 2>&1

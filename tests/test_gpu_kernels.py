@@ -710,6 +710,9 @@ HEAD_CASES = [
     # 5x5 / 7x7 on the halo-tiled kernels: one output, offset views, ragged tiles
     (2, 130, 140, 64, 1, 5, 1, 4.0, 0.0, 68, 4),
     (2, 128, 130, 32, 1, 7, 0, 1.0, 0.0, 36, 4),
+    # 5x5 / 7x7, two outputs: the row-walk filter gradient (head_rwk_wgrad_kernel; the mask cases above too)
+    (2, 130, 150, 16, 2, 7, 0, 1.0, 0.0, 20, 4),     # mask1-like, offset view, ragged last segment (150 = 4 x 32 + 22)
+    (3, 70, 200, 32, 2, 5, 1, 4.0, 0.0, 32, 0),      # mask2-like, sigmoid
     # 3-channel LINEAR disparity heads of nets.disp_net (nets.py:122-144: activation_fn=None, no BN, no scaling)
     (2, 24, 32, 128, 3, 3, 0, 1.0, 0.0, 128, 0),     # disp4 at 96x128 input
     (2, 48, 64, 64, 3, 3, 0, 1.0, 0.0, 64, 0),       # disp3

@@ -249,6 +249,8 @@ __device__ __forceinline__ void publish_bwd(const SumsPub& P, int C, int c) {
   }
 }
 
+constexpr int APPLY_RB = 8;   // rows in flight per lane in the apply passes
+
 // y = relu((z - mean) * invstd + beta): rows split over blocks, a thread owns one channel quad of a row
 // lane (no 64-bit division in the index math).
 // Row groups: rows [g*Mg, (g+1)*Mg) use the statistics at [g][C] (a thread moves to the next group's
@@ -276,26 +278,37 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int M, int C, const float
       is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
     }
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
-#pragma unroll 4
-    for (int r = r0 + rl; r < r1; r += rstep) {
-      if (r >= gend) {
-        g = r / Mg;
-        gend = (g + 1) * Mg;
-        if (SUMS) {
-          stats_from_sums(P.sums, C, g, c, P.Mt, P.eps, mu, is);
-        } else {
-          mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
-          is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
-        }
-      }
-      const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
-      f4 o;
+    // APPLY_RB rows' loads issued before the first is used (a load -> store chain per row left these passes at
+    // ~1/4 of HBM rate)
+    for (int rb = r0 + rl; rb < r1; rb += APPLY_RB * rstep) {
+      f4 zv[APPLY_RB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = (zv[j] - mu[j]) * is[j] + bt[j];
-        o[j] = (relu && v < 0.f) ? 0.f : v;
+      for (int i = 0; i < APPLY_RB; ++i) {
+        const int r = rb + i * rstep;
+        zv[i] = r < r1 ? *reinterpret_cast<const f4*>(z + (long)r * C + c) : f4{0.f, 0.f, 0.f, 0.f};
       }
-      tde_st(reinterpret_cast<f4*>(y + (long)r * ycs + yco + c), o);
+#pragma unroll
+      for (int i = 0; i < APPLY_RB; ++i) {
+        const int r = rb + i * rstep;
+        if (r >= r1) break;
+        if (r >= gend) {
+          g = r / Mg;
+          gend = (g + 1) * Mg;
+          if (SUMS) {
+            stats_from_sums(P.sums, C, g, c, P.Mt, P.eps, mu, is);
+          } else {
+            mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+            is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+          }
+        }
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = (zv[i][j] - mu[j]) * is[j] + bt[j];
+          o[j] = (relu && v < 0.f) ? 0.f : v;
+        }
+        tde_st(reinterpret_cast<f4*>(y + (long)r * ycs + yco + c), o);
+      }
     }
   }
 }
@@ -354,26 +367,35 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int M, int C, const f
     const f4 bt = *reinterpret_cast<const f4*>(beta + c);
     f4 mg, mgx;
     bwd_coef<SUMS>(coef, P, C, g, c, mg, mgx);
-#pragma unroll 4
-    for (int r = r0 + rl; r < r1; r += rstep) {
-      if (r >= gend) {
-        g = r / Mg;
-        gend = (g + 1) * Mg;
-        mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
-        is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
-        bwd_coef<SUMS>(coef, P, C, g, c, mg, mgx);
-      }
-      const f4 zv = *reinterpret_cast<const f4*>(z + (long)r * C + c);
-      const f4 gv = *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c);
-      f4 o;
+    for (int rb = r0 + rl; rb < r1; rb += APPLY_RB * rstep) {
+      f4 zv[APPLY_RB], gv[APPLY_RB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xh = (zv[j] - mu[j]) * is[j];
-        const float g = (!relu || xh + bt[j] > 0.f) ? gv[j] : 0.f;
-        o[j] = is[j] * (g - mg[j] - xh * mgx[j]);
-        mx = fmaxf(mx, fabsf(o[j]));
+      for (int i = 0; i < APPLY_RB; ++i) {
+        const int r = rb + i * rstep;
+        zv[i] = r < r1 ? *reinterpret_cast<const f4*>(z + (long)r * C + c) : f4{0.f, 0.f, 0.f, 0.f};
+        gv[i] = r < r1 ? *reinterpret_cast<const f4*>(dy + (long)r * dycs + dyco + c) : f4{0.f, 0.f, 0.f, 0.f};
       }
-      tde_st(reinterpret_cast<f4*>(dz + (long)r * C + c), o);
+#pragma unroll
+      for (int i = 0; i < APPLY_RB; ++i) {
+        const int r = rb + i * rstep;
+        if (r >= r1) break;
+        if (r >= gend) {
+          g = r / Mg;
+          gend = (g + 1) * Mg;
+          mu = *reinterpret_cast<const f4*>(mean + (long)g * C + c);
+          is = *reinterpret_cast<const f4*>(invstd + (long)g * C + c);
+          bwd_coef<SUMS>(coef, P, C, g, c, mg, mgx);
+        }
+        f4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (zv[i][j] - mu[j]) * is[j];
+          const float gg = (!relu || xh + bt[j] > 0.f) ? gv[i][j] : 0.f;
+          o[j] = is[j] * (gg - mg[j] - xh * mgx[j]);
+          mx = fmaxf(mx, fabsf(o[j]));
+        }
+        tde_st(reinterpret_cast<f4*>(dz + (long)r * C + c), o);
+      }
     }
   }
   block_absmax_to(mx, amax);

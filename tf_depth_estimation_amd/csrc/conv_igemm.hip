@@ -849,13 +849,15 @@ __global__ void __launch_bounds__(NT) skinny_kernel(const ConvArgs p) {
 // output quads: lane l sums splits l, l+ZL, ... with 4 loads in flight, then the ZL lanes of a quad are
 // combined through LDS in lane order (fixed order: deterministic).  ZL > 1 only when the output is too
 // small to fill the chip otherwise (few outputs, hundreds of splits: the WGRAD of 192x256 layers).
+// (The body takes the block's index among the nblk blocks of its reduction: splitk_reduce2_kernel runs a layer's data-
+// and filter-gradient reductions as one launch.)
 template <int MODE>
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols, int zl) {
-  __shared__ f4 tmp[256];
+__device__ __forceinline__ void splitk_reduce_body(const ConvArgs& p, int rows, int cols, int zl, int blk, int nblk,
+                                                   f4* tmp) {
   const long total4 = (long)rows * (cols / 4);
   const long stride = (long)rows * cols;
   const int zlane = threadIdx.x % zl, ql = threadIdx.x / zl, qpb = 256 / zl;
-  for (long i0 = (long)blockIdx.x * qpb; i0 < total4; i0 += (long)gridDim.x * qpb) {
+  for (long i0 = (long)blk * qpb; i0 < total4; i0 += (long)nblk * qpb) {
     const long i = i0 + ql;
     f4 s = {0.f, 0.f, 0.f, 0.f}, prev = {0.f, 0.f, 0.f, 0.f};
     int row = 0, col = 0;
@@ -901,6 +903,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
     }
     tde_st(reinterpret_cast<f4*>(dst), s);
   }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, int rows, int cols, int zl) {
+  __shared__ f4 tmp[256];
+  splitk_reduce_body<MODE>(p, rows, cols, zl, blockIdx.x, gridDim.x, tmp);
+}
+
+// Both split-K reductions of one layer's backward (data gradient in MODE1, filter gradient) in one launch: blocks
+// [0, nb1) reduce the first, the rest the second (per element the same sums as two launches).
+template <int MODE1>
+__global__ void __launch_bounds__(256) splitk_reduce2_kernel(const ConvArgs p1, int rows1, int cols1, int zl1, int nb1,
+                                                             const ConvArgs p2, int rows2, int cols2, int zl2) {
+  __shared__ f4 tmp[256];
+  if ((int)blockIdx.x < nb1) splitk_reduce_body<MODE1>(p1, rows1, cols1, zl1, blockIdx.x, nb1, tmp);
+  else splitk_reduce_body<MODE_WGRAD>(p2, rows2, cols2, zl2, blockIdx.x - nb1, gridDim.x - nb1, tmp);
 }
 
 // Split-K reduction for a conv followed by batch norm: z = sum_z ws[z] (same fixed order as
@@ -1470,16 +1488,36 @@ static bool skip_conv(const tde_conv_desc_t* d) {
   return (g_skip_le >= 0 && m <= g_skip_le) || (g_skip_gt >= 0 && m > g_skip_gt);
 }
 
+// z-lanes per output quad (fill >= ~256 blocks, keep >= 4 splits per lane) and blocks of a split-K reduction
+static void reduce_shape(const Plan& pl, int& zl, int& blocks) {
+  const long n4 = (long)pl.rows * (pl.cols / 4);
+  zl = 1;
+  while (zl < 64 && (n4 * zl * 2 + 255) / 256 <= 256 && pl.splits / (zl * 2) >= 4) zl *= 2;
+  long b = (n4 * zl + 255) / 256;
+  blocks = (int)(b > 4096 ? 4096 : b);
+}
+
 template <int MODE>
 static void launch_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st) {
   if (pl.splits <= 1) return;
-  const long n4 = (long)pl.rows * (pl.cols / 4);
-  // z-lanes per output quad: fill >= ~256 blocks, keep >= 4 splits per lane
-  int zl = 1;
-  while (zl < 64 && (n4 * zl * 2 + 255) / 256 <= 256 && pl.splits / (zl * 2) >= 4) zl *= 2;
-  long blocks = (n4 * zl + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3((int)blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
+  int zl, blocks;
+  reduce_shape(pl, zl, blocks);
+  hipLaunchKernelGGL(splitk_reduce_kernel<MODE>, dim3(blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
+}
+
+// The data- and filter-gradient reductions of a layer's backward: one launch when both GEMMs split K.
+template <int MODE1>
+static void launch_reduce2(const Plan& p1, const ConvArgs& a1, const Plan& p2, const ConvArgs& a2, hipStream_t st) {
+  if (p1.splits <= 1 || p2.splits <= 1) {
+    launch_reduce<MODE1>(p1, a1, st);
+    launch_reduce<MODE_WGRAD>(p2, a2, st);
+    return;
+  }
+  int zl1, b1, zl2, b2;
+  reduce_shape(p1, zl1, b1);
+  reduce_shape(p2, zl2, b2);
+  hipLaunchKernelGGL(splitk_reduce2_kernel<MODE1>, dim3(b1 + b2), dim3(256), 0, st, a1, p1.rows, p1.cols, zl1, b1, a2,
+                     p2.rows, p2.cols, zl2);
 }
 
 // Pixel-shuffle path of the stride-2 3x3 virtual DGRAD (deconv forward; MODE_PS above).  TDE_DECONV_PS_MINM:
@@ -1824,8 +1862,8 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
   }
   if (!skipr) {
-    launch_reduce<MODE1>(p1, a1, st);
-    if (!g_skip_wgrad) launch_reduce<MODE_WGRAD>(p2, a2, st);
+    if (g_skip_wgrad) launch_reduce<MODE1>(p1, a1, st);
+    else launch_reduce2<MODE1>(p1, a1, p2, a2, st);
   }
   return tde_launch_status();
 }

@@ -895,6 +895,111 @@ __global__ void __launch_bounds__(256) head_rw_wgrad_kernel(const HeadArgs p, in
   }
 }
 
+// ------------------------------------------------------------------ row-walk 5x5 / 7x7 filter gradients (round 5)
+// The explainability-mask heads' filter gradients (nets_optflow_depth_pairtest.py:198-206: mask2 5x5 over 32
+// channels at 1/2 resolution, mask1 7x7 over 16 channels at full resolution, 2 outputs each) on the halo-tiled
+// kernel read every staged value once per tap from LDS with ~3 LDS reads per 8 FMAs: 97 us for mask1 (config 4)
+// against ~16 us of packed-FMA work.  Here block row y = kernel row kh; thread = (channel quad q, SEG-pixel segment of
+// one output row r) walks its segment with a KS-wide window of x quads (input row r + kh - PT) in registers, one new
+// quad and one dz pair per pixel, and accumulates dW[kh][kw][4q..4q+3][0..1] for all KS kw as float2 (k0, k1) pairs:
+// KS x 4 packed FMAs per pixel, no LDS in the loop.  The CQ lanes of a pixel are adjacent (its channels one
+// contiguous read); blocks combine their lanes in a fixed order and write one partial per output, summed over the
+// blocks by head_wgrad_reduce_t_kernel.
+constexpr int RWK_SEG = 32;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int KS>
+__global__ void __launch_bounds__(256) head_rwk_wgrad_kernel(const HeadArgs p, int CQ, int segs, long threads,
+                                                             float* part) {
+  constexpr int NA = KS * 4;          // float2 accumulators per thread (kw, channel)
+  __shared__ f2 red[4][16][NA + 1];
+  const int kh = blockIdx.y;
+  const long t = blockIdx.x * 256L + threadIdx.x;
+  const bool live = t < threads;
+  const long tt = live ? t : 0;
+  const int q = (int)(tt % CQ);
+  const long u_ = tt / CQ;
+  const int x0 = (int)(u_ % segs) * RWK_SEG;
+  const long rr = u_ / segs;
+  const int n = (int)(rr / p.OH), r = (int)(rr - (long)n * p.OH);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const int ih = live ? r + kh - p.PT : -1;   // a dead thread reads zeros
+  f2 acc[KS][4], bacc = {0.f, 0.f};
+#pragma unroll
+  for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[kw][j] = f2{0.f, 0.f};
+  // window slot kw = input column ow - PL + kw of the current output pixel ow
+  f4 win[KS];
+#pragma unroll
+  for (int kw = 0; kw < KS - 1; ++kw) win[kw + 1] = rw_x(p, rx, n, ih, x0 - p.PL + kw, q);
+  for (int i0 = 0; i0 < RWK_SEG; i0 += 4) {
+    f4 col[4];
+    f2 d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ow = x0 + i0 + u;
+      col[u] = rw_x(p, rx, n, ih, ow - p.PL + KS - 1, q);
+      float dd[2];
+      dz_at<2>(p, n, live ? r : p.OH, ow, dd);   // outside the image (or a dead thread): 0
+      d[u] = f2{dd[0], dd[1]};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int kw = 0; kw < KS - 1; ++kw) win[kw] = win[kw + 1];
+      win[KS - 1] = col[u];
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[kw][j] = win[kw][j] * d[u] + acc[kw][j];
+      bacc += d[u];
+    }
+  }
+  // block combine (fixed order): xor tree over the lanes of a wave holding the same quad, then the 4 waves via LDS
+  for (int o = CQ; o < 64; o <<= 1) {
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[kw][j].x += __shfl_xor(acc[kw][j].x, o, 64);
+        acc[kw][j].y += __shfl_xor(acc[kw][j].y, o, 64);
+      }
+    bacc.x += __shfl_xor(bacc.x, o, 64);
+    bacc.y += __shfl_xor(bacc.y, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < CQ) {
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wv][lane][kw * 4 + j] = acc[kw][j];
+    red[wv][lane][NA] = bacc;
+  }
+  __syncthreads();
+  // outputs of this kernel row: e = ((kh KS + kw) wcin + c) K + k for c < wcin; kernel row 0 also the bias sums
+  const long R = gridDim.x;
+  const int nrow = KS * p.wcin * 2;
+  const int nout = nrow + (kh == 0 ? 2 : 0);
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    int qq = 0, slot = NA, k = o & 1;
+    long dst;
+    if (o < nrow) {
+      const int e = o >> 1, kw = e / p.wcin, c = e - kw * p.wcin;
+      qq = c >> 2;
+      slot = kw * 4 + (c & 3);
+      dst = (long)((kh * KS + kw) * p.wcin + c) * 2 + k;
+    } else {
+      k = o - nrow;
+      dst = (long)KS * KS * p.wcin * 2 + k;   // (every quad lane summed the same dz: quad 0's is used)
+    }
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += k ? red[w][qq][slot].y : red[w][qq][slot].x;
+    part[dst * R + blockIdx.x] = v;
+  }
+}
+
 // Data gradient: thread = (channel quad, 16-pixel segment of one input row); a 3 x 3 window of dz (KC floats each,
 // recomputed from y, dy) slides along the row, weights in registers.
 template <int KC>
@@ -969,6 +1074,20 @@ bool head_rw(const tde_conv_desc_t* d) {
 }
 long rw_threads(const tde_conv_desc_t* d) {
   return (long)d->N * d->OH * ((d->OW + RW_SEG - 1) / RW_SEG) * (d->C / 4);
+}
+
+bool head_tiled(const tde_conv_desc_t* d);
+
+// row-walk 5x5 / 7x7 filter gradient (head_rwk_wgrad_kernel): the tiled heads' shapes with K = 2, SAME padding and
+// every channel a weight row; TDE_HEAD_RWK=0 keeps head_twgrad_kernel (A/B)
+static const bool g_head_rwk_on = !(std::getenv("TDE_HEAD_RWK") && std::atol(std::getenv("TDE_HEAD_RWK")) == 0);
+bool head_rwk(const tde_conv_desc_t* d) {
+  const int cq = d->C / 4;
+  return g_head_rwk_on && head_tiled(d) && (d->KH == 5 || d->KH == 7) && d->K == 2 && d->w_cin == d->C &&
+         (cq == 4 || cq == 8 || cq == 16) && d->pad_top == (d->KH - 1) / 2 && d->pad_left == (d->KW - 1) / 2;
+}
+long rwk_threads(const tde_conv_desc_t* d) {
+  return (long)d->N * d->OH * ((d->OW + RWK_SEG - 1) / RWK_SEG) * (d->C / 4);
 }
 
 struct WgPlan {
@@ -1162,6 +1281,7 @@ size_t tde_head_workspace_size(const tde_conv_desc_t* d) {
   const WgPlan w = wg_plan(d);
   long rows = head_tiled(d) ? head_tiles(d, HT_TWG_TH) : w.chunks;
   if (head_rw(d)) rows = (rw_threads(d) + 255) / 256;
+  if (head_rwk(d)) rows = std::max(rows, (rwk_threads(d) + 255) / 256);
   const size_t part = (size_t)rows * (d->KH * d->KW * d->w_cin * d->K + d->K) * sizeof(float);
   return dz_bytes(d) + part;
 }
@@ -1245,11 +1365,21 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
     const int E = d->KH * d->KW * d->w_cin;
     const int total = E * d->K + d->K;
     float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
-    if (dw) launch_tiled(d, a, 2, part, st);
+    long prow = head_tiles(d, HT_TWG_TH);
+    if (dw && head_rwk(d)) {
+      const long th = rwk_threads(d);
+      const int segs = (d->OW + RWK_SEG - 1) / RWK_SEG;
+      prow = (th + 255) / 256;
+      const dim3 g((unsigned)prow, (unsigned)d->KH);
+      if (d->KH == 5) hipLaunchKernelGGL(head_rwk_wgrad_kernel<5>, g, dim3(256), 0, st, a, d->C / 4, segs, th, part);
+      else hipLaunchKernelGGL(head_rwk_wgrad_kernel<7>, g, dim3(256), 0, st, a, d->C / 4, segs, th, part);
+    } else if (dw) {
+      launch_tiled(d, a, 2, part, st);
+    }
     if (dx) launch_tiled(d, a, 1, nullptr, st);
     if (dw)
-      hipLaunchKernelGGL(head_wgrad_reduce_t_kernel, dim3(total), dim3(64), 0, st, part, (int)head_tiles(d, HT_TWG_TH),
-                         E * d->K, dw, dbias, accumulate_dw);
+      hipLaunchKernelGGL(head_wgrad_reduce_t_kernel, dim3(total), dim3(64), 0, st, part, (int)prow, E * d->K, dw,
+                         dbias, accumulate_dw);
     return tde_launch_status();
   }
   // the wgrad pass computes dz on the fly and stores it; without a weight gradient a dz pass does that
