@@ -451,7 +451,7 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "on"],
                     help="gradient exchange: auto = with N > 1; on = also at N = 1 over a world-1 RCCL group (times the "
                          "multi-GPU code path on one GPU)")
-    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "segments"],
+    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "inline", "segments"],
                     help="bucket all-reduces captured into the step's graphs (graph) or issued eagerly between graph "
                          "segments cut at each bucket launch point (segments, rounds 2-4)")
     args = ap.parse_args()

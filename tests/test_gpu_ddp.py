@@ -45,15 +45,15 @@ def _trainer(ddp, graph, steps, wgrad=None, mode="graph"):
         tr.capture(warmup=1)
         if ddp and mode == "segments":
             assert len(tr.segments) > 4, "expected the backward to be cut at bucket launches"
-        if ddp and mode == "graph":
-            assert tr.segments is None and len(tr.graphs) == 1, "graph mode: one graph, all-reduces captured"
+        if ddp and mode in ("graph", "inline"):
+            assert tr.segments is None and len(tr.graphs) == 1, f"{mode} mode: one graph, all-reduces captured"
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
     return tr.chunk.flat.clone(), tr.chunk.grad.clone()
 
 
-MODES = pytest.mark.parametrize("mode", ["graph", "segments"])
+MODES = pytest.mark.parametrize("mode", ["graph", "inline", "segments"])
 
 
 @MODES

@@ -24,6 +24,11 @@ Under hipGraph capture there are two modes:
     graph is cut, so each network's forward, loss, backward, exchange and Adam replay as the graph (piece) they are.
     Each chunk all-reduces on a communicator of its own (created in chunk order on every rank): with config 4's two
     networks on two streams, each communicator is used from one graph branch in a fixed order;
+  * mode "inline" (round 5): captured like "graph", but a bucket's all-reduce is issued on the reporting stream
+    itself (after waiting for the chunk's side streams) -- no comm branch, no extra stream.  Measured on one GPU
+    (config 4, world-1 RCCL group): every fork of a comm branch mid-backward adds cross-queue barrier packets that
+    stall the other network's chain (GPU_MAX_HW_QUEUES = 4 FIFO queues), so "graph" with 32 MB
+    buckets ran 782 pairs/s and with one bucket per network 1049, against 1089 without the exchange;
   * mode "segments" (rounds 2-4; gloo falls back to it): a launch point closes the current graph segment and replay
     runs segment, its buckets eagerly, next segment ... so RCCL stays outside the graphs.
 
@@ -107,9 +112,9 @@ class GradSync:
         self.log = []               # launch order (names), for tests
         nccl = self.gpu and dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.mode = mode or ("graph" if nccl else "segments")
-        if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
-            raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
-        self.captured = self.mode == "graph"
+        if self.mode not in ("graph", "inline", "segments") or (self.mode != "segments" and not nccl):
+            raise ValueError(f"exchange mode {self.mode!r}: 'graph' / 'inline' need RCCL (nccl backend), else 'segments'")
+        self.captured = self.mode != "segments"
         # graph mode: per chunk a comm stream and a communicator of its own (same creation order on every rank)
         # pre_fork(chunk): issue whatever the chunk's program still holds back for its side streams (the deferred
         # filter-gradient calls) before a launch point records events on them
@@ -117,7 +122,8 @@ class GradSync:
         self.comm_of, self.group_of = {}, {}
         if self.captured:
             for c in self.chunks:
-                self.comm_of[id(c)] = _lib.dedicated_stream()
+                if self.mode == "graph":
+                    self.comm_of[id(c)] = _lib.dedicated_stream()
                 self.group_of[id(c)] = dist.new_group(backend="nccl") if group is None else group
         self.forked = set()         # chunks whose comm stream has work not yet joined (graph mode)
         self.begin_step()
@@ -199,6 +205,13 @@ class GradSync:
             chunk = buckets[0].chunk
         if self.pre_fork is not None:
             self.pre_fork(chunk)
+        if self.mode == "inline":
+            cur = torch.cuda.current_stream()
+            for sd in (self.side_streams(chunk) if self.side_streams else ()):
+                _lib.wait_stream(cur, sd)
+            for b in buckets:
+                dist.all_reduce(b.view(), op=dist.ReduceOp.AVG, group=self.group_of[id(chunk)])
+            return
         comm = self.comm_of[id(chunk)]
         _lib.wait_stream(comm, torch.cuda.current_stream())
         for sd in (self.side_streams(chunk) if self.side_streams else ()):
