@@ -296,11 +296,7 @@ def build_trainer(args, name, N, world, rank):
         tr.enable_deferred_adam()
     if net_overlap:
         tr.enable_net_overlap()
-    branch = getattr(args, "branch_overlap", "off") == "on" and args.adam_overlap == "off" and not deferred
-    if branch:
-        tr.enable_branch_overlap()
-    branch = branch and tr._branch_on()
-    return tr, dict(deferred=deferred, net_overlap=net_overlap, wgrad_progs=wg_progs, branch_overlap=branch)
+    return tr, dict(deferred=deferred, net_overlap=net_overlap, wgrad_progs=wg_progs)
 
 
 def instrumented_step(tr):
@@ -420,7 +416,9 @@ def main():
     ap.add_argument("--graph-spans", default="", help="write the per-call conv spans of the graph timing (JSON)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workloads (configs 2, 3 and 5 timed after the headline at N = 1)")
-    ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--bucket-mb", type=float, default=256.0,
+                    help="gradient all-reduce bucket size (N > 1): 256 = one bucket per network; smaller buckets fork "
+                         "the comm branch mid-backward, measured slower on one GPU (ddp.py)")
     ap.add_argument("--adam-overlap", default="off", choices=["off", "side", "wgrad"],
                     help="N = 1: run each gradient bucket's Adam as soon as backward finalises it, on its own side "
                          "stream or on the filter-gradient stream")
@@ -439,10 +437,6 @@ def main():
                     help="config 4: depth_net's calls on a second stream beside disp_net's (independent "
                          "programs; one graph per piece, replayed with stream waits; bit-identical results). "
                          "Measured config 4 605 -> 665 samples/s")
-    ap.add_argument("--branch-overlap", default="off", choices=["on", "off"],
-                    help="depth_net's pose and explainability-mask branches on a stream of their own beside the decoder, "
-                         "forward and backward (bit-identical to the same calls on one stream).  Measured slower: config 4 "
-                         "1074-1082 -> 901-912 pairs/s (a third concurrent queue delays disp_net's chain; DESIGN.md)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="BatchNorm over the global batch (one RCCL all-reduce of every row group's sums per BN layer "
                          "and direction, on a communicator of its own, captured into the step's graphs)")
@@ -451,7 +445,7 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "on"],
                     help="gradient exchange: auto = with N > 1; on = also at N = 1 over a world-1 RCCL group (times the "
                          "multi-GPU code path on one GPU)")
-    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "inline", "segments"],
+    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "segments"],
                     help="bucket all-reduces captured into the step's graphs (graph) or issued eagerly between graph "
                          "segments cut at each bucket launch point (segments, rounds 2-4)")
     args = ap.parse_args()
@@ -540,7 +534,7 @@ def main():
                        "wgrad_overlap": args.wgrad_overlap == "on", "wgrad_progs": opts.get("wgrad_progs"),
                        "adam_overlap": args.adam_overlap if world == 1 else "off",
                        "deferred_adam": opts["deferred"],
-                       "net_overlap": opts["net_overlap"], "branch_overlap": opts.get("branch_overlap", False),
+                       "net_overlap": opts["net_overlap"],
                        "unit_note": "1 unit = 1 training sample: an image pair (configs 3/4); configs 2/5 train on "
                                     "one image of it"},
             "roofline": {"bound": "mfma", "kernel": kernel_name, "math": args.math,

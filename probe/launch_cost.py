@@ -16,7 +16,7 @@ from tf_depth_estimation_amd import _lib  # noqa: E402
 
 args = types.SimpleNamespace(ddp="overlap", bucket_mb=32.0, sync_bn=False, net_overlap="on", adam_overlap="off",
                              deferred_adam="off", wgrad_overlap="on", wgrad_progs="auto", adam_bucket_mb=16.0,
-                             branch_overlap=os.environ.get("BRANCH", "off"))
+                             exchange="auto", exchange_mode="graph")
 _lib.check(_lib.load().tde_set_conv_math(4), "math")
 tr, opts = bench.build_trainer(args, os.environ.get("WORKLOAD", "config4"), 8, 1, 0)
 tr.capture()

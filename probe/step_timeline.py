@@ -20,7 +20,7 @@ from tf_depth_estimation_amd.program import StepTimeline  # noqa: E402
 OUT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/timeline.txt"
 args = types.SimpleNamespace(ddp="overlap", bucket_mb=32.0, sync_bn=False, net_overlap="on", adam_overlap="off",
                              deferred_adam="off", wgrad_overlap="on", wgrad_progs="auto", adam_bucket_mb=16.0,
-                             branch_overlap=os.environ.get("BRANCH", "off"))
+                             exchange="auto", exchange_mode="graph")
 _lib.check(_lib.load().tde_set_conv_math(4), "math")
 tr, opts = bench.build_trainer(args, "config4", 8, 1, 0)
 

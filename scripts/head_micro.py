@@ -15,7 +15,8 @@ st = L.stream_ptr()
 SHAPES = [  # name, N, H, W, C, K, k
     ("disp1_b16", 16, 192, 256, 16, 1, 3), ("disp2_b16", 16, 96, 128, 32, 1, 3), ("disp3_b16", 16, 48, 64, 64, 1, 3),
     ("disp1", 8, 192, 256, 16, 1, 3), ("disp2", 8, 96, 128, 32, 1, 3), ("mask1", 8, 192, 256, 16, 2, 7),
-    ("mask2", 8, 96, 128, 32, 2, 5), ("flow1", 32, 192, 256, 16, 2, 3), ("c5disp1", 2, 480, 640, 16, 1, 3)]
+    ("mask2", 8, 96, 128, 32, 2, 5), ("flow1", 32, 192, 256, 16, 2, 3), ("c5disp1", 2, 480, 640, 16, 1, 3),
+    ("mask1_b16", 16, 192, 256, 16, 2, 7), ("mask2_b16", 16, 96, 128, 32, 2, 5)]
 
 
 def timeit(fn, reps=20):

@@ -45,7 +45,7 @@ def _trainer(ddp, graph, steps, wgrad=None, mode="graph"):
         tr.capture(warmup=1)
         if ddp and mode == "segments":
             assert len(tr.segments) > 4, "expected the backward to be cut at bucket launches"
-        if ddp and mode in ("graph", "inline"):
+        if ddp and mode == "graph":
             assert tr.segments is None and len(tr.graphs) == 1, f"{mode} mode: one graph, all-reduces captured"
     for _ in range(steps):
         tr.step()
@@ -53,7 +53,7 @@ def _trainer(ddp, graph, steps, wgrad=None, mode="graph"):
     return tr.chunk.flat.clone(), tr.chunk.grad.clone()
 
 
-MODES = pytest.mark.parametrize("mode", ["graph", "inline", "segments"])
+MODES = pytest.mark.parametrize("mode", ["graph", "segments"])
 
 
 @MODES
@@ -115,7 +115,7 @@ def test_sync_bn_world1_step_parity(pg):
     _api.clear_programs()
 
 
-def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False, mode="graph"):
+def _c4_trainer(ddp, graph, net_overlap, steps=2, mode="graph"):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
@@ -131,8 +131,6 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, branch=False, mode="graph"):
         assert len(gs.buckets) > 4
     if net_overlap:
         tr.enable_net_overlap()
-    if branch:
-        tr.enable_branch_overlap(serial=branch == "serial")
     if graph:
         tr.capture(warmup=1)
         if ddp and net_overlap and mode == "segments":
@@ -159,20 +157,6 @@ def test_config4_exchange_with_net_overlap(pg, graph, mode):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
-@MODES
-@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_config4_exchange_with_branch_overlap(pg, graph, mode):
-    """The benched config-4 schedule with depth_net's pose / mask branches on their own stream (enable_branch_overlap)
-    under the bucketed exchange: a branch's parameters are reported from the main stream, a bucket launch point joins
-    the branch before it cuts the graph, the comm stream waits on the branch's tail eagerly -- parameters, gradients
-    and moments equal the same branch schedule without an exchange, and its serial form, bit for bit."""
-    ref = _c4_trainer(False, graph, True, branch="serial")
-    for a, b in zip(ref, _c4_trainer(False, graph, True, branch=True)):
-        assert all(torch.equal(x, y) for x, y in zip(a, b))
-    for a, b in zip(ref, _c4_trainer(True, graph, True, branch=True, mode=mode)):
-        assert all(torch.equal(x, y) for x, y in zip(a, b))
-
-
 def _c4_syncbn(pg, graph, sync=True, steps=3, overlaps=None):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
@@ -188,14 +172,11 @@ def _c4_syncbn(pg, graph, sync=True, steps=3, overlaps=None):
         assert tr.sync_bn_capturable
     if overlaps is not None:
         # the benched schedule (or its serial form): depth_net's filter gradients on a side stream, the two
-        # networks on two streams, depth_net's pose / mask branches on a third -- each program (and its branches)
-        # all-reducing on a communicator of its own
+        # networks on two streams -- each program all-reducing on a communicator of its own
         serial = overlaps == "serial"
         tr.enable_wgrad_overlap(serial=serial, only=["pair"])
         if not serial:
             tr.enable_net_overlap()
-        tr.enable_branch_overlap(serial=serial)
-        assert tr._branch_on()
     n = steps
     if graph:
         tr.capture(warmup=1)

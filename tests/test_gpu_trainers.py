@@ -447,66 +447,6 @@ def test_net_overlap_matches_serial(graph, wgrad):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
-@pytest.mark.parametrize("combo", ["plain", "bench"])
-@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_branch_overlap_matches_serial(graph, combo):
-    """Trainer.enable_branch_overlap (config 4): depth_net's pose and explainability-mask branches on a stream of
-    their own beside the decoder, forward and backward, give the serial branch schedule's (the same calls on one
-    stream) parameters, gradients and Adam moments bit for bit after two steps; "bench" adds the benched net overlap
-    and depth_net's filter gradients on their side stream.  The first step's gradients also agree with the schedule
-    without branch overlap (fused filter + data gradients of the branch layers) to rounding."""
-    from tf_depth_estimation_amd import _api, train, variables
-
-    def run(branch):
-        variables.get_store().reset(seed=1)
-        _api.clear_programs()
-        B, H, W = 2, 64, 96
-        tr = train.DepthThenCamTrainer(B, H, W).enable_deterministic()
-        lab = np.random.default_rng(3).uniform(0.1, 2.0, (B, H, W, 1))
-        tr.set_batch(texture(B, H, W, 1).cuda(), texture(B, H, W, 2).cuda(),
-                     torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(),
-                     small_pose(B, 4).cuda())
-        if combo == "bench":
-            tr.enable_wgrad_overlap(only=["pair"])
-            tr.enable_net_overlap()
-        if branch is not None:
-            tr.enable_branch_overlap(serial=branch == "serial")
-            assert tr._branch_on()
-        if graph:
-            tr.capture(warmup=1)
-        tr.step()
-        torch.cuda.synchronize()
-        g1 = [c.grad.clone() for c in tr.chunks]
-        tr.step()
-        torch.cuda.synchronize()
-        return tr.total_loss(), g1, [(c.flat.clone(), c.grad.clone(), c.adam_m.clone(), c.adam_v.clone())
-                                     for c in tr.chunks]
-
-    l0, g0, ref = run("serial")
-    l1, g1, got = run("overlap")
-    np.testing.assert_allclose(l1, l0, rtol=1e-12)
-    for a, b in zip(ref, got):
-        assert all(torch.equal(x, y) for x, y in zip(a, b))
-    for x, y in zip(g0, g1):
-        assert torch.equal(x, y)
-    _, gp, _ = run(None)
-    for x, y in zip(g1, gp):
-        e = ((x.double() - y.double()).norm() / y.double().norm()).item()
-        assert e <= 1e-4, f"branch vs plain schedule first-step gradient rel-L2 {e:.2e}"
-
-
-def test_branch_overlap_exclusive_with_adam_overlaps():
-    from tf_depth_estimation_amd import _api, train, variables
-    variables.get_store().reset(seed=1)
-    _api.clear_programs()
-    tr = train.DepthThenCamTrainer(2, 64, 96)
-    tr.enable_branch_overlap()
-    with pytest.raises(ValueError):
-        tr.enable_adam_overlap(bucket_mb=0.5)
-    with pytest.raises(ValueError):
-        tr.enable_deferred_adam()
-
-
 def test_net_overlap_rejects_exchange_hooks():
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)

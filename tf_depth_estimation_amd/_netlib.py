@@ -147,7 +147,7 @@ def depth_net_spec(H, W, cin, levels=4, scope="depth_cam_net", decay=None, scale
     dec = Decoder(spec, hs, ws, "", 1, levels)
     feats = build_encoder(spec, dec.skip_slots(levels), decay)
     # pose head (:178-186) and explainability-mask branch (:189-206): side branches off the encoder that feed only
-    # the loss (NetProgram.enable_branch_overlap runs them on a stream of their own)
+    # the loss; tagged `branch` for the step timeline
     first_branch = len(spec.ops)
     cam = spec.dense("pose/cam_cnv7", hs[7], ws[7], 256)
     spec.add(ConvBN("pose/cam_cnv7", feats["cnv6b"], cam, 256, 3, 2, decay=decay))

@@ -905,13 +905,18 @@ __global__ void __launch_bounds__(256) head_rw_wgrad_kernel(const HeadArgs p, in
 // KS x 4 packed FMAs per pixel, no LDS in the loop.  The CQ lanes of a pixel are adjacent (its channels one
 // contiguous read); blocks combine their lanes in a fixed order and write one partial per output, summed over the
 // blocks by head_wgrad_reduce_t_kernel.
-constexpr int RWK_SEG = 32;
+// Segment = 4 groups of KS pixels: within a group the window is a ring of KS registers indexed by (pixel + kw) % KS
+// at compile time (fully unrolled), so sliding it costs no moves; dz comes from the dense dz pass (one float2 per
+// pixel).
+template <int KS>
+struct Rwk { static constexpr int SEG = 4 * KS; };
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int KS>
 __global__ void __launch_bounds__(256) head_rwk_wgrad_kernel(const HeadArgs p, int CQ, int segs, long threads,
                                                              float* part) {
   constexpr int NA = KS * 4;          // float2 accumulators per thread (kw, channel)
+  constexpr int SEG = Rwk<KS>::SEG;
   __shared__ f2 red[4][16][NA + 1];
   const int kh = blockIdx.y;
   const long t = blockIdx.x * 256L + threadIdx.x;
@@ -919,40 +924,42 @@ __global__ void __launch_bounds__(256) head_rwk_wgrad_kernel(const HeadArgs p, i
   const long tt = live ? t : 0;
   const int q = (int)(tt % CQ);
   const long u_ = tt / CQ;
-  const int x0 = (int)(u_ % segs) * RWK_SEG;
+  const int x0 = (int)(u_ % segs) * SEG;
   const long rr = u_ / segs;
   const int n = (int)(rr / p.OH), r = (int)(rr - (long)n * p.OH);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
+  const __amdgpu_buffer_rsrc_t rdz = make_rsrc(p.dz, (long)p.N * p.OH * p.OW * 2);
   const int ih = live ? r + kh - p.PT : -1;   // a dead thread reads zeros
+  const long dzrow = ((long)n * p.OH + r) * p.OW;
   f2 acc[KS][4], bacc = {0.f, 0.f};
 #pragma unroll
   for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[kw][j] = f2{0.f, 0.f};
-  // window slot kw = input column ow - PL + kw of the current output pixel ow
+  // ring slot m % KS holds input column x0 - PL + m
   f4 win[KS];
 #pragma unroll
-  for (int kw = 0; kw < KS - 1; ++kw) win[kw + 1] = rw_x(p, rx, n, ih, x0 - p.PL + kw, q);
-  for (int i0 = 0; i0 < RWK_SEG; i0 += 4) {
-    f4 col[4];
-    f2 d[4];
+  for (int m = 0; m < KS - 1; ++m) win[m] = rw_x(p, rx, n, ih, x0 - p.PL + m, q);
+  // per group: its KS new input columns and dz pairs, all loads issued before the first FMA.  (Prefetching the next
+  // group's beside this one's FMAs measured slower: 220 VGPRs, 2 waves per SIMD; mask1 at batch 16 96 vs 78 us.)
+#pragma unroll 1
+  for (int g0 = 0; g0 < SEG; g0 += KS) {
+    f4 col[KS];
+    f2 d[KS];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ow = x0 + i0 + u;
+    for (int u = 0; u < KS; ++u) {
+      const int ow = x0 + g0 + u;
       col[u] = rw_x(p, rx, n, ih, ow - p.PL + KS - 1, q);
-      float dd[2];
-      dz_at<2>(p, n, live ? r : p.OH, ow, dd);   // outside the image (or a dead thread): 0
-      d[u] = f2{dd[0], dd[1]};
+      const bool ok = live && ow < p.OW;
+      d[u] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rdz, ok ? 8 * (int)(dzrow + ow) : OOB, 0, 0));
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int kw = 0; kw < KS - 1; ++kw) win[kw] = win[kw + 1];
-      win[KS - 1] = col[u];
+    for (int u = 0; u < KS; ++u) {
+      win[(u + KS - 1) % KS] = col[u];
 #pragma unroll
       for (int kw = 0; kw < KS; ++kw)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[kw][j] = win[kw][j] * d[u] + acc[kw][j];
+        for (int j = 0; j < 4; ++j) acc[kw][j] = win[(u + kw) % KS][j] * d[u] + acc[kw][j];
       bacc += d[u];
     }
   }
@@ -1086,8 +1093,9 @@ bool head_rwk(const tde_conv_desc_t* d) {
   return g_head_rwk_on && head_tiled(d) && (d->KH == 5 || d->KH == 7) && d->K == 2 && d->w_cin == d->C &&
          (cq == 4 || cq == 8 || cq == 16) && d->pad_top == (d->KH - 1) / 2 && d->pad_left == (d->KW - 1) / 2;
 }
+int rwk_seg(const tde_conv_desc_t* d) { return 4 * d->KH; }   // Rwk<KS>::SEG
 long rwk_threads(const tde_conv_desc_t* d) {
-  return (long)d->N * d->OH * ((d->OW + RWK_SEG - 1) / RWK_SEG) * (d->C / 4);
+  return (long)d->N * d->OH * ((d->OW + rwk_seg(d) - 1) / rwk_seg(d)) * (d->C / 4);
 }
 
 struct WgPlan {
@@ -1367,8 +1375,11 @@ int tde_head_bwd(const tde_conv_desc_t* d, const float* x, const float* w, const
     float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + dz_bytes(d));
     long prow = head_tiles(d, HT_TWG_TH);
     if (dw && head_rwk(d)) {
+      // the dense dz pass (K = 2 floats per pixel), then the row walk reads one float2 per pixel
+      hipLaunchKernelGGL(head_dz_kernel, dim3(grid_for(M * d->K)), dim3(256), 0, st, M, d->K, y, dy, d->y_cstride,
+                         d->y_coff, act, scale, offset, dz);
       const long th = rwk_threads(d);
-      const int segs = (d->OW + RWK_SEG - 1) / RWK_SEG;
+      const int segs = (d->OW + rwk_seg(d) - 1) / rwk_seg(d);
       prow = (th + 255) / 256;
       const dim3 g((unsigned)prow, (unsigned)d->KH);
       if (d->KH == 5) hipLaunchKernelGGL(head_rwk_wgrad_kernel<5>, g, dim3(256), 0, st, a, d->C / 4, segs, th, part);

@@ -24,11 +24,11 @@ Under hipGraph capture there are two modes:
     graph is cut, so each network's forward, loss, backward, exchange and Adam replay as the graph (piece) they are.
     Each chunk all-reduces on a communicator of its own (created in chunk order on every rank): with config 4's two
     networks on two streams, each communicator is used from one graph branch in a fixed order;
-  * mode "inline" (round 5): captured like "graph", but a bucket's all-reduce is issued on the reporting stream
-    itself (after waiting for the chunk's side streams) -- no comm branch, no extra stream.  Measured on one GPU
-    (config 4, world-1 RCCL group): every fork of a comm branch mid-backward adds cross-queue barrier packets that
-    stall the other network's chain (GPU_MAX_HW_QUEUES = 4 FIFO queues), so "graph" with 32 MB
-    buckets ran 782 pairs/s and with one bucket per network 1049, against 1089 without the exchange;
+    Bucket size: measured on one GPU (config 4, world-1 RCCL group, bench.py --exchange on), every comm-branch fork
+    in the middle of a backward stalls the other network's chain (its wait packets sit in FIFO hardware queues shared
+    with it, GPU_MAX_HW_QUEUES = 4): 32 / 64 / 128 MB buckets 782 / 720 / 897 pairs/s, one bucket per
+    network (256 MB) 1049-1055, against 1089-1093 without the exchange -- hence Trainer.enable_ddp's 256 MB default.
+    (Issuing the all-reduce on the reporting stream itself, no branch at all, measured 780-784: worse.);
   * mode "segments" (rounds 2-4; gloo falls back to it): a launch point closes the current graph segment and replay
     runs segment, its buckets eagerly, next segment ... so RCCL stays outside the graphs.
 
@@ -38,6 +38,23 @@ world_size 2.
 import torch
 
 from . import _lib
+
+_GROUPS = {}
+
+
+def pooled_group(purpose, idx):
+    """The idx-th RCCL communicator of `purpose` ("exchange", "syncbn") over the default process group, created on
+    first use and reused by every later trainer of this process (all ranks ask in the same order, so the i-th group
+    of a purpose is the same communicator everywhere).  One new group per trainer would pile up communicators -- and
+    their device buffers and proxy threads -- in a process that builds many trainers (the GPU tests).  Entries hold
+    the default group they were made under, so a re-initialised default group gets fresh ones."""
+    import torch.distributed as dist
+    world = dist.distributed_c10d._get_default_group()
+    key = (id(world), purpose, idx)
+    hit = _GROUPS.get(key)
+    if hit is None:
+        hit = _GROUPS[key] = (world, dist.new_group(backend="nccl"))
+    return hit[1]
 
 
 class Bucket:
@@ -112,8 +129,8 @@ class GradSync:
         self.log = []               # launch order (names), for tests
         nccl = self.gpu and dist.is_initialized() and dist.get_backend(group) == "nccl"
         self.mode = mode or ("graph" if nccl else "segments")
-        if self.mode not in ("graph", "inline", "segments") or (self.mode != "segments" and not nccl):
-            raise ValueError(f"exchange mode {self.mode!r}: 'graph' / 'inline' need RCCL (nccl backend), else 'segments'")
+        if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
+            raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
         self.captured = self.mode != "segments"
         # graph mode: per chunk a comm stream and a communicator of its own (same creation order on every rank)
         # pre_fork(chunk): issue whatever the chunk's program still holds back for its side streams (the deferred
@@ -121,10 +138,9 @@ class GradSync:
         self.pre_fork = pre_fork
         self.comm_of, self.group_of = {}, {}
         if self.captured:
-            for c in self.chunks:
-                if self.mode == "graph":
-                    self.comm_of[id(c)] = _lib.dedicated_stream()
-                self.group_of[id(c)] = dist.new_group(backend="nccl") if group is None else group
+            for i, c in enumerate(self.chunks):
+                self.comm_of[id(c)] = _lib.dedicated_stream()
+                self.group_of[id(c)] = pooled_group("exchange", i) if group is None else group
         self.forked = set()         # chunks whose comm stream has work not yet joined (graph mode)
         self.begin_step()
 
@@ -205,13 +221,6 @@ class GradSync:
             chunk = buckets[0].chunk
         if self.pre_fork is not None:
             self.pre_fork(chunk)
-        if self.mode == "inline":
-            cur = torch.cuda.current_stream()
-            for sd in (self.side_streams(chunk) if self.side_streams else ()):
-                _lib.wait_stream(cur, sd)
-            for b in buckets:
-                dist.all_reduce(b.view(), op=dist.ReduceOp.AVG, group=self.group_of[id(chunk)])
-            return
         comm = self.comm_of[id(chunk)]
         _lib.wait_stream(comm, torch.cuda.current_stream())
         for sd in (self.side_streams(chunk) if self.side_streams else ()):

@@ -74,7 +74,7 @@ class View:
 
 class Op:
     params = ()
-    branch = 0      # 1: a side branch of the network (NetProgram.enable_branch_overlap)
+    branch = 0      # 1: a side branch of the network (depth_net's pose / mask heads: a timeline label only)
 
 
 class ConvBN(Op):
@@ -327,7 +327,6 @@ class NetProgram:
         # SyncBN: bn_sync(t) all-reduces (sums) a float64 device tensor in place across
         # bn_world data-parallel replicas; None = BatchNorm over the local batch (the default)
         self.bn_sync, self.bn_world = None, 1
-        self.bn_sync_branch = None   # SyncBN of the side branches' layers (their own communicator, branch overlap)
         self._bn_sums = {}
         self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
         # filter-gradient overlap (enable_wgrad_overlap): side stream, its workspace per batch, dz ring
@@ -354,10 +353,6 @@ class NetProgram:
         self.pre_op = None
         self.params_ready = None
         self.pre_backward = None    # called first thing in backward (before any gradient is written)
-        # TDE_SPLIT_HEAD=k > 0: weight splits staged on a side stream (_stage_splits: the first k conv layers' forward
-        # images on the compute stream, the rest beside them).  Default 0 (all at the first conv): measured, the extra
-        # stream costs the config-4 step ~25 % (GPU_MAX_HW_QUEUES = 4: another stream's packets queue behind the others)
-        self.split_head = _env_nonneg("TDE_SPLIT_HEAD", 0)
         self.timeline = None        # StepTimeline (diagnostic): a device stamp after every op, under capture only
 
     def _split_plan(self, N):
@@ -563,53 +558,6 @@ class NetProgram:
         w = self._ws.setdefault(N, Workspace())
         return w.get(ws, dz, "cuda")
 
-    # ---------------------------------------------------------------- branch overlap
-    def enable_branch_overlap(self, on=True, serial=False):
-        """Run the spec's side branches (ops with `branch == 1`: depth_net's pose and explainability-mask heads,
-        nets_optflow_depth_pairtest.py:178-206, which read encoder features and feed only the loss) on a stream of
-        their own, beside the decoder, in forward and backward.  Their ops use their own workspace, their own dz
-        buffers and the split filter / data-gradient calls (no filter-gradient side stream: every fork of a
-        captured step stays one level deep).  A branch op's data gradient into an encoder feature's gradient (the
-        one write the branch shares with the main chain) is ordered after the main chain's earlier writes to that
-        buffer and before its later ones (events), so every buffer sees the serial order of writes: results equal
-        serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
-        has = any(getattr(op, "branch", 0) for op in self.spec.ops)
-        self.branch_stream = None
-        if on and has:
-            self.branch_stream = SERIAL if serial else _lib.owned_stream(self, "branch")
-        self._branch_bufs = {op.dst.buf.name for op in self.spec.ops if getattr(op, "branch", 0)}
-        return self
-
-    def _branch_mode(self):
-        """The branch stream (or SERIAL) when the branch overlap applies to this call: not under the instrumented
-        eager step (its HIP-event timer records on one stream), and with SyncBN only when the branches have a
-        communicator of their own (RCCL, Trainer.enable_sync_bn)."""
-        bs = getattr(self, "branch_stream", None)
-        if bs is None or (self.bn_sync is not None and self.bn_sync_branch is None) or not self._production():
-            return None
-        return bs
-
-    def join_branch(self):
-        """Order the current (main) stream after everything the side-branch stream issued in this backward, if it
-        was forked: a graph segment must end with its forked branches joined (the exchange's launch points).  A
-        later branch op forks again from the main stream."""
-        bst = getattr(self, "_bst", None)
-        if bst is None or bst["refork"]:
-            return
-        if not bst["started"]:
-            # a graph cut before the branch's first op: the fork event recorded at the start of backward belongs to
-            # an ended capture segment, so the branch must fork from an event recorded when it starts
-            bst["refork"] = True
-            return
-        _lib.wait_stream(torch.cuda.current_stream(), bst["stream"])
-        bst["pend"].clear()
-        bst["refork"] = True
-
-    def branch_streams(self):
-        """The side-branch stream while a backward has it forked (the exchange's comm stream waits on its tail)."""
-        bst = getattr(self, "_bst", None)
-        return (bst["stream"],) if bst is not None and bst["started"] and not bst["refork"] else ()
-
     # ---------------------------------------------------------------- forward
     def forward(self, run, x, is_training=True, fold_bn=False):
         """x: [N,H,W,cin] fp32 on the device.  Returns the output view tensors.  fold_bn (inference only):
@@ -643,36 +591,10 @@ class NetProgram:
             self._cur_split = (key, {})
             for job in plan:
                 split_todo.setdefault(job[0], []).append(job)
-        main = torch.cuda.current_stream()
-        bmode = self._branch_mode() if is_training and not fold_bn else None
-        split_wait = split_side = None
-        if split_todo and self.pre_op is None and bmode is None and self.split_head > 0 and self._production():
-            split_todo, split_wait, split_side = self._stage_splits(split_todo, main)
-        ws_a, wsb_a = ws, wsb
-        forked = False
         tl = self.timeline
         for i, op in enumerate(spec.ops):
             if tl is not None and i > 0:
                 tl.mark(self.prefix, "F", spec.ops[i - 1])
-            if split_wait is not None and i == split_wait[0]:
-                _lib.wait_event(main, split_wait[1])     # the side stream's forward images are written
-                split_wait = None
-            br = bmode is not None and getattr(op, "branch", 0) == 1
-            if br and bmode is not SERIAL:
-                if not forked:
-                    # the branches read encoder features only, all issued by now
-                    _lib.wait_stream(bmode, main)
-                    forked = True
-                    if tl is not None:
-                        with torch.cuda.stream(bmode):
-                            tl.mark(self.prefix, "F", "branch fork")
-                torch.cuda.set_stream(bmode)
-                ws = self._scratch_side(N, "branch")
-                wsb = ws.numel() * 4
-            else:
-                torch.cuda.set_stream(main)
-                ws, wsb = ws_a, wsb_a
-            st = _lib.stream_ptr()
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             if self.pre_op is not None and isinstance(op, (ConvBN, Head)):
@@ -680,11 +602,8 @@ class NetProgram:
             if isinstance(op, ConvBN):
                 if i in split_todo:
                     # one split launch for every pending layer whose weights are final by now (all of them
-                    # unless an optimizer step is still running on a side stream); a branch op splits only its own
-                    # (main-chain ops read theirs on the other stream)
-                    ready = ([i] if br else
-                             [j for j in split_todo if (self.params_ready is None or self.params_ready(self, j)) and
-                              not (forked and getattr(spec.ops[j], "branch", 0))])
+                    # unless an optimizer step is still running on a side stream)
+                    ready = [j for j in split_todo if self.params_ready is None or self.params_ready(self, j)]
                     self._issue_split([job for j in ready for job in split_todo.pop(j)])
                 d = op.desc(N)
                 if not fold_bn:
@@ -727,7 +646,7 @@ class NetProgram:
                     fn = lib.tde_deconv2d_fwd_bn if op.deconv else lib.tde_conv2d_fwd_bn
                     _lib.check(fn(ctypes_ref(d), run.vptr(op.src), ptr(w), ptr(z), ctypes_ref(bn), ptr(ws), wsb, st),
                                op.layer + " bn sums")
-                    (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(sums)
+                    self.bn_sync(sums)
                     _lib.check(lib.tde_bn_fwd_from_sums(M, op.K, G, Mg * self.bn_world, ptr(z), ptr(sums), ptr(beta),
                                                         1e-3, op.decay, int(self.bessel), ptr(mm), ptr(mv), ptr(sm[0]),
                                                         ptr(sm[1]), run.vptr(op.dst), op.dst.buf.cs, op.dst.coff, 1, st),
@@ -777,40 +696,7 @@ class NetProgram:
                                              t.buf.cs, t.coff, 0, st), "copy")
         if tl is not None and spec.ops:
             tl.mark(self.prefix, "F", spec.ops[-1])
-        torch.cuda.set_stream(main)
-        if forked:
-            _lib.wait_stream(main, bmode)
-        if split_side is not None:
-            _lib.wait_stream(main, split_side)            # the backward's images (and the join of the side branch)
         return [run.view_tensor(v) for v in spec.outputs]
-
-    def _stage_splits(self, todo, main):
-        """The step's weight splits (halo and ring images, _split_plan) off the forward's critical path: the FORWARD
-        images of the first `split_head` conv layers on the main stream now; on a side stream forked here, the other
-        layers' forward images (the main stream waits for them before the first of those layers) and then every
-        backward image (joined at the end of the forward).  Under capture the side stream is a one-level branch.
-        Returns (empty todo, (op index to wait at, event) or None, side stream)."""
-        ops = self.spec.ops
-
-        def fwd_job(job):      # a conv's forward reads image 0, a deconv's forward (the virtual DGRAD) image 1
-            return job[1] == (1 if ops[job[0]].deconv else 0)
-        idx = sorted(todo)
-        head = set(idx[:self.split_head])
-        now = [j for i in idx if i in head for j in todo[i] if fwd_job(j)]
-        late_f = [j for i in idx if i not in head for j in todo[i] if fwd_job(j)]
-        late_b = [j for i in idx for j in todo[i] if not fwd_job(j)]
-        self._issue_split(now)
-        side = _lib.owned_stream(self, "split")
-        _lib.wait_stream(side, main)
-        wait = None
-        with torch.cuda.stream(side):
-            self._issue_split(late_f)
-            if late_f:
-                ev = torch.cuda.Event()
-                ev.record(side)
-                wait = (min(j[0] for j in late_f), ev)
-            self._issue_split(late_b)
-        return {}, wait, side
 
     # ---------------------------------------------------------------- backward
     def backward(self, run, grad_outputs, need_input_grad=False, on_grads=None, grad_accumulate=True):
@@ -873,63 +759,16 @@ class NetProgram:
         for j, o in enumerate(spec.ops):
             if isinstance(o, ConvBN):
                 conv_rank[j] = len(conv_rank)
-        # branch overlap (enable_branch_overlap): the side branches' ops on their stream from the start of backward
-        # (their output gradients come from the loss); pend: gradient buffer -> event after a branch op's write into
-        # it that the main chain also writes or reads later
-        main = torch.cuda.current_stream()
-        bmode = self._branch_mode()
-        ws_a, wsb_a, dz_a = ws, wsb, dz
-        bst = self._bst = None
-        if bmode is not None and bmode is not SERIAL:
-            # fork: the event the branch's first op waits on; pend: gradient buffer -> event after a branch op's
-            # write into it that the main chain also touches later; refork: join_branch() joined the branch
-            e0 = torch.cuda.Event()
-            e0.record(main)
-            bst = self._bst = dict(main=main, stream=bmode, fork=e0, started=False, pend={}, refork=False)
-        br_names = []     # parameters a branch op has written, reported (on_grads) from the main stream
         tl = self.timeline
         for i in range(len(spec.ops) - 1, -1, -1):
             op = spec.ops[i]
             if tl is not None and i + 1 < len(spec.ops):
                 tl.mark(self.prefix, "B", spec.ops[i + 1])
-            br = bmode is not None and getattr(op, "branch", 0) == 1
-            real_br = br and bmode is not SERIAL
-            if real_br:
-                if not bst["started"] or bst["refork"]:
-                    if bst["refork"]:
-                        bst["fork"] = torch.cuda.Event()
-                        bst["fork"].record(main)
-                    _lib.wait_event(bmode, bst["fork"])
-                    bst["started"], bst["refork"] = True, False
-                    if tl is not None:
-                        with torch.cuda.stream(bmode):
-                            tl.mark(self.prefix, "B", "branch fork")
-                torch.cuda.set_stream(bmode)
-                ws = self._scratch_side(N, "branch")
-                wsb = ws.numel() * 4
-            else:
-                torch.cuda.set_stream(main)
-                ws, wsb, dz = ws_a, wsb_a, dz_a
-                pend = bst["pend"] if bst is not None else None
-                for name in {op.dst.buf.name, op.src.buf.name} if pend else ():
-                    ev = pend.pop(name, None)
-                    if ev is not None:
-                        _lib.wait_event(main, ev)
-                if br_names and on_grads is not None:
-                    # the branch's finished parameters, reported from the main stream: the exchange's launch point
-                    # (a graph cut under capture) joins the branch first (Trainer._join_chunk_wgrad -> join_branch)
-                    names, br_names = br_names, []
-                    on_grads(names)
-            st = _lib.stream_ptr()
-            # a branch op whose input is a main-chain buffer (an encoder feature): its data gradient is the shared write
-            shared = br and op.src.buf.name not in self._branch_bufs
             if self.timer is not None:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
-            if br and not isinstance(op, ConvBN):
-                assert not shared, f"{type(op).__name__} in a branch writes a main-chain gradient"
             if isinstance(op, ConvBN):
-                use_side = (side is not None and not br and conv_rank[i] >= self.wgrad_tail and
+                use_side = (side is not None and conv_rank[i] >= self.wgrad_tail and
                             N * op.dst.H * op.dst.W > self.wgrad_inline_m)
                 d = op.desc(N)
                 self._use_split(d, i, N)
@@ -940,7 +779,7 @@ class NetProgram:
                     d.y_absmax = run.absmax_ptr(i)
                 M = N * op.dst.H * op.dst.W
                 sm = run.stats.get(i)
-                if side is not None or br:
+                if side is not None:
                     dz = self._dz_layer(N, i, M * op.K)
                 if not op.bn:
                     # BN-free layer: dz = dy * relu'(y), bias gradient (fixed-order fp64 sums)
@@ -963,7 +802,7 @@ class NetProgram:
                     _lib.check(lib.tde_bn_sums(M, op.K, G, ptr(zi), dy, op.dst.buf.cs, op.dst.coff, ptr(sm[0]),
                                                ptr(sm[1]), ptr(beta), 1, 1, ptr(gs), ptr(ls), ptr(ws), wsb, st),
                                op.layer + " bn sums")
-                    (self.bn_sync_branch if br and self.bn_sync_branch else self.bn_sync)(gs)
+                    self.bn_sync(gs)
                     _lib.check(lib.tde_bn_bwd_from_sums(M, op.K, G, Mg * self.bn_world, ptr(zi), ptr(sm[0]), ptr(sm[1]),
                                                         ptr(beta), dy, op.dst.buf.cs, op.dst.coff, ptr(gs), ptr(ls),
                                                         ptr(dz), ptr(self.G(f"{op.layer}/BatchNorm/beta")), pacc, 1,
@@ -977,28 +816,7 @@ class NetProgram:
                                                   run.absmax_ptr(i), ptr(ws), wsb, st), op.layer + " bn_bwd")
                 w, gw = self.P(f"{op.layer}/weights"), self.G(f"{op.layer}/weights")
                 fl = conv_flops(op, N)
-                if br:
-                    # branch op: filter gradient, then data gradient, as two calls on the branch stream; a data
-                    # gradient into a main-chain buffer waits for the main chain's writes issued before it
-                    wg = lib.tde_deconv2d_bwd_filter if op.deconv else lib.tde_conv2d_bwd_filter
-                    a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
-                    with self._span("conv_wgrad", fl, conv_bytes(op, N)):
-                        _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
-                    if src_needs:
-                        if shared and real_br:
-                            ev = torch.cuda.Event()
-                            ev.record(main)
-                            _lib.wait_event(bmode, ev)
-                        acc = mark(op.src)
-                        fd = lib.tde_deconv2d_bwd_data if op.deconv else lib.tde_conv2d_bwd_data
-                        with self._span("conv_dgrad", fl, conv_bytes(op, N)):
-                            _lib.check(fd(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True), acc, ptr(ws), wsb,
-                                          st), op.layer + " bwd data")
-                        if shared and real_br:
-                            ev = torch.cuda.Event()
-                            ev.record(bmode)
-                            bst["pend"][op.src.buf.name] = ev
-                elif use_side:
+                if use_side:
                     # this layer's filter gradient joins the deferred group; the group goes to the side stream
                     # behind one event recorded after the BN backward that completes it.  The data gradient is
                     # issued BEFORE the side stream waits on that event: under capture the graph executor keeps
@@ -1046,9 +864,7 @@ class NetProgram:
                     a1, a2 = (ptr(dz), run.vptr(op.src)) if op.deconv else (run.vptr(op.src), ptr(dz))
                     with self._span("conv_wgrad", fl, conv_bytes(op, N)):
                         _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, ptr(ws), wsb, st), op.layer + " wgrad")
-                if br:
-                    br_names += [f"{self.prefix}/{n}" for n, _, _ in op.params]
-                elif side is not None:
+                if side is not None:
                     # report the parameters of the filter gradients issued so far (a deferred one is reported
                     # once its group is on the side stream)
                     names, self._wg_issued = self._wg_issued, []
@@ -1063,7 +879,7 @@ class NetProgram:
                 acc = mark(op.src) if src_needs else 0
                 hw, hgw, hgb = (ptr(self.P(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/weights")),
                                 ptr(self.G(f"{op.layer}/biases")))
-                if side is not None and self.head_wgrad_side and not br:
+                if side is not None and self.head_wgrad_side:
                     # the head's filter gradient joins the deferred group on the side stream (it reads x, y and
                     # dy, none of which the rest of backward rewrites); the data gradient stays on this stream
                     def head_wgrad_call(wsp, wsb2, d=d, x=run.vptr(op.src), y=run.vptr(op.dst),
@@ -1093,9 +909,7 @@ class NetProgram:
                                                 run.vptr(op.src, True) if src_needs else None, acc,
                                                 hgw, hgb, pacc, op.act, op.scale, op.offset, ptr(ws), wsb, st),
                                op.layer + " bwd")
-                if br:
-                    br_names += [f"{self.prefix}/{n}" for n, _, _ in op.params]
-                elif on_grads is not None:
+                if on_grads is not None:
                     on_grads([f"{self.prefix}/{n}" for n, _, _ in op.params])
             elif isinstance(op, Resize):
                 s, t = op.src, op.dst
@@ -1111,11 +925,6 @@ class NetProgram:
                                              run.vptr(s, True), s.buf.cs, s.coff, acc, st), "copy bwd")
         if tl is not None and spec.ops:
             tl.mark(self.prefix, "B", spec.ops[0])
-        torch.cuda.set_stream(main)
-        self.join_branch()
-        self._bst = None
-        if br_names and on_grads is not None:
-            on_grads(br_names)
         if side is not None:
             self._flush_wgrad()
             names, self._wg_issued = self._wg_issued, []

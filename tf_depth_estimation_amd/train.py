@@ -307,8 +307,8 @@ class Trainer:
     def enable_deferred_adam(self, first_mb=2.0):
         """Run each step's Adam at the start of the next step, overlapped with its forward (DeferredAdam).
         The parameters then lag the gradients by one update until flush()."""
-        if self.grad_sync is not None or self.adam_ov is not None or self._branch_on():
-            raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap or branch overlap")
+        if self.grad_sync is not None or self.adam_ov is not None:
+            raise ValueError("deferred Adam is for the single-GPU step without another Adam overlap")
         if self.net_stream is not None:
             # the overlapped capture has no _begin() piece: a deferred update would never be launched
             raise ValueError("deferred Adam and net overlap are exclusive")
@@ -335,9 +335,8 @@ class Trainer:
         with a data-parallel exchange the update must wait for the all-reduce).  on_wgrad_stream: on each
         program's filter-gradient stream (enable_wgrad_overlap first), behind the filter gradients it holds,
         so the compute stream never waits for it until the end of the step."""
-        if self.grad_sync is not None or self._branch_on():
-            raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it) without "
-                             "branch overlap")
+        if self.grad_sync is not None:
+            raise ValueError("Adam overlap is for the single-GPU step (the exchange orders Adam after it)")
         if self.net_stream is not None:
             raise ValueError("Adam overlap and net overlap are exclusive")
         opts = self.opt.opts if hasattr(self.opt, "opts") else [self.opt]
@@ -368,36 +367,20 @@ class Trainer:
             p.enable_wgrad_overlap(on and (only is None or name in only), serial)
         return self
 
-    def enable_branch_overlap(self, on=True, serial=False):
-        """The networks' side branches (depth_net's pose and explainability-mask heads) on a stream of their own,
-        beside the decoder, forward and backward (NetProgram.enable_branch_overlap; serial=True: the same calls on
-        one stream, the bit-exact reference).  With the data-parallel exchange a branch's finished parameters are
-        reported from the main stream, a bucket launch point joins the branch first (a graph segment ends with its
-        forks joined) and the comm stream waits on the branch stream's tail eagerly.  Not with the Adam overlap or
-        deferred Adam."""
-        if on and (self.adam_ov is not None or self.dadam is not None):
-            raise ValueError("branch overlap and the Adam overlap / deferred Adam are exclusive")
-        if on and not serial:
-            self._check_sync_bn_streams(branch=True)
-        for p in self.programs():
-            p.enable_branch_overlap(on, serial)
-        return self
-
-    def _check_sync_bn_streams(self, net=False, branch=False):
+    def _check_sync_bn_streams(self, net=False):
         """RCCL SyncBN across replicas issues its all-reduces from every stream that runs a BatchNorm.  Per-program
-        (and per-branch) communicators keep each communicator on one stream, but with GPU_MAX_HW_QUEUES = 4 the
-        kernels of different communicators may share a hardware queue in a different order on different GPUs,
-        which no world > 1 run has checked: refuse SyncBN over more than one replica combined with the
-        net or branch overlap, and an explicit shared group with any overlap or the gradient exchange."""
+        communicators keep each communicator on one stream, but with GPU_MAX_HW_QUEUES = 4 the kernels of different
+        communicators may share a hardware queue in a different order on different GPUs, which no world > 1 run has
+        checked: refuse SyncBN over more than one replica combined with the net overlap, and an explicit
+        shared group with any overlap or the gradient exchange."""
         if not getattr(self, "sync_bn", False):
             return
         world = max((getattr(p, "bn_world", 1) for p in self.programs()), default=1)
         net = net or self.net_stream is not None
-        branch = branch or self._branch_on()
-        if world > 1 and (net or branch):
-            raise ValueError("SyncBN over RCCL at world > 1 runs its collectives from one stream: no net or branch "
-                             "overlap with it")
-        if getattr(self, "_sync_bn_group", None) is not None and (net or branch or self.grad_sync is not None):
+        if world > 1 and net:
+            raise ValueError("SyncBN over RCCL at world > 1 runs its collectives from one stream: no net overlap "
+                             "with it")
+        if getattr(self, "_sync_bn_group", None) is not None and (net or self.grad_sync is not None):
             raise ValueError("SyncBN with an explicit process group shares one communicator over several streams: "
                              "no overlap or bucketed exchange with it")
 
@@ -411,9 +394,6 @@ class Trainer:
     def _tl(self, label):
         if self.timeline is not None:
             self.timeline.mark("trainer", "T", label)
-
-    def _branch_on(self):
-        return any(getattr(p, "branch_stream", None) is not None for p in self.programs())
 
     def join_wgrad(self):
         for p in self.programs():
@@ -447,7 +427,6 @@ class Trainer:
         p = self._program_of(chunk)
         for q in ([p] if p is not None else self.programs()):
             q.join_wgrad()
-            q.join_branch()
 
     def _chunk_side_streams(self, chunk):
         """Eagerly: the streams besides the current one that write `chunk`'s gradients (its program's
@@ -456,7 +435,7 @@ class Trainer:
         if p is None:
             return ()
         wg = () if p.wgrad_stream is None or isinstance(p.wgrad_stream, str) else tuple(p.wgrad_streams)
-        return wg + p.branch_streams()
+        return wg
 
     def _flush_chunk_wgrad(self, chunk):
         """Issue the deferred filter-gradient calls of the program owning `chunk` on its side stream (a captured
@@ -466,7 +445,7 @@ class Trainer:
             if q.wgrad_stream is not None:
                 q._flush_wgrad()
 
-    def enable_ddp(self, world, bucket_mb=32.0, group=None, mode=None):
+    def enable_ddp(self, world, bucket_mb=256.0, group=None, mode=None):
         """Bucketed gradient all-reduce overlapped with backward (ddp.GradSync).  mode "graph" (default over RCCL):
         the all-reduces are captured into the step's graphs on a per-network comm branch, joined at the end of that
         network's backward (its Adam then runs inline, as in the single-GPU step); "segments": the round-2 scheme,
@@ -498,18 +477,14 @@ class Trainer:
                 dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
             return sync
 
-        for p in self.programs():
+        from .ddp import pooled_group
+        for pi, p in enumerate(self.programs()):
             # over RCCL one communicator PER PROGRAM (created in program order on every rank): each program's
             # collectives are then issued from one stream in a fixed order, so the two networks of config 4 may run
             # on two streams (enable_net_overlap) without their all-reduces meeting in different orders on
             # different GPUs
-            g = dist.new_group(backend="nccl") if nccl and group is None else group
+            g = pooled_group("syncbn", pi) if nccl and group is None else group
             p.bn_sync, p.bn_world = make_sync(g), world
-            # the program's side branches (enable_branch_overlap) issue theirs from the branch stream: a communicator
-            # of their own as well
-            p.bn_sync_branch = None
-            if nccl and group is None and any(getattr(op, "branch", 0) for op in p.spec.ops):
-                p.bn_sync_branch = make_sync(dist.new_group(backend="nccl"))
         self.sync_bn = True
         self.sync_bn_capturable = nccl
         self._sync_bn_group = group
