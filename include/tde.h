@@ -103,7 +103,8 @@ int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
 /* Which conv calls of conv math 4 run the LDS-DMA ring tiles (process-wide, set before capture): a mask of
  * 1 = forward calls (tde_conv2d_fwd*, tde_deconv2d_fwd*), 2 = data-gradient calls (tde_*_bwd_data and the data half
- * of tde_*_bwd), 4 = filter-gradient GEMMs.  Default 0 (env TDE_RING).  Returns the previous mask, -1 if out of range.
+ * of tde_*_bwd), 4 = filter-gradient GEMMs, 8 = forward calls whose GEMM gets 64-row tiles (the deep levels).
+ * Default 0 (env TDE_RING): measured slower at config 4.  Returns the previous mask, -1 if out of range.
  * Results are the same either way (tests/test_gpu_kernels.py::test_ring_*); only speed differs. */
 int tde_set_conv_ring(int roles);
 int tde_get_conv_ring(void);

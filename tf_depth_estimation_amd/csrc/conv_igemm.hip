@@ -1208,19 +1208,24 @@ static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr
 // ---- LDS-DMA ring tiles (conv_ring.hip) for the fp16x3 GEMMs that take neither the halo nor the skinny path, by
 // the role of the call (TDE_RING / tde_set_conv_ring: a mask of RING_FWD = the forward calls tde_conv2d_fwd* /
 // tde_deconv2d_fwd*, RING_DATA = the data-gradient calls (tde_*_bwd_data, the data half of tde_*_bwd), RING_FILTER =
-// the filter-gradient GEMMs).  Default 0 (opt-in): measured on config 4 (profiles/r05/ring_ab.md), the ring tiles win
-// some forward GEMMs (icnv5 / icnv6 -25 %) but lose the backward ones, whose two GEMMs the register-staged tiles run
-// as ONE fused launch (igemm_bwd2) that fills the chip where neither alone does, and the per-step B images (4 bytes
-// per weight, 384 MB written for the two networks' forward GEMMs) cost ~190 us of prep: 1066 pairs/s with the
-// forward ring vs 1079 without, 994 with every GEMM on it.
-enum { RING_FWD = 1, RING_DATA = 2, RING_FILTER = 4, RING_ALL = 7 };
+// the filter-gradient GEMMs, RING_DEEP = the forward calls whose GEMM the planner gives 64-row tiles: the deep
+// levels).  Measured on config 4 (profiles/r05/ring_ab.md), the ring tiles win the deep forward GEMMs (icnv5 / icnv6
+// -25 %) but lose the backward ones, whose two GEMMs the register-staged tiles run as ONE fused launch (igemm_bwd2)
+// that fills the chip where neither alone does, and the per-step B images cost 4 bytes per weight of prep (384 MB
+// for every forward GEMM of the two networks, ~190 us): 1066 pairs/s with every forward call on the ring vs 1079
+// without, 994 with every GEMM on it, 1076-1078 with the deep forward calls only (their layers hold nearly all the
+// weights, so the prep stays) vs 1085-1092 without.  Default 0: opt-in.
+enum { RING_FWD = 1, RING_DATA = 2, RING_FILTER = 4, RING_ALL = 7, RING_DEEP = 8 };
 static long g_ring = env_long("TDE_RING", 0);
 
 // Plan + B-image geometry of the ring GEMM of d in `mode` (MODE_FWD / MODE_DGRAD / MODE_PS / MODE_WGRAD) for a call
 // of `role` (RING_ALL: any call -- the workspace queries); false: not on the ring.  The column tile follows
 // make_plan's rule over the ring widths {32, 64, 96, 128}; make_plan picks rows and splits.
 static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg, int role) {
-  if (!(g_ring & role) || g_conv_math != 4) return false;
+  if (g_conv_math != 4) return false;
+  const bool full = (g_ring & role & RING_ALL) != 0;
+  const bool deep = !full && (g_ring & RING_DEEP) && (role & RING_FWD);   // 64-row forward tiles only
+  if (!full && !deep) return false;
   if (mode == MODE_WGRAD) {
     // the filter gradient of every layer the halo-tiled WGRAD does not take; no B image (both operands activations)
     HwgPlan wp;
@@ -1248,6 +1253,7 @@ static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg
     pl.bm = bm; pl.bn = bn; pl.splits = 1; pl.kt_per = tde_cdiv(4L * d.K, BK3);
     pl.gx = tde_cdiv(M, bm); pl.gy = Nn / bn; pl.gz = 1;
     pl.rows = (int)((long)d.N * d.H * d.W); pl.cols = d.C;
+    if (deep && bm != 64) return false;
     rg = RingGeom{MODE_PS, bm, bn, 1, tde_cdiv(4L * d.K, BK3), Nn / bn};
     return true;
   }
@@ -1270,6 +1276,7 @@ static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg
   // the narrow GEMMs whose column tile would be 16 or 48 in the register-staged planner (16-channel outputs: a 32-wide
   // ring tile computes twice the columns) stay there
   if (make_plan(d, mode).bn % 32 != 0) return false;
+  if (deep && pl.bm != 64) return false;
   rg = RingGeom{mode, pl.bm, bn, ncls, tde_cdiv(Kd, BK3), tde_cdiv(Nn, bn)};
   return true;
 }
@@ -1973,7 +1980,7 @@ int tde_set_conv_math(int mode) {
 int tde_get_conv_math(void) { return g_conv_math; }
 
 int tde_set_conv_ring(int roles) {
-  if (roles < 0 || roles > RING_ALL) return -1;
+  if (roles < 0 || roles > (RING_ALL | RING_DEEP)) return -1;
   const int prev = (int)g_ring;
   g_ring = roles;
   return prev;
