@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 8
+#define TDE_ABI_VERSION 9
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
