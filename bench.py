@@ -580,11 +580,12 @@ def main():
                 rf["mfma_busy_note"] = ("SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs) over the conv "
                                         "family's dispatches (includes the 2 redundant fp16 products of fp16x3 and "
                                         "tile padding)")
-                cyc = conv_t.get("gui_active_cycles_per_step")
-                if cyc and conv_t.get("hbm_bytes_per_step"):
-                    rf["hbm_gbs"] = round(conv_t["hbm_bytes_per_step"] / (cyc / 2.1e9) / 1e9, 1)
-                    rf["hbm_gbs_note"] = "PMC bytes / conv-family busy cycles at an assumed 2.1 GHz"
+            if conv_t.get("hbm_bytes_per_step") and conv_ms > 0:
+                rf["hbm_gbs"] = round(conv_t["hbm_bytes_per_step"] / (conv_ms * 1e-3) / 1e9, 1)
+                rf["hbm_gbs_note"] = ("PMC conv-family bytes per step / the conv family's busy time per step measured "
+                                      "here (the roofline's timing): no clock assumption")
             rf["traffic_source"] = os.path.relpath(tr_path, ROOT)
+            rf["traffic_label"] = pm.get("label")
         if world == 1 and not args.no_secondary:
             sec = {}
             for name in ("config2", "config3", "config5"):
