@@ -59,11 +59,13 @@ def main():
     fetch = load(a.fetch, "FETCH_SIZE")
     write = load(a.write, "WRITE_SIZE")
     fams = {}
+    by_kernel = []
     for name in set(fetch) | set(write):
         fam = family(name)
         rd = 2.0 * fetch.get(name, (0.0, 0))[0] * 1024 / a.steps
         wr = write.get(name, (0.0, 0))[0] * 1024 / a.steps
         launches = max(fetch.get(name, (0, 0))[1], write.get(name, (0, 0))[1]) / a.steps
+        by_kernel.append((rd + wr, rd, wr, launches, name))
         f = fams.setdefault(fam, {"read_bytes_per_step": 0.0, "write_bytes_per_step": 0.0, "launches_per_step": 0.0})
         f["read_bytes_per_step"] += rd
         f["write_bytes_per_step"] += wr
@@ -99,7 +101,10 @@ def main():
     out = {"label": a.label, "steps": a.steps,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950 "
                      "16-B/lane read calibration, MI355X_MICROARCH.md §HBM), KB -> bytes, summed per family / steps",
-           "families": fams}
+           "families": fams,
+           "top_kernels_by_bytes": [{"kernel": n[:120], "hbm_bytes_per_step": round(t), "read": round(r),
+                                     "write": round(w), "launches_per_step": round(l, 2)}
+                                    for t, r, w, l, n in sorted(by_kernel, reverse=True)[:40]]}
     if a.sq:
         out["mfma_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE (own pass): "
                               "mfma_busy = MFMA SIMD-cycles / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)")

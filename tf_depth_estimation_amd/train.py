@@ -848,15 +848,27 @@ class DepthThenCamTrainer(Trainer):
                 ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
 
     def _chain_pair(self):
+        self._chain_pair_a()
+        self._chain_pair_b()
+
+    def _chain_single(self):
+        self._chain_single_a()
+        self._chain_single_b()
+
+    def _chain_pair_a(self):
         self._tl("pair chain start")
         self._p_fwd_pair()
+
+    def _chain_pair_b(self):
         self._p_loss()
         self._tl("pair loss")
         self._p_bwd_pair()
 
-    def _chain_single(self):
+    def _chain_single_a(self):
         self._tl("single chain start")
         self._p_fwd_single()
+
+    def _chain_single_b(self):
         self._tl("single pyramids")
         self._p_bwd_single()
 
