@@ -13,6 +13,8 @@
 //           deterministic fixed-order reduction over chunks.
 #include "tde_common.h"
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 #include <cstdlib>
 
 namespace {
@@ -910,7 +912,6 @@ __global__ void __launch_bounds__(256) head_rw_wgrad_kernel(const HeadArgs p, in
 // pixel).
 template <int KS>
 struct Rwk { static constexpr int SEG = 4 * KS; };
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int KS>
 __global__ void __launch_bounds__(256) head_rwk_wgrad_kernel(const HeadArgs p, int CQ, int segs, long threads,
