@@ -383,7 +383,7 @@ def conv_family(fam):
 # experiments, serial replays): a bench line is never taken with one set.  (The work-skipping switches exist only in
 # a -DTDE_TIMING_DIAG build of libtde.so; the shipped library ignores them, and bench refuses them anyway.)
 DIAG_ENV = ("TDE_SKIP_CONV_LE", "TDE_SKIP_CONV_GT", "TDE_SKIP_WHAT", "TDE_SKIP_WGRAD", "TDE_HWG_DIAG",
-            "TDE_DBG_PHASE", "TDE_C4_OV_SERIAL")
+            "TDE_DBG_PHASE")
 
 
 def env_knobs():

@@ -16,31 +16,12 @@ network called twice with shared variables (train_depth_then_cam_lr.py:130-136) 
 TF does.
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import ConvDesc, ptr
-
-
-def _env_nonneg(name, default):
-    """Non-negative integer tuning knob from the environment (missing / non-numeric / negative: default)."""
-    try:
-        v = int(os.environ.get(name, ""))
-    except ValueError:
-        return default
-    return v if v >= 0 else default
-
-
-def _env_pos(name, default):
-    """Positive integer tuning knob from the environment (missing / non-numeric / non-positive: default)."""
-    try:
-        v = int(os.environ.get(name, ""))
-    except ValueError:
-        return default
-    return v if v > 0 else default
 
 
 def same_pad(n, k, s):
@@ -330,19 +311,10 @@ class NetProgram:
         self._bn_sums = {}
         self._folded = None     # layer -> (weights with BN folded in, bias); see fold_bn()
         # filter-gradient overlap (enable_wgrad_overlap): side stream, its workspace per batch, dz ring
+        # (every conv layer but the first of forward sends its filter gradient to the side stream, each behind one event,
+        # and the heads' filter gradients join it; measured and removed in round 5: groups of 2-3 layers per wait,
+        # 2-3 tail layers inline, the deep layers inline, two side streams -- all equal or slower)
         self.wgrad_stream = None
-        self.wgrad_group = _env_pos("TDE_WGRAD_GROUP", 1)
-        # the last `wgrad_tail` conv layers of backward (the first of forward) keep their filter gradient on the
-        # compute stream (fused launch): the side stream's backlog at the end of backward is what the compute
-        # stream waits for
-        self.wgrad_tail = _env_pos("TDE_WGRAD_TAIL", 1)
-        # layers whose forward output has at most this many rows (N*OH*OW) keep the fused data + filter gradient
-        # launch on the compute stream: at the deep levels the data gradient alone leaves most CUs idle, so the
-        # filter-gradient blocks ride along, instead of queueing on the side stream behind the high-resolution
-        # layers' filter gradients (0: every layer but the tail goes to the side stream)
-        self.wgrad_inline_m = _env_nonneg("TDE_WGRAD_INLINE_M", 0)
-        # the heads' filter gradients join the side stream too (their data gradient stays on the compute stream)
-        self.head_wgrad_side = _env_nonneg("TDE_HEAD_WGRAD_SIDE", 1) > 0
         self._ws2 = {}
         self._dzl = {}
         self._wsplit = {}       # (N, conv math) -> pre-split weight images (_split_plan)
@@ -471,20 +443,15 @@ class NetProgram:
         the current stream and its filter gradient (tde_conv2d_bwd_filter / tde_deconv2d_bwd_filter) on a side
         stream, with its own workspace.  Every layer's BN backward writes its own dz buffer, so nothing on the
         data-gradient chain ever waits for a filter gradient (TF's Conv2DBackpropFilter has no consumer but
-        the optimizer): the side stream only waits for the compute stream, once per `wgrad_group` conv
-        layers (TDE_WGRAD_GROUP; each cross-stream edge of a captured graph costs the stream that waits
-        ~5 us), and under capture it is a parallel graph branch joined at the end of backward (and before
+        the optimizer): the side stream only waits for the compute stream, once per conv layer (one event),
+        and under capture it is a parallel graph branch joined at the end of backward (and before
         any gradient-exchange launch point: join_wgrad()).  The two GEMMs are the separate data- and
         filter-gradient calls (their own tile plans, not the fused launch's shared tile), so results equal
         serial=True -- the same calls in the same order on ONE stream -- bit for bit."""
         # dedicated HIP streams, one per role and program (torch.cuda.Stream() recycles a fixed pool: a pooled
         # side stream can alias a capture stream or another program's side stream, _lib.dedicated_stream)
         self.wgrad_stream = (SERIAL if serial else _lib.owned_stream(self, "wgrad0")) if on else None
-        # TDE_WGRAD_STREAMS > 1: the filter-gradient groups alternate over that many side streams (each with its
-        # own workspace), so independent filter gradients may run concurrently with each other
-        n = 1 if (serial or not on) else _env_pos("TDE_WGRAD_STREAMS", 1)
-        self.wgrad_streams = ([self.wgrad_stream] + [_lib.owned_stream(self, f"wgrad{j}") for j in range(1, n)]
-                              if on else [])
+        self.wgrad_streams = [self.wgrad_stream] if on else []
         self._wg_rr = 0
         return self
 
@@ -768,8 +735,7 @@ class NetProgram:
                 self.timer.tag = getattr(op, "layer", type(op).__name__)
             src_needs = need_input_grad or op.src.buf is not spec.input
             if isinstance(op, ConvBN):
-                use_side = (side is not None and conv_rank[i] >= self.wgrad_tail and
-                            N * op.dst.H * op.dst.W > self.wgrad_inline_m)
+                use_side = side is not None and conv_rank[i] >= 1   # (the first layer: no data gradient)
                 d = op.desc(N)
                 self._use_split(d, i, N)
                 # dz (the conv's output gradient) is the y view of a conv's descriptor, the x view of a deconv's
@@ -830,10 +796,8 @@ class NetProgram:
                             _lib.check(wg(ctypes_ref(d), a1, a2, ptr(gw), pacc, wsp, wsb2, _lib.stream_ptr()),
                                        layer + " wgrad")
                     self._wg_pending.append((wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
-                    ev = None
-                    if len(self._wg_pending) >= self.wgrad_group:
-                        ev = torch.cuda.Event()
-                        ev.record()
+                    ev = torch.cuda.Event()
+                    ev.record()
                     if src_needs:
                         acc = mark(op.src)
                         with self._span("conv_dgrad", fl, conv_bytes(op, N)):
@@ -844,8 +808,7 @@ class NetProgram:
                             else:
                                 _lib.check(lib.tde_conv2d_bwd_data(ctypes_ref(d), ptr(dz), ptr(w), run.vptr(op.src, True),
                                                                    acc, ptr(ws), wsb, st), op.layer + " bwd data")
-                    if ev is not None:
-                        self._flush_wgrad(ev)
+                    self._flush_wgrad(ev)
                 elif src_needs:
                     # data + filter gradient: one fused launch (tde_conv2d_bwd / tde_deconv2d_bwd)
                     acc = mark(op.src)
@@ -879,7 +842,7 @@ class NetProgram:
                 acc = mark(op.src) if src_needs else 0
                 hw, hgw, hgb = (ptr(self.P(f"{op.layer}/weights")), ptr(self.G(f"{op.layer}/weights")),
                                 ptr(self.G(f"{op.layer}/biases")))
-                if side is not None and self.head_wgrad_side:
+                if side is not None:
                     # the head's filter gradient joins the deferred group on the side stream (it reads x, y and
                     # dy, none of which the rest of backward rewrites); the data gradient stays on this stream
                     def head_wgrad_call(wsp, wsb2, d=d, x=run.vptr(op.src), y=run.vptr(op.dst),
@@ -888,17 +851,14 @@ class NetProgram:
                                                     op.scale, op.offset, wsp, wsb2, _lib.stream_ptr()),
                                    op.layer + " head wgrad")
                     self._wg_pending.append((head_wgrad_call, [f"{self.prefix}/{n}" for n, _, _ in op.params]))
-                    ev = None
-                    if len(self._wg_pending) >= self.wgrad_group:
-                        ev = torch.cuda.Event()
-                        ev.record()
+                    ev = torch.cuda.Event()
+                    ev.record()
                     if src_needs:
                         _lib.check(lib.tde_head_bwd(ctypes_ref(d), run.vptr(op.src), hw, run.vptr(op.dst),
                                                     run.vptr(op.dst, True), run.vptr(op.src, True), acc, None, None,
                                                     0, op.act, op.scale, op.offset, ptr(ws), wsb, st),
                                    op.layer + " head dgrad")
-                    if ev is not None:
-                        self._flush_wgrad(ev)
+                    self._flush_wgrad(ev)
                     names, self._wg_issued = self._wg_issued, []
                     if on_grads is not None and names:
                         on_grads(names)

@@ -21,10 +21,6 @@ W_CONFIG2 = dict(smooth=1.0, depth=1.0)     # train_depth_only.py:33-37
 # being recorded; under the default "global" mode that poll is an illegal call during capture and
 # aborts the process (hipErrorStreamCaptureUnsupported).
 CAPTURE_MODE = "thread_local"
-# config 4's per-scale pose and warp-loss calls as multi-call launches (TDE_LOSS_MULTI=0: one launch per call, A/B)
-LOSS_MULTI = os.environ.get("TDE_LOSS_MULTI", "1") != "0"
-# config 4 as two independent per-network chains with one join (TDE_C4_CHAINS=0: the two-join schedule, A/B)
-C4_CHAINS = os.environ.get("TDE_C4_CHAINS", "1") != "0"
 
 
 def _halves(a, b):
@@ -743,7 +739,7 @@ class DepthThenCamTrainer(Trainer):
         self.N, self.H, self.W = batch, H, W
         self.w = weights or W_CONFIG4
         self.twin = bool(twin)
-        self.ov_net = os.environ.get("TDE_C4_OV_NET", "pair")   # the network on the second stream (net overlap)
+        self.ov_net = "pair"   # the network on the second stream (net overlap); disp_net there measured 999 vs 1045
         self.BACKWARD_USES = 1 if self.twin else 2     # backward calls per chunk per step
         with variables.variable_scope("model_singledepth"):
             self.single = _api.get_program("depth_net", _netlib.disp_net_spec, H, W, 3, decay=0.99, scale=4.0,
@@ -830,22 +826,16 @@ class DepthThenCamTrainer(Trainer):
     # forked onto a captured side branch made capture_end crash in a long-lived process -- ROCm 7 graph
     # instantiation, not reproducible alone), and replay interleaves them with stream waits.
     def _pieces(self):
-        """The step as stream pieces: the overlapped network's calls (`ov_net`, default depth_net = "pair"; env
-        TDE_C4_OV_NET) on the second stream, issued before the other network's on the compute stream."""
-        fwd = {"pair": self._p_fwd_pair, "single": self._p_fwd_single}
-        bwd = {"pair": self._p_bwd_pair, "single": self._p_bwd_single}
-        o = self.ov_net if self.ov_net in fwd else "pair"
+        """The step as stream pieces: depth_net's chain (`ov_net` = "pair") on the second stream, issued before
+        disp_net's on the compute stream.  disp_net's outputs enter only its own loss terms (smoothness of both maps,
+        the depth L1 of the left; train_depth_then_cam_lr.py:211-355, oracle.losses.loss_depth_then_cam_lr), so each
+        network's forward -> loss -> backward -> Adam is an independent chain: ONE join at the end of the step, and
+        the depth_net-dependent loss runs beside disp_net's backward.  The second stream waits only for the inputs
+        (concat + image area pyramids).  (Round 3's two-join schedule, TDE_C4_CHAINS=0, was deleted in round 5.)"""
+        chain = {"pair": self._chain_pair, "single": self._chain_single}
+        o = self.ov_net if self.ov_net in chain else "pair"
         m = "single" if o == "pair" else "pair"
-        if C4_CHAINS:
-            # disp_net's outputs enter only its own loss terms (smoothness of both maps, the depth L1 of the left;
-            # train_depth_then_cam_lr.py:211-355, oracle.losses.loss_depth_then_cam_lr), so each network's
-            # forward -> loss -> backward -> Adam is an independent chain: ONE join at the end of the step instead
-            # of a join before the loss, and the depth_net-dependent loss runs beside disp_net's backward.  The
-            # second stream waits only for the inputs (concat + image area pyramids)
-            chain = {"pair": self._chain_pair, "single": self._chain_single}
-            return [("main", self._p_inputs), ("ov", chain[o]), ("main", chain[m]), ("join", None)]
-        return [("main", self._p_inputs), ("ov", fwd[o]), ("main", fwd[m]), ("join", None),
-                ("main", self._p_loss), ("ov", bwd[o]), ("main", bwd[m]), ("join", None)]
+        return [("main", self._p_inputs), ("ov", chain[o]), ("main", chain[m]), ("join", None)]
 
     def _chain_pair(self):
         self._chain_pair_a()
@@ -875,8 +865,7 @@ class DepthThenCamTrainer(Trainer):
     def _p_inputs(self):
         self._tl("inputs start")
         self._p_concat()
-        if C4_CHAINS:
-            self._area_pyramids()
+        self._area_pyramids()
         self._tl("inputs")
 
     def _p_concat(self):
@@ -919,19 +908,11 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._out["sl"] = self.single.forward(self.runs["sl"], self.img["l"])
             self._out["sr"] = self.single.forward(self.runs["sr"], self.img["r"])
-        if LOSS_MULTI:
-            from . import losses as Ls
-            # the loss terms that need only this network's outputs and the inputs run here, on this network's
-            # stream: disp_net's smoothness + depth-L1 pyramids (and, in the two-join schedule, the image area
-            # pyramids, before the join beside the other network's forward); the rest of the loss needs depth_net's
-            # outputs (_p_loss)
-            if not C4_CHAINS:
-                self._area_pyramids()
-            Ls.pyramid_multi([self._pyramid_map(k) for k in ("sr", "sl")])
-        elif C4_CHAINS:
-            from . import losses as Ls
-            for k in ("sr", "sl"):
-                Ls.pyramid(**self._pyramid_map(k))
+        from . import losses as Ls
+        # the loss terms that need only this network's outputs and the inputs run here, on this network's stream:
+        # disp_net's smoothness + depth-L1 pyramids in one launch; the rest of the loss needs depth_net's outputs
+        # (_p_loss)
+        Ls.pyramid_multi([self._pyramid_map(k) for k in ("sr", "sl")])
 
     def _area_pyramids(self):
         from . import losses as Ls
@@ -963,8 +944,7 @@ class DepthThenCamTrainer(Trainer):
         backward on that backward's stream -- depth_net's update overlaps disp_net's backward tail (and the
         other way round) instead of both updates waiting for the join.  The same update arithmetic."""
         gs = self.grad_sync
-        return ((gs is None or getattr(gs, "captured", False)) and self.adam_ov is None and self.dadam is None and
-                os.environ.get("TDE_C4_INLINE_ADAM", "1") != "0")
+        return (gs is None or getattr(gs, "captured", False)) and self.adam_ov is None and self.dadam is None
 
     def _p_bwd_pair(self):
         if self.twin:
@@ -1084,8 +1064,6 @@ class DepthThenCamTrainer(Trainer):
         if self.graphs is None or getattr(self, "ov_seq", None) is None:
             return super().step()
         cur, ov = torch.cuda.current_stream(), self.net_stream
-        if os.environ.get("TDE_C4_OV_SERIAL") == "1":
-            ov = cur        # diagnostic: the same piece graphs replayed one after another on one stream
         gs = self.grad_sync
         seg = gs is not None and hasattr(gs, "begin_step") and not getattr(gs, "captured", False)
         if seg:
@@ -1123,31 +1101,21 @@ class DepthThenCamTrainer(Trainer):
         # pose_final = reduce_mean(pose_pred, [1,2]) (nets_optflow_depth.py:183-186)
         pl, pr = out["pl"][4], out["pr"][4]
         hw = pl.shape[1] * pl.shape[2]
-        if LOSS_MULTI and _halves(pl, pr):
+        if _halves(pl, pr):
             _lib.check(lib.tde_spatial_mean_fwd(2 * B, hw, 6, ptr(pl), 6, ptr(self.pose2), st), "pose mean")
         else:
             for pp, d in ((pl, "lr"), (pr, "rl")):
                 _lib.check(lib.tde_spatial_mean_fwd(B, hw, 6, ptr(pp), 6, ptr(self.pose[d]), st), "pose mean")
-        if not LOSS_MULTI and not C4_CHAINS:
-            self._area_pyramids()
         jobs = [dict(K=self.Ks[s], T=self.T[d] if s == 0 else None, P=self.P[d][s], Kinv=self.Kinv[s],
                      vec=self.pose[d]) for s in range(4) for d in ("lr", "rl")]
-        if LOSS_MULTI:
-            Ls.pose_prep_multi(jobs)
-        else:
-            for j in jobs:
-                Ls.pose_prep(j["K"], T=j["T"], P=j["P"], Kinv=j["Kinv"], vec=j["vec"])
+        Ls.pose_prep_multi(jobs)
         S = self.SLOTS
         _lib.check(lib.tde_cam_loss(B, ptr(self.gt_cam), ptr(self.T["lr"]), ptr(self.T["rl"]), w["cam"],
                                     Ls.dptr(self.acc, S["cam"]), ptr(self.gT["lr"]), ptr(self.gT["rl"]), st), "cam")
         # smoothness of 1/disp on the 4 maps at every scale (:216-225) and, on the single left net, the depth L1
-        # to the area-downsampled label with replace_nonfinite (:227-232,241-243): one multi-scale launch per map,
-        # or (LOSS_MULTI) depth_net's two maps in one launch here, disp_net's two before the join (_p_fwd_single)
-        if LOSS_MULTI:
-            Ls.pyramid_multi([self._pyramid_map(k) for k in ("pl", "pr")])   # disjoint gradient buffers
-        else:
-            for k in ("pl", "pr") if C4_CHAINS else ("pl", "pr", "sr", "sl"):
-                Ls.pyramid(**self._pyramid_map(k))
+        # to the area-downsampled label with replace_nonfinite (:227-232,241-243): depth_net's two maps in one
+        # launch here, disp_net's two on its own chain (_p_fwd_single)
+        Ls.pyramid_multi([self._pyramid_map(k) for k in ("pl", "pr")])   # disjoint gradient buffers
         dirs = (("l", "r", "pl", "pr", "lr"), ("r", "l", "pr", "pl", "rl"))
         calls = {d: [dict(img_src=self.pyr[src][s], img_tgt=self.pyr[tgt][s], P=self.P[d][s], Kinv=self.Kinv[s],
                           disp=out[run][s], logits=out[run][5 + s], disp_other=out[oth][s], photo_w=w["data"],
@@ -1155,7 +1123,7 @@ class DepthThenCamTrainer(Trainer):
                           g_logits=self.d_out[run][5 + s], g_other=self.d_out[oth][s], g_P=self.gP[d][s],
                           det_ws=self.det_ws) for s in range(4)]
                  for tgt, src, run, oth, d in dirs}
-        if LOSS_MULTI and self.det_ws is None:
+        if self.det_ws is None:
             # one launch per direction over the 4 scales (a direction's calls write disjoint g_disp / g_logits;
             # the two directions of one scale do not: g_disp of one is g_other of the other)
             for d in ("lr", "rl"):
@@ -1166,22 +1134,12 @@ class DepthThenCamTrainer(Trainer):
                     Ls.warp_loss(self.acc, S["photo"], **calls[d][s])
         # pose gradients -> pose_pred (spatial mean backward)
         gl, gr = self.d_out["pl"][4], self.d_out["pr"][4]
-        if LOSS_MULTI:
-            # both directions' pose gradients and their spatial-mean backward into the pose maps: one launch
-            jobs = (_lib.PoseGradArgs * 2)()
-            for j, (d, g) in enumerate((("lr", gl), ("rl", gr))):
-                jobs[j] = _lib.PoseGradArgs(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
-                                            ptr(self.g_pose[d]), 0, ptr(g), hw, 6, 0)
-            _lib.check(lib.tde_pose_grad_spread(jobs, 2, st), "pose grad spread")
-            return
-        for d in ("lr", "rl"):
-            _lib.check(lib.tde_pose_grad(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
-                                         ptr(self.g_pose[d]), 0, st), "pose grad")
-        if LOSS_MULTI and _halves(gl, gr):
-            _lib.check(lib.tde_spatial_mean_bwd(2 * B, hw, 6, ptr(gl), 6, 0, ptr(self.g_pose2), st), "pose mean bwd")
-        else:
-            for gpp, d in ((gl, "lr"), (gr, "rl")):
-                _lib.check(lib.tde_spatial_mean_bwd(B, hw, 6, ptr(gpp), 6, 0, ptr(self.g_pose[d]), st), "pose mean bwd")
+        # both directions' pose gradients and their spatial-mean backward into the pose maps: one launch
+        jobs = (_lib.PoseGradArgs * 2)()
+        for j, (d, g) in enumerate((("lr", gl), ("rl", gr))):
+            jobs[j] = _lib.PoseGradArgs(B, 4, ptr(self.pose[d]), ptr(self.K), 36, ptr(self.gP[d]), ptr(self.gT[d]),
+                                        ptr(self.g_pose[d]), 0, ptr(g), hw, 6, 0)
+        _lib.check(lib.tde_pose_grad_spread(jobs, 2, st), "pose grad spread")
 
     def loss_parts(self):
         v = self.acc.cpu().tolist()
