@@ -490,8 +490,11 @@ int tde_cam_loss(int B, const float* gt_vec, const float* T_lr, const float* T_r
  * a flat parameter buffer.  `step` is a device counter (incremented on device by tde_adam_step_begin)
  * so a captured graph replays correctly.  lr_t = lr*sqrt(1-b2^t)/(1-b1^t). */
 int tde_adam_step_begin(float* step, void* stream);
+/* grad_scale multiplies the gradient as it is read (1: as stored; 1/world: the data-parallel mean of a summed
+ * gradient -- the captured exchange all-reduces with SUM, which RCCL skips at one rank, ABI 9). */
 int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* v,
-                    const float* step, float lr, float beta1, float beta2, float eps, void* stream);
+                    const float* step, float lr, float beta1, float beta2, float eps, float grad_scale,
+                    void* stream);
 
 /* ---------------------------------------------------------------- utilities */
 int tde_fill(size_t n, float* x, float value, void* stream);

@@ -943,7 +943,10 @@ def test_loss_l1(L, nonfinite, N, H, W):
     close(g, pr.grad, what="l1 grad")
 
 
-def test_adam_matches_tf_form(L):
+@pytest.mark.parametrize("gscale", [1.0, 0.125])
+def test_adam_matches_tf_form(L, gscale):
+    """TF Adam (epsilon-hat form); gscale = tde_adam_update's grad_scale (1/world for the captured exchange's summed
+    gradient): Adam of gscale * g."""
     lib = L.load()
     n = 1000
     p0, g1, g2 = rnd(n, seed=21), rnd(n, seed=22), rnd(n, seed=23)
@@ -954,8 +957,8 @@ def test_adam_matches_tf_form(L):
     for g in (g1, g2):
         L.check(lib.tde_adam_step_begin(L.ptr(step), L.stream_ptr()))
         L.check(lib.tde_adam_update(n, L.ptr(gp), L.ptr(dev(g)), L.ptr(gm), L.ptr(gv), L.ptr(step), 2e-4, 0.9, 0.999,
-                                    1e-8, L.stream_ptr()))
-        opt.step(pr, {"p": g})
+                                    1e-8, gscale, L.stream_ptr()))
+        opt.step(pr, {"p": g * gscale})
     close(gp - dev(p0), pr["p"] - p0, tol=1e-4, what="adam delta")
 
 

@@ -157,7 +157,7 @@ _SIGS = {
                                 P, c_int, c_int, P]),
     "tde_loss_l1": (c_int, [c_int, c_int, c_int, P, c_int, c_int, P, c_int, c_float, P, P, c_int, c_int, P]),
     "tde_adam_step_begin": (c_int, [P, P]),
-    "tde_adam_update": (c_int, [c_size_t, P, P, P, P, P, c_float, c_float, c_float, c_float, P]),
+    "tde_adam_update": (c_int, [c_size_t, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P]),
     "tde_fill": (c_int, [c_size_t, P, c_float, P]),
     "tde_scale": (c_int, [c_size_t, P, c_float, P]),
     "tde_zero_bytes": (c_int, [c_size_t, P, P]),

@@ -18,11 +18,11 @@ __global__ void __launch_bounds__(256) zero_bytes_kernel(unsigned char* p, size_
 
 __global__ void __launch_bounds__(256) adam_kernel(long n4, f4* __restrict__ p, const f4* __restrict__ g,
                                                    f4* __restrict__ m, f4* __restrict__ v, const float* step,
-                                                   float lr, float b1, float b2, float eps) {
+                                                   float lr, float b1, float b2, float eps, float gs) {
   const double t = (double)step[0];
   const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const f4 gi = g[i];
+    const f4 gi = g[i] * gs;   // gs == 1: exact, the gradient as stored
     f4 mi = m[i], vi = v[i], pi = p[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -116,14 +116,14 @@ int tde_adam_step_begin(float* step, void* stream) {
 }
 
 int tde_adam_update(size_t n, float* param, const float* grad, float* m, float* v, const float* step, float lr,
-                    float beta1, float beta2, float eps, void* stream) {
+                    float beta1, float beta2, float eps, float grad_scale, void* stream) {
   tde_clear_error();
   TDE_CHECK_ARG(n % 4 == 0 && param && grad && m && v && step);
   TDE_CHECK_ARG(tde_aligned16(param) && tde_aligned16(grad) && tde_aligned16(m) && tde_aligned16(v));
   const long n4 = (long)(n / 4);
   hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(n4)), dim3(256), 0, static_cast<hipStream_t>(stream), n4,
                      reinterpret_cast<f4*>(param), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(m),
-                     reinterpret_cast<f4*>(v), step, lr, beta1, beta2, eps);
+                     reinterpret_cast<f4*>(v), step, lr, beta1, beta2, eps, grad_scale);
   return tde_launch_status();
 }
 

@@ -19,8 +19,7 @@ bucket never reported and makes the compute stream wait for the comm stream befo
 Under hipGraph capture there are two modes:
   * mode "graph" (the default over RCCL, round 5): the all-reduces are CAPTURED.  A launch point forks the chunk's
     comm stream off the capture stream (an event; the filter-gradient / branch streams that wrote the bucket's
-    gradients are waited on the same way), the bucket's all-reduce (ReduceOp.AVG: no separate 1/world scale pass)
-    becomes a graph node on that branch, and `join(chunk)` at the end of the program's backward joins it back -- no
+    gradients are waited on the same way), the bucket's all-reduce (ReduceOp.SUM) becomes a graph node on that branch, and `join(chunk)` at the end of the program's backward joins it back -- no
     graph is cut, so each network's forward, loss, backward, exchange and Adam replay as the graph (piece) they are.
     Each chunk all-reduces on a communicator of its own (created in chunk order on every rank): with config 4's two
     networks on two streams, each communicator is used from one graph branch in a fixed order;
@@ -28,7 +27,12 @@ Under hipGraph capture there are two modes:
     in the middle of a backward stalls the other network's chain (its wait packets sit in FIFO hardware queues shared
     with it, GPU_MAX_HW_QUEUES = 4): 32 / 64 / 128 MB buckets 782 / 720 / 897 pairs/s, one bucket per
     network (256 MB) 1049-1055, against 1089-1093 without the exchange -- hence Trainer.enable_ddp's 256 MB default.
-    (Issuing the all-reduce on the reporting stream itself, no branch at all, measured 780-784: worse.);
+    (Issuing the all-reduce on the reporting stream itself, no branch at all, measured 780-784: worse.)
+    The 1/world of the mean is NOT a pass of its own: chunk.grad holds the replicas' SUM after the exchange and Adam
+    applies `grad_scale` (= 1/world, Trainer.enable_ddp) as it reads the gradient.  ReduceOp.AVG would fold the scale
+    into RCCL instead, but RCCL runs AVG as a pre-multiplied sum with an extra kernel per call -- at world 1 a
+    oneRankReduce copy pass, 52 calls x 219 us per config-4 step, measured 1048-1051 pairs/s against 1083-1087 with
+    SUM (profiles/r05/bench_ab_exchange_sum.md);
   * mode "segments" (rounds 2-4; gloo falls back to it): a launch point closes the current graph segment and replay
     runs segment, its buckets eagerly, next segment ... so RCCL stays outside the graphs.
 
@@ -132,6 +136,9 @@ class GradSync:
         if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
             raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
         self.captured = self.mode != "segments"
+        # what the optimizer multiplies the exchanged gradient by: graph mode leaves the replicas' SUM in chunk.grad
+        # (no scale pass on the comm branch), segments mode the mean
+        self.grad_scale = 1.0 / world if self.captured else 1.0
         # graph mode: per chunk a comm stream and a communicator of its own (same creation order on every rank)
         # pre_fork(chunk): issue whatever the chunk's program still holds back for its side streams (the deferred
         # filter-gradient calls) before a launch point records events on them
@@ -212,7 +219,7 @@ class GradSync:
                 _lib.check(lib.tde_scale(v.numel(), _lib.ptr(v), 1.0 / self.world, st), "grad scale")
 
     def launch_forked(self, buckets, chunk):
-        """Graph mode: all-reduce (average) `buckets` on the chunk's comm stream, forked from the current stream (and
+        """Graph mode: all-reduce (sum; Adam applies 1/world) `buckets` on the chunk's comm stream, forked from the current stream (and
         after the chunk's side streams' tails) by events -- capture-legal, so under capture the all-reduces are graph
         nodes of a branch that join(chunk) merges back; eagerly the same stream order."""
         import torch.distributed as dist
@@ -227,7 +234,7 @@ class GradSync:
             _lib.wait_stream(comm, sd)
         with torch.cuda.stream(comm):
             for b in buckets:
-                dist.all_reduce(b.view(), op=dist.ReduceOp.AVG, group=self.group_of[id(chunk)])
+                dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.group_of[id(chunk)])
         self.forked.add(id(chunk))
 
     def join(self, chunk):

@@ -51,6 +51,9 @@ class Adam:
     def __init__(self, chunk, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8):
         self.chunk, self.lr, self.b1, self.b2, self.eps = chunk, lr, beta1, beta2, eps
         self.t = torch.zeros(1, device="cuda", dtype=torch.float32)
+        # applied to the gradient as Adam reads it: 1/world when the captured exchange leaves the replicas' SUM in
+        # chunk.grad (ddp.GradSync graph mode)
+        self.grad_scale = 1.0
 
     def step(self):
         self.begin()
@@ -70,7 +73,7 @@ class Adam:
         def at(t):
             return ctypes.c_void_p(t.data_ptr() + 4 * lo)
         _lib.check(lib.tde_adam_update(hi - lo, at(c.flat), at(c.grad), at(c.adam_m), at(c.adam_v), ptr(self.t),
-                                       self.lr, self.b1, self.b2, self.eps, st), "adam")
+                                       self.lr, self.b1, self.b2, self.eps, self.grad_scale, st), "adam")
 
 
 class AdamOverlap:
@@ -453,6 +456,8 @@ class Trainer:
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
                                   pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams, mode=mode,
                                   pre_fork=self._flush_chunk_wgrad)
+        for o in (self.opt.opts if hasattr(self.opt, "opts") else [self.opt]):
+            o.grad_scale = self.grad_sync.grad_scale
         self._check_sync_bn_streams()
         return self.grad_sync
 
