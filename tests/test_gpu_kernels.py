@@ -246,10 +246,12 @@ def test_deconv2d_fwd_bwd(L, case, conv_tol):
     close(gdw, wr.grad, tol=tol, what="deconv wgrad")
 
 
+@pytest.mark.parametrize("k", [3, 5, 7])
 @pytest.mark.parametrize("acc", [0, 1])
-def test_deconv_pixel_shuffle_views(L, acc):
+def test_deconv_pixel_shuffle_views(L, acc, k):
     """The pixel-shuffle deconv forward (conv_igemm.hip MODE_PS: one GEMM over the four parity classes, taken for
-    3x3 stride-2 deconvs with >= TDE_DECONV_PS_MINM input pixels, default 8192) reading its input from a channel
+    k x k stride-2 deconvs, k = 3 / 5 / 7 -- a 2x2 / 3x3 / 4x4 tap window over the deconv input -- with >=
+    TDE_DECONV_PS_MINM input pixels, default 8192) reading its input from a channel
     view and writing (or accumulating) into a channel view of a wider concat buffer, the other channels untouched:
     against the fp64 conv2d_transpose (nets_optflow_depth.py:103-140 slim.conv2d_transpose, SAME)."""
     lib = L.load()
@@ -260,11 +262,12 @@ def test_deconv_pixel_shuffle_views(L, acc):
     H, W = 2 * h, 2 * w_
     icv, ico, ocv, oco = 40, 4, 48, 16
     x = rnd(N, h, w_, cin, seed=51)
-    wt = rnd(3, 3, cout, cin, seed=52) * 0.2
+    wt = rnd(k, k, cout, cin, seed=52) * 0.2
     xin = torch.zeros(N, h, w_, icv, dtype=torch.float64)
     xin[..., ico:ico + cin] = x
     out0 = rnd(N, H, W, ocv, seed=53)
-    d = conv_desc(L, N=N, H=H, W=W, C=cout, OH=h, OW=w_, K=cin, KH=3, KW=3, stride=2, pad_top=0, pad_left=0,
+    _, pt, _ = T.same_pad(H, k, 2)
+    d = conv_desc(L, N=N, H=H, W=W, C=cout, OH=h, OW=w_, K=cin, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pt,
                   w_cin=cout, x_cstride=ocv, x_coff=oco, y_cstride=icv, y_coff=ico)
     ws = ws_for(L, d, deconv=True)
     gout = dev(out0)
@@ -280,10 +283,11 @@ def test_deconv_pixel_shuffle_views(L, acc):
     assert torch.equal(got[..., oco + cout:], out0[..., oco + cout:].float().double())
 
 
+@pytest.mark.parametrize("k", [3, 5, 7])
 @pytest.mark.parametrize("acc", [0, 1])
-def test_conv_bwd_data_pixel_shuffle(L, acc):
-    """The data gradient of a 3x3 stride-2 SAME conv (even input size: pad_top = pad_left = 0) is the same virtual
-    DGRAD as a deconv forward, so tde_conv2d_bwd_data takes the pixel-shuffle GEMM too when the rule allows it
+def test_conv_bwd_data_pixel_shuffle(L, acc, k):
+    """The data gradient of a k x k stride-2 SAME conv (even input size) is the same virtual DGRAD as a deconv
+    forward, so tde_conv2d_bwd_data takes the pixel-shuffle GEMM too when the rule allows it
     (ADVICE r03): against the fp64 autograd data gradient of conv2d_same, written into / accumulated onto a channel
     view of a wider buffer (the split data/filter-gradient calls of enable_wgrad_overlap use this entry point)."""
     lib = L.load()
@@ -292,11 +296,12 @@ def test_conv_bwd_data_pixel_shuffle(L, acc):
     OH, OW = H // 2, W // 2
     xcv, xco = 24, 4
     x = rnd(N, H, W, cin, seed=61).requires_grad_(True)
-    wt = rnd(3, 3, cin, cout, seed=62) * 0.2
+    wt = rnd(k, k, cin, cout, seed=62) * 0.2
     gy = rnd(N, OH, OW, cout, seed=63)
     (T.conv2d_same(x, wt, 2) * gy).sum().backward()
     ref = x.grad.detach()
-    d = conv_desc(L, N=N, H=H, W=W, C=cin, OH=OH, OW=OW, K=cout, KH=3, KW=3, stride=2, pad_top=0, pad_left=0,
+    _, pt, _ = T.same_pad(H, k, 2)
+    d = conv_desc(L, N=N, H=H, W=W, C=cin, OH=OH, OW=OW, K=cout, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pt,
                   w_cin=cin, x_cstride=xcv, x_coff=xco, y_cstride=cout, y_coff=0)
     ws = ws_for(L, d)
     base = rnd(N, H, W, xcv, seed=64)
@@ -632,7 +637,17 @@ def test_conv_fused_bn_grouped(L, case):
     close(db3, dbeta, tol=1e-6, what="from-sums dbeta (groups added, not accumulated)")
 
 
-@pytest.mark.parametrize("case", CONV_CASES)
+PS_BWD_CASES = [
+    # tde_conv2d_bwd of stride-2 layers whose data gradient takes the pixel-shuffle GEMM (ps_ok: >= 8192 output
+    # pixels, >= 512 tiles, C % 16 == 0), the filter gradient its own launch: 3x3 / 5x5 / 7x7, offset view; cnv2-like
+    (8, 128, 128, 16, 16, 32, 3, 2, 24, 4),
+    (8, 128, 128, 16, 16, 32, 5, 2, 16, 0),
+    (8, 128, 128, 16, 16, 32, 7, 2, 20, 4),
+    (16, 128, 96, 32, 32, 64, 5, 2, 32, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES + PS_BWD_CASES)
 def test_conv2d_bwd_fused(L, case):
     """tde_conv2d_bwd: data + filter gradient in one fused launch == the separate reference gradients
     (dx accumulated into an offset view, dw accumulated onto a prior value)."""

@@ -9,12 +9,15 @@
 namespace tdeconv {
 
 constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
-// MODE_PS: the forward of a 3x3 stride-2 deconv (slim.conv2d_transpose, nets_optflow_depth.py:103-140) as ONE
-// pixel-shuffle GEMM instead of 4 parity-class DGRAD GEMMs: rows = input pixels (n, a, b), columns = the 2x2 output
-// block (py, px) x Cout, K = the 2x2 input neighbourhood (a - 1 + th, b - 1 + tw) x Cin -- a stride-1 2x2 forward
-// conv whose B operand is the deconv weight w[kh][kw][c][k] gathered at kh = 2 (1 - th) + py, kw = 2 (1 - tw) + px
-// (zero past the 3x3 kernel: 9 of the 16 taps x class pairs), and whose epilogue scatters column (py, px, c) to
-// output pixel (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes.
+// MODE_PS: the forward of a k x k stride-2 deconv (slim.conv2d_transpose, nets_optflow_depth.py:103-140; k = 3, 5, 7)
+// -- equally the data gradient of a k x k stride-2 conv -- as ONE pixel-shuffle GEMM instead of 4 parity-class DGRAD
+// GEMMs: rows = input pixels (n, a, b), columns = the 2x2 output block (py, px) x Cout, K = the T x T input
+// neighbourhood (a - PW + th, b - PW + tw) x Cin -- a stride-1 T x T forward conv (KH = KW = T, PT = PL = PW: the
+// union of the four classes' tap windows, T = 2 / 3 / 4 for k = 3 / 5 / 7) whose B operand is the deconv weight
+// w[kh][kw][c][k] gathered at kh = ps_kh0 + py - 2 th, kw = ps_kh0 + px - 2 tw (zero outside the k x k kernel: 9 of
+// 16, 25 of 36, 49 of 64 tap x class pairs), and whose epilogue scatters column (py, px, c) to output pixel
+// (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes, and the GEMM is 4 x Cout wide
+// where the class GEMMs are Cout wide (16 / 32 columns for the high-resolution layers).
 constexpr int MODE_PS = 3;
 
 struct ConvArgs {
@@ -36,8 +39,9 @@ struct ConvArgs {
   // fp16x3 (math 4) operand bounds |x| <= *bound of the x view, the y view and the weights (null: unscaled
   // x / y, fixed weight scale; split_math.h)
   const float* xmax; const float* ymax; const float* wmax;
-  // MODE_PS: deconv output channels / height / width, weight input channels (w[3][3][ps_C][ps_K])
-  int ps_C, ps_H, ps_W, ps_K;
+  // MODE_PS: deconv output channels / height / width, weight input channels (w[ps_KS][ps_KS][ps_C][ps_K]), kernel size
+  // and the kernel-row origin of the B gather (kh = ps_kh0 + py - 2 th)
+  int ps_C, ps_H, ps_W, ps_K, ps_KS, ps_kh0;
   FDiv fpsC;
   // ring tiles (conv_ring.hip): the pre-split fp16 hi / lo B-operand image [class][k-tile][column tile][2][BN][32]
   // (ring_wprep) and its k-tile / column-tile counts

@@ -279,7 +279,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, (long)p.N * p.H * p.W * p.xcs);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, (long)p.N * p.OH * p.OW * p.ycs);
   const __amdgpu_buffer_rsrc_t rw =
-      make_rsrc(p.w, MODE == MODE_PS ? 9L * p.ps_C * p.ps_K : (long)p.KH * p.KW * p.wcin * p.K);
+      make_rsrc(p.w, MODE == MODE_PS ? (long)p.ps_KS * p.ps_KS * p.ps_C * p.ps_K : (long)p.KH * p.KW * p.wcin * p.K);
 
   // per-slot row geometry (float offsets; `pb` = element offset of the row at tap/k origin)
   int a_pb[A_PER], a_i1[A_PER], a_i2[A_PER];
@@ -394,13 +394,14 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const bool ok = slot && kq < Kd && ci < p.wcin;
         rb[i][0] = bload(rw, ok ? 4 * (dg_wtap + ci * p.K) : OOB);
       } else if constexpr (MODE == MODE_PS) {
-        // column n = (py, px, c), k quad kq = (th, tw, kin..kin+3): w[2 (1 - th) + py][2 (1 - tw) + px][c][kin..]
+        // column n = (py, px, c), k quad kq = (th, tw, kin..kin+3): w[kh0 + py - 2 th][kh0 + px - 2 tw][c][kin..]
         const int n = n0 + (s >> 3);
         const int gq = fdiv(n, p.fpsC), c = n - gq * p.ps_C;
         const int tap = fdiv(kq, p.fC), kin = kq - tap * p.C;
-        const int kh = 2 - 2 * (tap >> 1) + (gq >> 1), kw = 2 - 2 * (tap & 1) + (gq & 1);
-        const bool ok = slot && n < Nn && kq < Kd && kh < 3 && kw < 3;
-        rb[i][0] = bload(rw, ok ? 4 * (((kh * 3 + kw) * p.ps_C + c) * p.ps_K + kin) : OOB);
+        const int th = fdiv(tap, p.fKW), tw = tap - th * p.KW;
+        const int kh = p.ps_kh0 + (gq >> 1) - 2 * th, kw = p.ps_kh0 + (gq & 1) - 2 * tw;
+        const bool ok = slot && n < Nn && kq < Kd && (unsigned)kh < (unsigned)p.ps_KS && (unsigned)kw < (unsigned)p.ps_KS;
+        rb[i][0] = bload(rw, ok ? 4 * (((kh * p.ps_KS + kw) * p.ps_C + c) * p.ps_K + kin) : OOB);
       } else {
         const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
         const bool ok = slot && n < Nn;
@@ -1246,7 +1247,8 @@ static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg
   }
   if (mode == MODE_PS) {
     int bm = 0, bn = 0;
-    if (!ps_ok(d, &bm, &bn)) return false;
+    // (the ring's B-image prep gathers the 3x3 form only: larger kernels take the register-staged PS tile)
+    if (d.KH != 3 || !ps_ok(d, &bm, &bn)) return false;
     const long M = (long)d.N * d.OH * d.OW;
     const int Nn = 4 * d.C;
     pl = Plan{};
@@ -1527,18 +1529,36 @@ static void launch_reduce2(const Plan& p1, const ConvArgs& a1, const Plan& p2, c
                      p2.rows, p2.cols, zl2);
 }
 
-// Pixel-shuffle path of the stride-2 3x3 virtual DGRAD (deconv forward; MODE_PS above).  TDE_DECONV_PS_MINM:
-// input pixels (N x OH x OW) from which it replaces the four parity-class GEMMs (0: never).  Split-K never runs
-// here (below that size the class GEMMs and their split-K remain).
+// Pixel-shuffle path of the stride-2 k x k virtual DGRAD (deconv forward, conv data gradient; MODE_PS above; k = 3,
+// 5, 7).  TDE_DECONV_PS_MINM: input pixels (N x OH x OW) from which it replaces the four parity-class GEMMs (0:
+// never).  Split-K never runs here (below that size the class GEMMs and their split-K remain).  The 5x5 / 7x7 forms
+// (round 5: exp_upcnv1 / exp_upcnv2 forwards, cnv2's data gradient; before, 16 / 32-column class GEMMs) moved config
+// 4 from 1077-1079 to 1092-1095 pairs/s (profiles/r05/ps_ab.md).
 static const long g_ps_minm = env_long("TDE_DECONV_PS_MINM", 8192);
 // ... and only with enough tiles to fill the chip (the class GEMMs have 4x the tiles and split K): >= 512 blocks of
 // 128 rows, else >= 512 of 64 rows (measured, batch 8, us: upcnv1 48.2 -> 35.5 with 768 blocks of 128 rows;
 // upcnv2 28.7 -> 29.7 with 192, upcnv3 32.8 -> 37.7 with 96, upcnv4 29.5 -> 57.3 with 24: r03x)
 static const long g_ps_minblocks = env_long("TDE_DECONV_PS_MINBLOCKS", 512);
+
+// The pixel-shuffle GEMM's tap window over the deconv input for a k x k kernel at pad pt: input row a - PW + th
+// (th < T) feeds output row 2a + py through kernel row kh = kh0 + py - 2 th, kh0 = pt + 2 PW -- the union over
+// py = 0, 1 of the rows a + (py + pt - kh) / 2 with kh = py + pt (mod 2), 0 <= kh < k.
+struct PsWindow { int T, PW, kh0; };
+static PsWindow ps_window(int k, int pt) {
+  int lo = 1 << 20, hi = -(1 << 20);
+  for (int py = 0; py < 2; ++py)
+    for (int kh = 0; kh < k; ++kh)
+      if (((py + pt - kh) & 1) == 0) {
+        const int di = (py + pt - kh) / 2;
+        lo = di < lo ? di : lo;
+        hi = di > hi ? di : hi;
+      }
+  return PsWindow{hi - lo + 1, -lo, pt - 2 * lo};
+}
 static bool ps_ok(const tde_conv_desc_t& d, int* bm, int* bn) {
-  if (!(g_ps_minm > 0 && g_conv_math == 4 && d.stride == 2 && d.KH == 3 && d.KW == 3 && d.pad_top == 0 &&
-        d.pad_left == 0 && d.H == 2 * d.OH && d.W == 2 * d.OW && d.w_cin == d.C && d.C % 16 == 0 && d.K % 4 == 0 &&
-        (long)d.N * d.OH * d.OW >= g_ps_minm))
+  if (!(g_ps_minm > 0 && g_conv_math == 4 && d.stride == 2 && d.KH == d.KW && (d.KH & 1) && d.KH <= 7 &&
+        d.pad_top == d.pad_left && d.pad_top >= 0 && d.pad_top < d.KH && d.H == 2 * d.OH && d.W == 2 * d.OW &&
+        d.w_cin == d.C && d.C % 16 == 0 && d.K % 4 == 0 && (long)d.N * d.OH * d.OW >= g_ps_minm))
     return false;
   const long M = (long)d.N * d.OH * d.OW;
   const int Nn = 4 * d.C, BN = Nn % 128 == 0 ? 128 : 64;
@@ -1555,15 +1575,17 @@ static bool ps_ok(const tde_conv_desc_t& d, int* bm, int* bn) {
 // a0.dx (view x of d, C channels).
 static ConvArgs ps_args(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate) {
   ConvArgs a{};
+  const PsWindow pw = ps_window(d->KH, d->pad_top);
   a.N = d->N; a.H = d->OH; a.W = d->OW; a.C = d->K; a.OH = d->OH; a.OW = d->OW; a.K = 4 * d->C;
-  a.KH = 2; a.KW = 2; a.S = 1; a.PT = 1; a.PL = 1; a.wcin = d->K;
+  a.KH = pw.T; a.KW = pw.T; a.S = 1; a.PT = pw.PW; a.PL = pw.PW; a.wcin = d->K;
   a.xcs = d->y_cstride; a.xco = d->y_coff; a.ycs = d->x_cstride; a.yco = d->x_coff;
-  a.fC = make_fdiv(d->K); a.fK = make_fdiv(4 * d->C); a.fKW = make_fdiv(2); a.fOW = make_fdiv(d->OW);
+  a.fC = make_fdiv(d->K); a.fK = make_fdiv(4 * d->C); a.fKW = make_fdiv(pw.T); a.fOW = make_fdiv(d->OW);
   a.fOHW = make_fdiv(d->OH * d->OW);
   a.xmax = a0.ymax; a.wmax = a0.wmax;
   a.x = a0.dy; a.w = a0.w; a.y = a0.dx; a.bias = a0.bias; a.relu = a0.relu;
-  a.ps_C = d->C; a.ps_H = d->H; a.ps_W = d->W; a.ps_K = d->K; a.fpsC = make_fdiv(d->C);
-  a.splits = 1; a.kt_per = tde_cdiv(4L * d->K, BK3); a.accumulate = accumulate;
+  a.ps_C = d->C; a.ps_H = d->H; a.ps_W = d->W; a.ps_K = d->K; a.ps_KS = d->KH; a.ps_kh0 = pw.kh0;
+  a.fpsC = make_fdiv(d->C);
+  a.splits = 1; a.kt_per = tde_cdiv((long)pw.T * pw.T * d->K, BK3); a.accumulate = accumulate;
   return a;
 }
 
@@ -1830,11 +1852,22 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     ring1 = true;
     m1 = MODE_PS;
   }
-  if (!ring1) p1 = make_plan(*d, MODE1);
+  // a stride-2 conv whose data gradient fits the pixel-shuffle GEMM (ps_ok: the high-resolution 3x3 / 5x5 / 7x7 layers)
+  // runs it off the ring too: one 4 x C-wide launch without split-K, then the filter gradient as its own launch
+  // (config 4, cnv2's 5x5: 1090 -> 1092-1095 pairs/s against the fused class-GEMM launch, profiles/r05/ps_ab.md)
+  int pbm = 0, pbn = 0;
+  const bool ps1 = !ring1 && MODE1 == MODE_DGRAD && ps_ok(*d, &pbm, &pbn);
+  if (ps1) {
+    p1 = Plan{};
+    p1.bm = pbm; p1.bn = pbn; p1.splits = 1; p1.gz = 1;
+    p1.gx = (int)tde_cdiv((long)d->N * d->OH * d->OW, pbm); p1.gy = 4 * d->C / pbn;
+  } else if (!ring1) {
+    p1 = make_plan(*d, MODE1);
+  }
   bool r2 = false;
   const Plan p2w = wgrad_plan(*d, r2);
   // fused data + filter gradient launch only when neither GEMM is on the ring tiles
-  const bool fuse = !ring1 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
+  const bool fuse = !ring1 && !ps1 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
   const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : p2w;
   const void* img = ring1 ? d->w_split[MODE1 == MODE_FWD ? 0 : 1] : nullptr;
   const size_t img_bytes = ring1 && img == nullptr ? rg1.image_bytes() : 0;
@@ -1861,6 +1894,10 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
       a1.img_nkt = rg1.nkt; a1.img_ncolt = rg1.ncolt;
       ring_launch(MODE1, p1.bm, p1.bn, dim3(p1.gx, p1.gy, p1.gz), a1, st);
     }
+    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
+  } else if (ps1) {
+    ConvArgs ap = ps_args(d, a1, acc1);
+    launch_ps(d, ap, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), nullptr, nullptr, nullptr, st);
     if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
   } else if (fuse) {
     launch_bwd2<MODE1>(p1, a1, p2, a2, st);
