@@ -44,6 +44,12 @@ SHAPES = [
     ("upcnv1_b16", 16, 192, 256, 16, 32, 3, 2),
     ("upcnv2_b16", 16, 96, 128, 32, 64, 3, 2),
     ("upcnv3_b16", 16, 48, 64, 64, 128, 3, 2),
+    # config 4's stride-2 layers at the twin batch (pixel-shuffle forms: deconv forward / conv dgrad, filter gradient)
+    ("cnv1p_b16", 16, 192, 256, 8, 32, 7, 2),
+    ("cnv2_b16", 16, 96, 128, 32, 64, 5, 2),
+    ("cnv3_b16", 16, 48, 64, 64, 128, 3, 2),
+    ("cnv4_b16", 16, 24, 32, 128, 256, 3, 2),
+    ("expup1_b16", 16, 192, 256, 16, 32, 7, 2),
 ]
 
 

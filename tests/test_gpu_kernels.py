@@ -680,7 +680,12 @@ def test_conv2d_bwd_fused(L, case):
     close(gdw, w0 + wr.grad, what="fused wgrad")
 
 
-@pytest.mark.parametrize("case", DECONV_CASES)
+# deconvs whose data gradient runs its FWD GEMM and whose filter gradient the pixel-shuffle form (MODE_PSW: >= 8192
+# input pixels): the upcnv1 / exp_upcnv2 / exp_upcnv1 kernel sizes
+PSW_DECONV_CASES = [(8, 32, 32, 32, 16, 3), (8, 32, 32, 64, 32, 5), (8, 32, 32, 32, 16, 7)]
+
+
+@pytest.mark.parametrize("case", DECONV_CASES + PSW_DECONV_CASES)
 def test_deconv2d_bwd_fused(L, case):
     N, h, w_, cin, cout, k = case
     lib = L.load()
@@ -702,6 +707,52 @@ def test_deconv2d_bwd_fused(L, case):
                                  L.ptr(gdw), 0, L.ptr(ws), ws.numel() * 4, st))
     close(gdx, xr.grad, what="fused deconv dgrad")
     close(gdw, wr.grad, what="fused deconv wgrad")
+
+
+@pytest.mark.parametrize("deconv", [False, True])
+@pytest.mark.parametrize("k", [3, 5, 7])
+def test_wgrad_pixel_shuffle(L, k, deconv):
+    """The filter gradient of a k x k stride-2 layer in the pixel-shuffle form (conv_igemm.hip MODE_PSW: rows (py, px,
+    c) of the input, columns (th, tw, k) of the T x T dy window, reduce scattering to dw[kh][kw][c][k]; taken from
+    TDE_PSW_MINM = 8192 dy pixels) through tde_conv2d_bwd_filter / tde_deconv2d_bwd_filter, reading channel views and
+    accumulating onto a prior dw: against the fp64 autograd gradient of conv2d_same / conv2d_transpose_same."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, h, cin, cout = 8, 32, 16, 32                  # 8 x 32 x 32 = 8192 dy pixels (conv) / input pixels (deconv)
+    H = 2 * h
+    _, pt, _ = T.same_pad(H, k, 2)
+    if not deconv:
+        xcv, xco, ycv, yco = 24, 4, 40, 8
+        x = rnd(N, H, H, cin, seed=71)
+        gy = rnd(N, h, h, cout, seed=72)
+        w = rnd(k, k, cin, cout, seed=73).requires_grad_(True)
+        (T.conv2d_same(x, w, 2) * gy).sum().backward()
+        xin = torch.zeros(N, H, H, xcv, dtype=torch.float64)
+        xin[..., xco:xco + cin] = x
+        gin = torch.zeros(N, h, h, ycv, dtype=torch.float64)
+        gin[..., yco:yco + cout] = gy
+        d = conv_desc(L, N=N, H=H, W=H, C=cin, OH=h, OW=h, K=cout, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pt,
+                      w_cin=cin, x_cstride=xcv, x_coff=xco, y_cstride=ycv, y_coff=yco)
+        ws = ws_for(L, d)
+        w0 = rnd(k, k, cin, cout, seed=74)
+        gdw = dev(w0)
+        L.check(lib.tde_conv2d_bwd_filter(ctypes.byref(d), L.ptr(dev(xin)), L.ptr(dev(gin)), L.ptr(gdw), 1, L.ptr(ws),
+                                          ws.numel() * 4, st))
+    else:
+        # deconv cin (input, h x h) -> cout (output, H x H): the virtual conv has C = cout, K = cin
+        xs = rnd(N, h, h, cout, seed=75)
+        gy = rnd(N, H, H, cin, seed=76)
+        w = rnd(k, k, cin, cout, seed=77).requires_grad_(True)
+        (T.conv2d_transpose_same(xs, w, 2) * gy).sum().backward()
+        d = conv_desc(L, N=N, H=H, W=H, C=cin, OH=h, OW=h, K=cout, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pt,
+                      w_cin=cin, x_cstride=cin, x_coff=0, y_cstride=cout, y_coff=0)
+        ws = ws_for(L, d, deconv=True)
+        w0 = rnd(k, k, cin, cout, seed=78)
+        gdw = dev(w0)
+        L.check(lib.tde_deconv2d_bwd_filter(ctypes.byref(d), L.ptr(dev(gy)), L.ptr(dev(xs)), L.ptr(gdw), 1,
+                                            L.ptr(ws), ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    close(gdw, w0 + w.grad, what=f"pixel-shuffle wgrad k{k} {'deconv' if deconv else 'conv'}")
 
 
 HEAD_CASES = [

@@ -19,6 +19,14 @@ constexpr int MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2;
 // (2a + py, 2b + px).  Each input pixel is staged once per tile for all four classes, and the GEMM is 4 x Cout wide
 // where the class GEMMs are Cout wide (16 / 32 columns for the high-resolution layers).
 constexpr int MODE_PS = 3;
+// MODE_PSW: the filter gradient of the same stride-2 layers in the pixel-shuffle form.  dw[kh][kw][c][k] =
+// sum_(n,a,b) x[n, 2a + py, 2b + px, c] dy[n, a - PW + th, b - PW + tw, k] with kh = kh0 + py - 2 th (the MODE_PS
+// relation read the other way): rows = (py, px, c) -- the WGRAD im2col gather of x with a 2x2 "kernel" at stride 2 --
+// columns = (th, tw, k) -- the T x T stride-1 window of dy over its own grid -- reduction over dy's pixels.  4 x C
+// rows and T^2 x K columns where the direct filter-gradient GEMM has k^2 x C rows and K columns (16 / 32 for the
+// high-resolution layers); every output goes through the split-K slab, whose reduce scatters (row, column) to
+// dw[kh][kw][c][k] and drops the (py, th) pairs outside the kernel.
+constexpr int MODE_PSW = 4;
 
 struct ConvArgs {
   int N, H, W, C, OH, OW, K, KH, KW, S, PT, PL, wcin;
@@ -43,6 +51,9 @@ struct ConvArgs {
   // and the kernel-row origin of the B gather (kh = ps_kh0 + py - 2 th)
   int ps_C, ps_H, ps_W, ps_K, ps_KS, ps_kh0;
   FDiv fpsC;
+  // MODE_PSW: the dy window (T x T from -PW) and its division
+  int ps_T, ps_PW;
+  FDiv fpsT;
   // ring tiles (conv_ring.hip): the pre-split fp16 hi / lo B-operand image [class][k-tile][column tile][2][BN][32]
   // (ring_wprep) and its k-tile / column-tile counts
   const unsigned short* wimg;
@@ -122,6 +133,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f4 (&acc)[BM / 
                                               const DgClass& g, float* red) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr bool FWDLIKE = (MODE == MODE_FWD || MODE == MODE_PS);
+  constexpr bool WGLIKE = (MODE == MODE_WGRAD || MODE == MODE_PSW);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int r16 = lane & 15, q = lane >> 4;
@@ -131,7 +143,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f4 (&acc)[BM / 
   // sum and sum of squares over the tile's rows (rows past M hold exact zeros: their operand rows loaded
   // as zero), lanes -> waves in a fixed order, one fp64 partial per row tile.  Workgroup-local: the
   // cross-tile reduction is the next kernel's (a launch costs what an in-kernel hand-off costs).
-  if constexpr (MODE != MODE_WGRAD) {
+  if constexpr (!WGLIKE) {
     if (p.bnp != nullptr) {
       float cs[TN], cq[TN];
 #pragma unroll
@@ -201,7 +213,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f4 (&acc)[BM / 
   // ---- epilogue (16x16 C/D map is dtype-independent on gfx950).  Row addresses first; when
   // accumulating into the destination, ALL old values are loaded before any store (a store may alias a
   // later load, so an interleaved read-modify-write would serialise one memory latency per element).
-  const bool direct = (p.splits == 1);
+  const bool direct = (p.splits == 1) && MODE != MODE_PSW;    // MODE_PSW: always the slab (its reduce scatters)
   float* base;
   if constexpr (FWDLIKE) base = direct ? p.y : p.ws;
   else if constexpr (MODE == MODE_DGRAD) base = direct ? p.dx : p.ws;
@@ -263,7 +275,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& p, f4 (&acc)[BM / 
           if (rowaddr[a][r] >= 0 && n < Nn) acc[a][b][r] += base[rowaddr[a][r] + coff[b]];
         }
   }
-  if constexpr (MODE != MODE_WGRAD) {
+  if constexpr (!WGLIKE) {
     if (direct && (p.bias || p.relu)) {
 #pragma unroll
       for (int b = 0; b < TN; ++b) {

@@ -225,7 +225,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
                                           typename ImgSel<MATH, BM>::T* smem) {
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
-  constexpr bool A_T = (MODE == MODE_WGRAD);   // A global vectors along rows -> register transpose
+  constexpr bool A_T = (MODE == MODE_WGRAD || MODE == MODE_PSW);   // A global vectors along rows -> register transpose
   constexpr bool B_T = (MODE != MODE_DGRAD && MODE != MODE_PS);   // B global vectors along rows (n) -> transpose
   constexpr bool FWDLIKE = (MODE == MODE_FWD || MODE == MODE_PS);  // A = the forward im2col gather of x
   using IA = typename ImgSel<MATH, BM>::type;
@@ -241,7 +241,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
   float sA = 1.f, sB = 1.f;
   if constexpr (MATH == 4) {
     sA = f16x3_scale(MODE == MODE_DGRAD ? p.ymax : p.xmax, 1.f);
-    sB = MODE == MODE_WGRAD ? f16x3_scale(p.ymax, 1.f) : f16x3_scale(p.wmax, F16X3_WSCALE);
+    sB = (MODE == MODE_WGRAD || MODE == MODE_PSW) ? f16x3_scale(p.ymax, 1.f) : f16x3_scale(p.wmax, F16X3_WSCALE);
   }
 
   int M, Nn, Kd;
@@ -258,7 +258,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
     M = p.N * p.OH * p.OW; Nn = p.K; Kd = p.KH * p.KW * p.C;
   } else {
     zsplit = bz;
-    M = p.KH * p.KW * p.C; Nn = p.K; Kd = p.N * p.OH * p.OW;
+    M = p.KH * p.KW * p.C; Nn = MODE == MODE_PSW ? p.ps_T * p.ps_T * p.K : p.K; Kd = p.N * p.OH * p.OW;
   }
   FDiv fntw{};
   if constexpr (MODE == MODE_DGRAD) fntw = make_fdiv(g.ntw);
@@ -402,6 +402,22 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
         const int kh = p.ps_kh0 + (gq >> 1) - 2 * th, kw = p.ps_kh0 + (gq & 1) - 2 * tw;
         const bool ok = slot && n < Nn && kq < Kd && (unsigned)kh < (unsigned)p.ps_KS && (unsigned)kw < (unsigned)p.ps_KS;
         rb[i][0] = bload(rw, ok ? 4 * (((kh * p.ps_KS + kw) * p.ps_C + c) * p.ps_K + kin) : OOB);
+      } else if constexpr (MODE == MODE_PSW) {
+        // columns n..n+3 = (th, tw, k..k+3): dy at (a - PW + th, b - PW + tw) of pixels pix0..pix0+3 = (img, a, b)
+        const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
+        const bool ok = slot && n < Nn;
+        const int tap = fdiv(n, p.fK), k = n - tap * p.K;
+        const int th = fdiv(tap, p.fpsT), tw = tap - th * p.ps_T;
+        int img = fdiv(pix0, p.fOHW);
+        const int r = pix0 - img * p.OH * p.OW;
+        int aa = fdiv(r, p.fOW), bb = r - aa * p.OW;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ia = aa + th - p.ps_PW, ib = bb + tw - p.ps_PW;
+          const bool okj = ok && pix0 + j < Kd && (unsigned)ia < (unsigned)p.OH && (unsigned)ib < (unsigned)p.OW;
+          rb[i][j] = bload(rdy, okj ? 4 * (((img * p.OH + ia) * p.OW + ib) * p.ycs + p.yco + k) : OOB);
+          if (++bb == p.OW) { bb = 0; if (++aa == p.OH) { aa = 0; ++img; } }
+        }
       } else {
         const int n = n0 + 4 * (s % (BN / 4)), pix0 = kbase + 4 * (s / (BN / 4));
         const bool ok = slot && n < Nn;
@@ -870,6 +886,15 @@ __device__ __forceinline__ void splitk_reduce_body(const ConvArgs& p, int rows, 
         dst = p.y + (long)row * p.ycs + p.yco + col;
       } else if constexpr (MODE == MODE_DGRAD) {
         dst = p.dx + (long)row * p.xcs + p.xco + col;
+      } else if constexpr (MODE == MODE_PSW) {
+        // row (py, px, c), columns col..col+3 = (th, tw, k..k+3) -> dw[kh0 + py - 2 th][kh0 + px - 2 tw][c][k..k+3]
+        const int gq = row / p.C, c = row - gq * p.C;
+        const int tap = col / p.K, k = col - tap * p.K;
+        const int th = tap / p.ps_T, tw = tap - th * p.ps_T;
+        const int kh = p.ps_kh0 + (gq >> 1) - 2 * th, kw = p.ps_kh0 + (gq & 1) - 2 * tw;
+        dst = ((unsigned)kh < (unsigned)p.ps_KS && (unsigned)kw < (unsigned)p.ps_KS)
+                  ? p.dw + ((long)(kh * p.ps_KS + kw) * p.wcin + c) * p.K + k
+                  : nullptr;
       } else {
         const int tap = row / p.C, c = row - tap * p.C;
         dst = c < p.wcin ? p.dw + (long)(tap * p.wcin + c) * p.K + col : nullptr;
@@ -896,7 +921,7 @@ __device__ __forceinline__ void splitk_reduce_body(const ConvArgs& p, int rows, 
     }
     if (zlane != 0 || i >= total4 || !dst) continue;
     if (p.accumulate) s += prev;
-    if constexpr (MODE != MODE_WGRAD) {
+    if constexpr (MODE != MODE_WGRAD && MODE != MODE_PSW) {
       if (p.bias || p.relu) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) s[j] = bias_act(s[j], p.bias, col + j, p.relu);
@@ -914,12 +939,12 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs p, in
 
 // Both split-K reductions of one layer's backward (data gradient in MODE1, filter gradient) in one launch: blocks
 // [0, nb1) reduce the first, the rest the second (per element the same sums as two launches).
-template <int MODE1>
+template <int MODE1, int MODE2 = MODE_WGRAD>
 __global__ void __launch_bounds__(256) splitk_reduce2_kernel(const ConvArgs p1, int rows1, int cols1, int zl1, int nb1,
                                                              const ConvArgs p2, int rows2, int cols2, int zl2) {
   __shared__ f4 tmp[256];
   if ((int)blockIdx.x < nb1) splitk_reduce_body<MODE1>(p1, rows1, cols1, zl1, blockIdx.x, nb1, tmp);
-  else splitk_reduce_body<MODE_WGRAD>(p2, rows2, cols2, zl2, blockIdx.x - nb1, gridDim.x - nb1, tmp);
+  else splitk_reduce_body<MODE2>(p2, rows2, cols2, zl2, blockIdx.x - nb1, gridDim.x - nb1, tmp);
 }
 
 // Split-K reduction for a conv followed by batch norm: z = sum_z ws[z] (same fixed order as
@@ -1205,6 +1230,8 @@ static size_t hwg_ws_bytes(const tde_conv_desc_t& d) {
 }
 
 static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr);
+static bool psw_ok(const tde_conv_desc_t& d);
+static Plan psw_plan(const tde_conv_desc_t& d);
 
 // ---- LDS-DMA ring tiles (conv_ring.hip) for the fp16x3 GEMMs that take neither the halo nor the skinny path, by
 // the role of the call (TDE_RING / tde_set_conv_ring: a mask of RING_FWD = the forward calls tde_conv2d_fwd* /
@@ -1341,8 +1368,8 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
     if (ring_plan(d, MODE_PS, pp, rp, RING_ALL)) pb += rp.image_bytes();
     if (pb > b) b = pb;
   }
-  HwgPlan wp;
   if (mode == MODE_WGRAD && hwg_ws_bytes(d) > b) b = hwg_ws_bytes(d);
+  if (mode == MODE_WGRAD && psw_ok(d) && psw_plan(d).ws_bytes > b) b = psw_plan(d).ws_bytes;
   return b;
 }
 
@@ -1515,17 +1542,24 @@ static void launch_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st) {
 }
 
 // The data- and filter-gradient reductions of a layer's backward: one launch when both GEMMs split K.
-template <int MODE1>
+// (MODE2 = MODE_PSW: the pixel-shuffle filter gradient, whose slab is reduced -- and scattered -- even at one split)
+template <int MODE1, int MODE2 = MODE_WGRAD>
 static void launch_reduce2(const Plan& p1, const ConvArgs& a1, const Plan& p2, const ConvArgs& a2, hipStream_t st) {
-  if (p1.splits <= 1 || p2.splits <= 1) {
+  if (p1.splits <= 1 || (p2.splits <= 1 && MODE2 != MODE_PSW)) {
     launch_reduce<MODE1>(p1, a1, st);
-    launch_reduce<MODE_WGRAD>(p2, a2, st);
+    if constexpr (MODE2 == MODE_PSW) {
+      int zl, blocks;
+      reduce_shape(p2, zl, blocks);
+      hipLaunchKernelGGL(splitk_reduce_kernel<MODE_PSW>, dim3(blocks), dim3(256), 0, st, a2, p2.rows, p2.cols, zl);
+    } else {
+      launch_reduce<MODE2>(p2, a2, st);
+    }
     return;
   }
   int zl1, b1, zl2, b2;
   reduce_shape(p1, zl1, b1);
   reduce_shape(p2, zl2, b2);
-  hipLaunchKernelGGL(splitk_reduce2_kernel<MODE1>, dim3(b1 + b2), dim3(256), 0, st, a1, p1.rows, p1.cols, zl1, b1, a2,
+  hipLaunchKernelGGL((splitk_reduce2_kernel<MODE1, MODE2>), dim3(b1 + b2), dim3(256), 0, st, a1, p1.rows, p1.cols, zl1, b1, a2,
                      p2.rows, p2.cols, zl2);
 }
 
@@ -1650,6 +1684,62 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   return tde_launch_status();
 }
 
+// Pixel-shuffle filter gradient (MODE_PSW) of a stride-2 k x k layer with the MODE_PS geometry (k = 3, 5, 7; no
+// ps_ok tile-count rule: the reduction over every dy pixel splits K) from TDE_PSW_MINM dy pixels (0: never), for
+// 16 input channels only: measured per layer at config 4's twin batch (scripts/conv_micro.py, profiles/r05/psw_micro.txt)
+// it wins for the 16-channel deconvs -- upcnv1 71.5 -> 58.6 us, exp_upcnv1 173 -> 137 us, whose direct GEMM is
+// k^2 x 16 rows by 32 columns -- and loses for 8 / 32 / 64 channels (cnv1 110 -> 138, upcnv3 35 -> 40 us).
+static const long g_psw_minm = env_long("TDE_PSW_MINM", 8192);
+static bool psw_ok(const tde_conv_desc_t& d) {
+  return g_psw_minm > 0 && g_conv_math == 4 && d.C == 16 && d.stride == 2 && d.KH == d.KW && (d.KH & 1) && d.KH <= 7 &&
+         d.pad_top == d.pad_left && d.pad_top < d.KH && d.H == 2 * d.OH && d.W == 2 * d.OW && d.w_cin == d.C &&
+         (long)d.N * d.OH * d.OW >= g_psw_minm;
+}
+// rows 4 C, columns T^2 K, K = dy pixels; 64-row tiles for 4 C <= 64, 64 / 128 columns by make_plan's cost rule,
+// split-K to make_plan's block target.  Every tile writes the slab (splits >= 1), the reduce scatters.
+static Plan psw_plan(const tde_conv_desc_t& d) {
+  const PsWindow pw = ps_window(d.KH, d.pad_top);
+  const long M = 4L * d.C, Nn = (long)pw.T * pw.T * d.K, Kd = (long)d.N * d.OH * d.OW;
+  Plan pl{};
+  pl.bm = M <= 64 ? 64 : 128;
+  pl.bn = (tde_cdiv(Nn, 64) * 88 < tde_cdiv(Nn, 128) * 152) ? 64 : 128;
+  const long tiles = tde_cdiv(M, pl.bm) * tde_cdiv(Nn, pl.bn);
+  const int nkt = tde_cdiv(Kd, BK3);
+  long splits = tiles < g_split_target ? (g_split_target + tiles - 1) / tiles : 1;
+  if (splits > nkt / g_split_minkt) splits = nkt / g_split_minkt;
+  if (splits < 1) splits = 1;
+  if (splits > 512) splits = 512;
+  while (splits > 1 && splits * M * Nn * 4 > g_split_slab) splits /= 2;
+  pl.kt_per = tde_cdiv(nkt, (int)splits);
+  pl.splits = tde_cdiv(nkt, pl.kt_per);
+  pl.gx = (int)tde_cdiv(M, pl.bm); pl.gy = (int)tde_cdiv(Nn, pl.bn); pl.gz = pl.splits;
+  pl.rows = (int)M; pl.cols = (int)Nn;
+  pl.slab_bytes = (size_t)pl.splits * M * Nn * sizeof(float);
+  pl.ws_bytes = pl.slab_bytes;
+  return pl;
+}
+// The PSW GEMM's arguments from the layer's filter-gradient arguments (x, dy, dw, accumulate of the virtual conv).
+static ConvArgs psw_args(const tde_conv_desc_t* d, const ConvArgs& a0, const Plan& pl) {
+  const PsWindow pw = ps_window(d->KH, d->pad_top);
+  ConvArgs a = a0;
+  a.KH = 2; a.KW = 2; a.S = 2; a.PT = 0; a.PL = 0; a.fKW = make_fdiv(2);
+  a.ps_T = pw.T; a.ps_PW = pw.PW; a.ps_KS = d->KH; a.ps_kh0 = pw.kh0; a.fpsT = make_fdiv(pw.T);
+  a.splits = pl.splits; a.kt_per = pl.kt_per; a.bnp = nullptr;
+  return a;
+}
+static void launch_psw(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  const dim3 grid(pl.gx, pl.gy, pl.gz);
+  if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PSW, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (pl.bm == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PSW, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else if (pl.bn == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PSW, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((igemmx_kernel<4, MODE_PSW, 64, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
+}
+static void launch_psw_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st) {
+  int zl, blocks;
+  reduce_shape(pl, zl, blocks);
+  hipLaunchKernelGGL(splitk_reduce_kernel<MODE_PSW>, dim3(blocks), dim3(256), 0, st, a, pl.rows, pl.cols, zl);
+}
+
 template <int MODE>
 static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
                size_t ws_bytes, void* stream, int role) {
@@ -1658,6 +1748,19 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   }
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  if (MODE == MODE_WGRAD && psw_ok(*d)) {
+    const Plan pl = psw_plan(*d);
+    if (pl.ws_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    a.ws = reinterpret_cast<float*>(tde_ws_body(ws));
+    a.accumulate = accumulate;
+    const ConvArgs ap = psw_args(d, a, pl);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    span_mark(0, st);
+    if (!skip) launch_psw(pl, ap, st);
+    if (!skipr) launch_psw_reduce(pl, ap, st);
+    span_mark(1, st);
+    return tde_launch_status();
+  }
   HwgPlan wp;
   if (MODE == MODE_WGRAD && hwg_plan(*d, wp, g_conv_math)) {
     // stride-1, narrow, high-resolution layer: halo-tiled filter gradient (halo_wgrad.hip)
@@ -1866,9 +1969,12 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   }
   bool r2 = false;
   const Plan p2w = wgrad_plan(*d, r2);
-  // fused data + filter gradient launch only when neither GEMM is on the ring tiles
-  const bool fuse = !ring1 && !ps1 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
-  const Plan p2 = fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : p2w;
+  // the filter gradient of a stride-2 layer in the pixel-shuffle form (MODE_PSW) where it applies
+  const bool psw2 = !r2 && !g_skip_wgrad && psw_ok(*d);
+  // fused data + filter gradient launch only when neither GEMM is on the ring tiles or a pixel-shuffle GEMM
+  const bool fuse = !ring1 && !ps1 && !psw2 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 &&
+                    !g_skip_wgrad;
+  const Plan p2 = psw2 ? psw_plan(*d) : (fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : p2w);
   const void* img = ring1 ? d->w_split[MODE1 == MODE_FWD ? 0 : 1] : nullptr;
   const size_t img_bytes = ring1 && img == nullptr ? rg1.image_bytes() : 0;
   if (p1.slab_bytes + p2.slab_bytes + img_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
@@ -1877,7 +1983,13 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
   a2.ws = reinterpret_cast<float*>(body + p1.slab_bytes);
   a2.splits = p2.splits; a2.kt_per = p2.kt_per; a2.accumulate = acc2; a2.bnp = nullptr;
+  const ConvArgs a2p = psw2 ? psw_args(d, a2, p2) : a2;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  auto wgrad = [&] {
+    if (g_skip_wgrad) return;
+    if (psw2) launch_psw(p2, a2p, st);
+    else launch_wgrad(p2, r2, a2, st);
+  };
   if (skip) {
   } else if (ring1) {
     if (img == nullptr) {
@@ -1894,19 +2006,20 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
       a1.img_nkt = rg1.nkt; a1.img_ncolt = rg1.ncolt;
       ring_launch(MODE1, p1.bm, p1.bn, dim3(p1.gx, p1.gy, p1.gz), a1, st);
     }
-    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
+    wgrad();
   } else if (ps1) {
     ConvArgs ap = ps_args(d, a1, acc1);
     launch_ps(d, ap, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), nullptr, nullptr, nullptr, st);
-    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
+    wgrad();
   } else if (fuse) {
     launch_bwd2<MODE1>(p1, a1, p2, a2, st);
   } else {
     launch_mode<MODE1>(p1, a1, st);
-    if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
+    wgrad();
   }
   if (!skipr) {
     if (g_skip_wgrad) launch_reduce<MODE1>(p1, a1, st);
+    else if (psw2) launch_reduce2<MODE1, MODE_PSW>(p1, a1, p2, a2p, st);
     else launch_reduce2<MODE1>(p1, a1, p2, a2, st);
   }
   return tde_launch_status();
@@ -1919,8 +2032,8 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   size_t b = fused > split ? fused : split;
   {
     // the ring data gradient: its slab + the filter gradient's + the B image (no pre-split weights)
-    Plan pr;
-    RingGeom rg;
+    Plan pr{};
+    RingGeom rg{};
     bool r2;
     const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
     if (ring_plan(d, mode1, pr, rg, RING_ALL) || (mode1 == MODE_DGRAD && ring_plan(d, MODE_PS, pr, rg, RING_ALL))) {
@@ -1928,6 +2041,12 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
       if (r > b) b = r;
     }
     if (p1.slab_bytes + w2 > b) b = p1.slab_bytes + w2;
+    if (psw_ok(d)) {
+      // the pixel-shuffle filter gradient beside any data gradient above
+      const size_t pw = psw_plan(d).slab_bytes;
+      const size_t r = std::max(p1.slab_bytes, pr.slab_bytes + rg.image_bytes()) + pw;
+      if (r > b) b = r;
+    }
   }
   if (mode1 == MODE_DGRAD) {
     const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
