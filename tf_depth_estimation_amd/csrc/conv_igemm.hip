@@ -1032,14 +1032,11 @@ static const long g_split_slab = tde_env_pos("TDE_SPLIT_SLAB_MB", 128) << 20;
 static const long g_force_bn = env_long("TDE_FORCE_BN", 0);
 static const long g_force_bm = env_long("TDE_FORCE_BM", 0);
 static const long g_force_splits = env_long("TDE_FORCE_SPLITS", 0);
-// column tile cap of the 64-row (deep-level) tiles: narrower tiles = more tiles = fewer K splits (tuning)
-static const long g_deep_bn = env_long("TDE_DEEP_BN", 0);
 
 static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to which FWD / DGRAD go skinny
 // FWD / DGRAD GEMMs with at most this many rows (and < 256 tiles) take 64-row tiles (more blocks); above it, and
 // for every WGRAD, 128 (half the weight re-reads of a weight-streaming deep layer per row tile)
 static const long g_bm64_maxm = env_long("TDE_BM64_MAXM", 4096);
-static const long g_wgrad_bm64 = env_long("TDE_WGRAD_BM64", 0);
 
 // fix_bm / fix_bn > 0: plan with that tile (the fused backward launch needs one tile for both GEMMs)
 static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fix_bn = 0) {
@@ -1085,17 +1082,11 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
   pl.bm = 128;
   long tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   // WGRAD reduces over every pixel (Kd ~ 1e5): parallelism comes from split-K, so keep the
-  // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.
-  // WGRAD of a low-resolution layer (few pixels to reduce over, so split-K cannot add blocks) with < 256 tiles:
-  // 64-row tiles double the blocks of an otherwise under-filled chip (TDE_WGRAD_BM64=0: always 128)
-  const bool wg_small = mode == MODE_WGRAD && g_wgrad_bm64 && tiles < 256 &&
-                        tde_cdiv(Kd, BK) < 2 * g_split_minkt;
-  if ((mode != MODE_WGRAD && tiles < 256 && M <= g_bm64_maxm) || wg_small || g_force_bm == 64 || fix_bm == 64) {
+  // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.  (64-row filter-gradient
+  // tiles for the low-resolution layers and a column cap on the 64-row tiles were measured no better and removed in
+  // round 5.)
+  if ((mode != MODE_WGRAD && tiles < 256 && M <= g_bm64_maxm) || g_force_bm == 64 || fix_bm == 64) {
     pl.bm = 64;
-    tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
-  }
-  if (g_deep_bn && pl.bm == 64 && !fix_bn && !g_force_bn && pl.bn > g_deep_bn) {
-    pl.bn = (int)g_deep_bn;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
   if (fix_bm == 128 && pl.bm != 128) {
