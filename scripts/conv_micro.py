@@ -50,6 +50,10 @@ SHAPES = [
     ("cnv3_b16", 16, 48, 64, 64, 128, 3, 2),
     ("cnv4_b16", 16, 24, 32, 128, 256, 3, 2),
     ("expup1_b16", 16, 192, 256, 16, 32, 7, 2),
+    # stride-1 64-output-channel layers at the twin batch (halo-tiled filter gradient candidates)
+    ("cnv2b_b16", 16, 48, 64, 64, 64, 5, 1),
+    ("icnv3_b16", 16, 48, 64, 132, 64, 3, 1),
+    ("icnv2_b16", 16, 96, 128, 68, 32, 3, 1),
 ]
 
 
