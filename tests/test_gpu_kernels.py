@@ -597,6 +597,16 @@ def test_conv_fused_bn_grouped(L, case):
     # the ReLU mask the GPU applied (y > 0): at millions of elements a pre-activation within rounding of zero flips
     # between the fp32 and fp64 evaluations, and dz is discontinuous there (dy vs 0)
     ym = (y[:, yco:yco + Kc] > 0).double().cpu()
+    # ... and that mask is the fp64 reference's wherever the pre-activation is not within rounding of zero (VERDICT
+    # r04: pin the mask itself): every flip at |BN(z)| <= 1e-4 (the conv's fp16x3 error after normalisation), at most
+    # 1e-5 of the elements
+    with torch.no_grad():
+        pre = torch.cat([(z64[g * Mg:(g + 1) * Mg] - z64[g * Mg:(g + 1) * Mg].mean(0)) /
+                         torch.sqrt(z64[g * Mg:(g + 1) * Mg].var(0, unbiased=False) + 1e-3) + beta.double().cpu()
+                         for g in range(G)])
+        flips = ym != (pre > 0).double()
+    assert flips.sum().item() <= max(1, 1e-5 * flips.numel()), f"{flips.sum().item()} ReLU mask flips"
+    assert flips.sum().item() == 0 or pre[flips].abs().max().item() <= 1e-4, "ReLU mask flip away from zero"
     outs = []
     for g in range(G):
         zg = zr_[g * Mg:(g + 1) * Mg]
