@@ -38,9 +38,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--math", default="fp16x3", choices=list(_lib.CONV_MATH))
     args = ap.parse_args()
     lib = _lib.load()
-    _lib.check(lib.tde_set_conv_math(3))
+    _lib.check(lib.tde_set_conv_math(_lib.CONV_MATH[args.math]))
     rows = []
     for net, H, W, B in [("disp_net", 224, 224, 1), ("disp_net", 192, 256, 8), ("disp_net", 192, 256, 64)]:
         for fold, graph in [(True, True), (False, True), (True, False)]:
@@ -55,7 +56,7 @@ def main():
                          "ms_per_call": round(s * 1e3, 4), "images_per_s": round(B / s, 1),
                          "conv_tflops": round(f / s / 1e12, 2)})
             print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
-    print(json.dumps({"metric": "disp_net inference (batch_prediction.py path)", "math": "bf16x6r",
+    print(json.dumps({"metric": "disp_net inference (batch_prediction.py path)", "math": args.math,
                       "data": "synthetic U(-0.5,0.5) images, Glorot weights", "rows": rows}))
 
 
