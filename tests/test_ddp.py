@@ -72,6 +72,18 @@ def test_bucket_launches_follow_backward_schedule():
     assert min(fired.values()) < len(sched) // 2
 
 
+def test_exchange_mode_and_grad_scale():
+    """Without RCCL the exchange runs in "segments" mode and leaves the MEAN in chunk.grad (grad_scale 1 for Adam);
+    "graph" mode (the bucket all-reduces captured as graph nodes) needs the nccl backend and is refused otherwise.
+    Graph mode all-reduces with SUM and hands Adam grad_scale = 1 / world (tde_adam_update's grad_scale; the RCCL
+    side is checked by tests/test_gpu_ddp.py)."""
+    _, chunk = _chunk()
+    gs = ddp.GradSync([chunk], 4, bucket_mb=1.0)
+    assert gs.mode == "segments" and not gs.captured and gs.grad_scale == 1.0
+    with pytest.raises(ValueError):
+        ddp.GradSync([chunk], 4, bucket_mb=1.0, mode="graph")
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
