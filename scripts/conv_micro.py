@@ -54,6 +54,10 @@ SHAPES = [
     ("cnv2b_b16", 16, 48, 64, 64, 64, 5, 1),
     ("icnv3_b16", 16, 48, 64, 132, 64, 3, 1),
     ("icnv2_b16", 16, 96, 128, 68, 32, 3, 1),
+    ("cnv3b_b16", 16, 24, 32, 128, 128, 3, 1),
+    ("cnv4b_b16", 16, 12, 16, 256, 256, 3, 1),
+    ("icnv4_b16", 16, 24, 32, 260, 128, 3, 1),
+    ("icnv5_b16", 16, 12, 16, 512, 256, 3, 1),
 ]
 
 
