@@ -93,3 +93,13 @@ def test_halo_images_are_role_independent(lib):
     s0 = sizes(lib, d)
     lib.tde_set_conv_ring(7)
     assert sizes(lib, d) == s0 and s0[0] > 0
+
+
+def test_large_kernel_pixel_shuffle_takes_no_ring_image(lib):
+    # a 5x5 / 7x7 stride-2 deconv large enough for the pixel-shuffle GEMM runs its register-staged form (the ring's
+    # B-image prep gathers the 3x3 form only): no split image for its forward, whatever the ring mask
+    for k in (5, 7):
+        d = conv_desc(16, 128, 96, 16, 32, k, 2)   # virtual conv of a 64x48 -> 128x96 deconv, 32 -> 16 channels
+        lib.tde_set_conv_ring(7)
+        s = sizes(lib, d, deconv=True)
+        assert s[1] == 0, (k, s)
