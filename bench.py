@@ -445,9 +445,11 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "on"],
                     help="gradient exchange: auto = with N > 1; on = also at N = 1 over a world-1 RCCL group (times the "
                          "multi-GPU code path on one GPU)")
-    ap.add_argument("--exchange-mode", default="graph", choices=["graph", "segments"],
-                    help="bucket all-reduces captured into the step's graphs (graph) or issued eagerly between graph "
-                         "segments cut at each bucket launch point (segments, rounds 2-4)")
+    ap.add_argument("--exchange-mode", default="segments", choices=["graph", "segments"],
+                    help="bucket all-reduces issued eagerly by the host between graph segments cut at each bucket "
+                         "launch point, in program order on one comm stream (segments, the default since round 6), or "
+                         "captured into the step's graphs on per-network comm branches (graph; refused with the net "
+                         "overlap at N > 1, see ddp.py)")
     args = ap.parse_args()
     knobs = env_knobs()
 
@@ -527,7 +529,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        # captured graphs of the step and the cuts the exchange forces between them (graph mode: the
                        # bucket all-reduces are graph nodes, so 0; segments mode: one cut per bucket launch point)
-                       "graph_segment_cuts": (len(getattr(tr, "segments", None) or [1]) - 1) if use_graph else None,
+                       "graph_segment_cuts": tr.segment_cuts() if use_graph else None,
                        "grad_exchange": (None if world == 1 and args.exchange != "on" else
                                          f"{args.ddp}, {args.bucket_mb} MB buckets, {args.exchange_mode}"),
                        "batch_norm": "sync (global batch)" if args.sync_bn else "per-replica batch",

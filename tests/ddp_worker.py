@@ -20,6 +20,11 @@ ParamChunk, and asserts on every rank; a non-zero exit fails the test.
                 and its fp64 autograd) on the concatenated batch, the reference's one-device semantics
                 (train_depth_then_cam_lr.py:130-136).  The kernels themselves run on the GPU in
                 tests/test_gpu_ddp_world2.py (c2_syncbn).
+  order       : the issue order of a step's collectives is the program order on every rank, whatever the timing
+                (VERDICT r05 item 2): config 4's two chunks in one GradSync (the default segments mode), each rank
+                sleeping a different random time before each report and inside each collective; every rank records
+                the bucket order it issued, the orders are gathered and must be identical, and the exchanged
+                gradients are the exact mean (a mismatched order would pair different buckets).
   oracle_step : one data-parallel config-2 step: each rank takes its shard of the global batch,
                 computes the oracle gradient, writes it op by op with hooks; after the exchange and
                 the oracle Adam, parameters are bit-identical across ranks and equal to Adam applied
@@ -150,6 +155,47 @@ def case_two_programs(rank, world):
     assert torch.all(chunk_s.grad == n) and torch.all(chunk_p.grad == 10 * n)
 
 
+def case_order(rank, world):
+    import random
+    import time
+    spec_s, chunk_s = build()
+    spec_p = _netlib.depth_net_spec(128, 128, 6, levels=4)
+    specs, bn = spec_p.param_specs()
+    pre_p = "model/depth_cam_net"
+    chunk_p = ParamChunk([(f"{pre_p}/{n}", s, i) for n, s, i in specs], [(f"{pre_p}/{n}", c) for n, c in bn],
+                         device="cpu", seed=2)
+    gs = ddp.GradSync([chunk_s, chunk_p], world, bucket_mb=2.0)
+    assert gs.mode == "segments"
+    rnd = random.Random(1000 + rank)
+    issued = []
+    real = gs.launch
+
+    def delayed_launch(buckets, streams=()):
+        time.sleep(rnd.uniform(0, 0.004) * (rank + 1))
+        issued.extend((b.chunk is chunk_p, b.lo, b.hi) for b in buckets)
+        real(buckets, streams)
+    gs.launch = delayed_launch
+    for step in range(2):
+        gs.begin_step()
+        chunk_s.grad.fill_(float(rank + 1 + step))
+        chunk_p.grad.fill_(float(10 * (rank + 1) + step))
+        # the replay order of config 4's pieces: depth_net's chain (second stream) is issued before disp_net's
+        for ch, sched in ((chunk_p, [[f"{pre_p}/{n}" for n, _, _ in op.params] for op in reversed(spec_p.ops)
+                                      if op.params]),
+                          (chunk_s, schedule(spec_s))):
+            hook = gs.hook(ch)
+            for names in sched:
+                time.sleep(rnd.uniform(0, 0.0005))
+                hook(names)
+        gs.finish()
+        n = sum(range(1, world + 1)) / world
+        assert torch.all(chunk_s.grad == n + step) and torch.all(chunk_p.grad == 10 * n + step)
+    orders = [None] * world
+    dist.all_gather_object(orders, issued)
+    assert len(issued) == 2 * len(gs.buckets)
+    assert all(o == orders[0] for o in orders), "ranks issued their collectives in different orders"
+
+
 def case_syncbn(rank, world):
     from oracle import tf_ops as T
     N, Hh, Ww, C = 3, 5, 7, 12           # per-rank shard: 105 rows x 12 channels
@@ -250,7 +296,8 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     try:
         {"mean": case_mean, "uses2": case_uses2, "two_programs": case_two_programs,
-         "oracle_step": case_oracle_step, "syncbn": case_syncbn}[case](rank, world)
+         "oracle_step": case_oracle_step, "syncbn": case_syncbn,
+         "order": case_order}[case](rank, world)
         dist.barrier()
     finally:
         dist.destroy_process_group()

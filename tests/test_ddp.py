@@ -73,7 +73,7 @@ def test_bucket_launches_follow_backward_schedule():
 
 
 def test_exchange_mode_and_grad_scale():
-    """Without RCCL the exchange runs in "segments" mode and leaves the MEAN in chunk.grad (grad_scale 1 for Adam);
+    """The default exchange is "segments" (round 6) and leaves the MEAN in chunk.grad (grad_scale 1 for Adam);
     "graph" mode (the bucket all-reduces captured as graph nodes) needs the nccl backend and is refused otherwise.
     Graph mode all-reduces with SUM and hands Adam grad_scale = 1 / world (tde_adam_update's grad_scale; the RCCL
     side is checked by tests/test_gpu_ddp.py)."""
@@ -84,13 +84,136 @@ def test_exchange_mode_and_grad_scale():
         ddp.GradSync([chunk], 4, bucket_mb=1.0, mode="graph")
 
 
+class _Stream:
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return self.name
+
+
+class _TopologySync(ddp.GradSync):
+    """GradSync in graph mode with its stream / collective primitives recorded instead of run: the fork/join topology
+    a captured step would build, on CPU."""
+    cur = None
+    ops = None
+
+    def _rccl(self, group):
+        return True
+
+    def _new_stream(self):
+        return _Stream(f"comm{len(self.ops) if self.ops is not None else 0}_{id(self) % 997}")
+
+    @staticmethod
+    def _chunk_group(i):
+        return f"group{i}"
+
+    def _current(self):
+        return _TopologySync.cur
+
+    def _on(self, stream):
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            prev, _TopologySync.cur = _TopologySync.cur, stream
+            try:
+                yield
+            finally:
+                _TopologySync.cur = prev
+        return ctx()
+
+    def _wait(self, waiter, waitee):
+        _TopologySync.ops.append(("wait", waiter, waitee))
+
+    def _all_reduce(self, view, group):
+        _TopologySync.ops.append(("allreduce", _TopologySync.cur, group))
+
+
+@pytest.mark.parametrize("mb", [1.0, 256.0])
+def test_graph_mode_forks_one_level_deep(mb):
+    """the graph-mode exchange's fork/join topology under a (recorded) capture.  The capture
+    stream `cap` has one side branch, the program's filter-gradient stream `wgrad` (forked by the program, joined by
+    pre_launch = Trainer._join_chunk_wgrad).  Every comm branch must fork from the capture stream ALONE, after the
+    filter-gradient branch was joined into it: no stream forks from a branch, and the comm stream never waits on the
+    filter-gradient stream.  Every comm branch is joined back before the step ends, its all-reduces run on it."""
+    import ddp_worker
+    spec, chunk = _chunk()
+    cap, wgrad = _Stream("cap"), _Stream("wgrad")
+    _TopologySync.ops, _TopologySync.cur = [], cap
+
+    def join_wgrad(c):
+        _TopologySync.ops.append(("wait", _TopologySync.cur, wgrad))
+
+    def wgrad_fork():
+        _TopologySync.ops.append(("wait", wgrad, cap))
+    gs = _TopologySync([chunk], 2, bucket_mb=mb, mode="graph", pre_launch=join_wgrad,
+                       side_streams=lambda c: (wgrad,), pre_fork=lambda c: None)
+    assert gs.captured and gs.grad_scale == 0.5
+    comm = gs.comm_of[id(chunk)]
+    gs.begin_step()
+    hook = gs.hook(chunk)
+    for names in ddp_worker.schedule(spec):
+        wgrad_fork()                      # the program forks its filter-gradient branch once per layer
+        hook(names)
+    join_wgrad(chunk)                     # the backward's own final join
+    gs.join(chunk)
+    ops = _TopologySync.ops
+    # branches: a stream is a branch of `cap` once it waited on cap; a fork from a branch would be a wait whose
+    # waitee is neither the capture stream nor the waiter's own parent joining back
+    for kind, a, b in ops:
+        if kind != "wait":
+            continue
+        if a is comm:
+            assert b is cap, f"comm branch waits on {b!r}: a fork of a fork"
+        if b is comm:
+            assert a is cap, "comm branch joined into a side branch"
+    waits_comm = [i for i, (k, a, b) in enumerate(ops) if k == "wait" and a is comm]
+    assert waits_comm, "no bucket was forked"
+    for i in waits_comm:                  # the filter-gradient branch was joined right before each fork
+        assert ops[i - 1] == ("wait", cap, wgrad), ops[i - 1:i + 1]
+    reduces = [(a, g) for k, a, g in ops if k == "allreduce"]
+    assert len(reduces) == len(gs.buckets) and all(a is comm and g == "group0" for a, g in reduces)
+    assert ops[-1] == ("wait", cap, comm), "the comm branch is not joined back at the end"
+    assert all(b.launched for b in gs.buckets)
+
+
+def test_graph_mode_refuses_shared_group_over_chunks():
+    """an explicit communicator under several chunks' comm branches is refused in graph mode."""
+    _, c1 = _chunk()
+    _, c2 = _chunk()
+    _TopologySync.ops = []
+    with pytest.raises(ValueError):
+        _TopologySync([c1, c2], 2, bucket_mb=1.0, mode="graph", group="explicit")
+    gs = _TopologySync([c1, c2], 2, bucket_mb=1.0, mode="graph")
+    assert gs.group_of[id(c1)] != gs.group_of[id(c2)]
+
+
+def test_adam_reads_grad_scale_from_the_exchange():
+    """every Adam behind a trainer's optimizer (MultiAdam's sub-optimizers included) reads the exchange's
+    gradient convention at update time: 1/world while graph mode leaves the SUM in chunk.grad, 1 when unlinked."""
+    from tf_depth_estimation_amd import train
+    _, c1 = _chunk()
+    _, c2 = _chunk()
+    opt = train.MultiAdam([c1, c2])
+    assert all(o.grad_scale == 1.0 for o in opt.opts)
+    _TopologySync.ops = []
+    gs = _TopologySync([c1, c2], 4, bucket_mb=1.0, mode="graph")
+    train.link_grad_scale(opt, gs)
+    assert all(o.grad_scale == 0.25 for o in opt.opts)
+    gs.grad_scale = 0.125                 # read at call time, not copied at link time
+    assert all(o.grad_scale == 0.125 for o in opt.opts)
+    train.link_grad_scale(opt, None)
+    assert all(o.grad_scale == 1.0 for o in opt.opts)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("case", ["mean", "uses2", "two_programs", "oracle_step", "syncbn"])
+@pytest.mark.parametrize("case", ["mean", "uses2", "two_programs", "oracle_step", "syncbn", "order"])
 def test_gloo_world2(case):
     env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

@@ -2,7 +2,11 @@
 real path -- backward hooks, bucket all-reduce on the comm stream, segmented hipGraph capture and
 replay -- and must leave parameters bit-identical to the single-graph trainer (all-reduce over one
 rank is the identity and the scale is 1.0).  The multi-rank mean itself is covered on CPU with gloo
-(tests/test_ddp.py)."""
+(tests/test_ddp.py).
+
+These tests carry the `rccl` marker: tests/conftest.py runs them after every other GPU test, so the process-wide RCCL
+state they create (communicators, ProcessGroupNCCL's watchdog thread, RCCL's proxy threads) exists only at the end of
+the suite."""
 import os
 import socket
 
@@ -11,7 +15,7 @@ import pytest
 import torch
 
 # an empty captured segment is dropped, not replayed (train._end_segment): the warning must not surface
-pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("error:The CUDA Graph is empty")]
+pytestmark = [pytest.mark.gpu, pytest.mark.rccl, pytest.mark.filterwarnings("error:The CUDA Graph is empty")]
 
 
 @pytest.fixture(scope="module")
@@ -115,7 +119,7 @@ def test_sync_bn_world1_step_parity(pg):
     _api.clear_programs()
 
 
-def _c4_trainer(ddp, graph, net_overlap, steps=2, mode="graph"):
+def _c4_trainer(ddp, graph, net_overlap, steps=2, mode="graph", bucket_mb=4.0):
     from test_gpu_trainers import intrinsics, small_pose, texture
     from tf_depth_estimation_amd import _api, train, variables
     variables.get_store().reset(seed=1)
@@ -127,8 +131,8 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, mode="graph"):
                  torch.tensor(lab, dtype=torch.float32).cuda(), intrinsics(B, H, W).cuda(), small_pose(B, 4).cuda())
     tr.enable_wgrad_overlap()
     if ddp:
-        gs = tr.enable_ddp(1, bucket_mb=4.0, mode=mode)
-        assert len(gs.buckets) > 4
+        gs = tr.enable_ddp(1, bucket_mb=bucket_mb, mode=mode)
+        assert len(gs.buckets) > (4 if bucket_mb <= 4.0 else 1)
     if net_overlap:
         tr.enable_net_overlap()
     if graph:
@@ -143,18 +147,39 @@ def _c4_trainer(ddp, graph, net_overlap, steps=2, mode="graph"):
 
 
 @MODES
+@pytest.mark.parametrize("bucket_mb", [4.0, 256.0], ids=["b4", "b256"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_config4_exchange_with_net_overlap(pg, graph, mode):
+def test_config4_exchange_with_net_overlap(pg, graph, bucket_mb, mode):
     """Config 4 (twin-batched programs, filter gradients on their side streams, depth_net on the second stream)
     under the bucketed exchange (world-1 RCCL group): each program's bucket launch points cut its own piece's
-    graphs (only that program's filter-gradient branch is joined), the comm stream waits on events -- the
-    parameters, gradients and moments equal the same step without an exchange bit for bit (deterministic
-    warp-loss mode; world 1: the all-reduce is the identity)."""
+    graphs (segments) or fork its comm branch one level deep (graph; only that program's filter-gradient branch is
+    joined first) -- the parameters, gradients and moments equal the same step without an exchange bit for bit
+    (deterministic warp-loss mode; world 1: the all-reduce is the identity).  b256 = the benched default, one
+    bucket per network; b4 = many mid-backward launch points."""
     ref = _c4_trainer(False, graph, True)
-    for a, b in zip(ref, _c4_trainer(True, graph, True, mode=mode)):
+    for a, b in zip(ref, _c4_trainer(True, graph, True, mode=mode, bucket_mb=bucket_mb)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
-    for a, b in zip(ref, _c4_trainer(True, graph, False, mode=mode)):
+    for a, b in zip(ref, _c4_trainer(True, graph, False, mode=mode, bucket_mb=bucket_mb)):
         assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+def test_graph_exchange_refused_with_net_overlap_beyond_world1(pg):
+    """with the net overlap the two networks' captured exchanges would run two communicators from two
+    concurrently replayed graphs; at world > 1 that order is not fixed, so it is refused (segments mode, the default,
+    is accepted).  Only the schedule check runs here (no collective is issued at world 2 on a world-1 group)."""
+    from tf_depth_estimation_amd import _api, train, variables
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    tr = train.DepthThenCamTrainer(1, 64, 96)
+    gs = tr.enable_ddp(2, mode="graph")
+    assert gs.grad_scale == 0.5 and all(o.grad_scale == 0.5 for o in tr.opt.opts)
+    with pytest.raises(ValueError):
+        tr.enable_net_overlap()
+    tr2 = train.DepthThenCamTrainer(1, 64, 96)
+    gs2 = tr2.enable_ddp(2)
+    assert gs2.mode == "segments" and all(o.grad_scale == 1.0 for o in tr2.opt.opts)
+    tr2.enable_net_overlap()
+    _api.clear_programs()
 
 
 def _c4_syncbn(pg, graph, sync=True, steps=3, overlaps=None):

@@ -267,6 +267,11 @@ class capture_scope:
             _GC_WAS_ON[0] = gc.isenabled()
             gc.collect()
             gc.disable()
+            # graphs the collection destroyed (an older trainer's, possibly holding captured RCCL work whose
+            # resources RCCL releases through graph user objects) are torn down with the device idle, before the
+            # next capture begins
+            if torch.cuda.is_initialized():
+                torch.cuda.synchronize()
         _CAPTURE_DEPTH[0] += 1
         return self
 

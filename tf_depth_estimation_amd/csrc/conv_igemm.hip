@@ -1683,8 +1683,8 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
 static const long g_psw_minm = env_long("TDE_PSW_MINM", 8192);
 static bool psw_ok(const tde_conv_desc_t& d) {
   return g_psw_minm > 0 && g_conv_math == 4 && d.C == 16 && d.stride == 2 && d.KH == d.KW && (d.KH & 1) && d.KH <= 7 &&
-         d.pad_top == d.pad_left && d.pad_top < d.KH && d.H == 2 * d.OH && d.W == 2 * d.OW && d.w_cin == d.C &&
-         (long)d.N * d.OH * d.OW >= g_psw_minm;
+         d.pad_top == d.pad_left && d.pad_top >= 0 && d.pad_top < d.KH && d.H == 2 * d.OH && d.W == 2 * d.OW &&
+         d.w_cin == d.C && (long)d.N * d.OH * d.OW >= g_psw_minm;
 }
 // rows 4 C, columns T^2 K, K = dy pixels; 64-row tiles for 4 C <= 64, 64 / 128 columns by make_plan's cost rule,
 // split-K to make_plan's block target.  Every tile writes the slab (splits >= 1), the reduce scatters.

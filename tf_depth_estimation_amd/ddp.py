@@ -17,24 +17,33 @@ so the exchange of late layers overlaps the backward conv of early ones.  `finis
 bucket never reported and makes the compute stream wait for the comm stream before Adam.
 
 Under hipGraph capture there are two modes:
-  * mode "graph" (the default over RCCL, round 5): the all-reduces are CAPTURED.  A launch point forks the chunk's
-    comm stream off the capture stream (an event; the filter-gradient / branch streams that wrote the bucket's
-    gradients are waited on the same way), the bucket's all-reduce (ReduceOp.SUM) becomes a graph node on that branch, and `join(chunk)` at the end of the program's backward joins it back -- no
-    graph is cut, so each network's forward, loss, backward, exchange and Adam replay as the graph (piece) they are.
-    Each chunk all-reduces on a communicator of its own (created in chunk order on every rank): with config 4's two
-    networks on two streams, each communicator is used from one graph branch in a fixed order;
+  * mode "segments" (the default; gloo and RCCL): a launch point closes the current graph segment (the program's
+    filter-gradient branch joined first) and replay runs segment, its buckets eagerly, next segment ... so the
+    collectives stay OUTSIDE the graphs.  Every all-reduce of a step is issued by the host thread, in replay order,
+    on ONE comm stream and ONE communicator: the issue order is the program order on every rank, whatever the GPU
+    timing (tests/test_ddp.py `order` case), and ProcessGroupNCCL's watchdog only ever polls events recorded
+    eagerly.  Round 6 made this the default everywhere: the captured mode below
+    aborted once in the driver's GPU suite (GPUTEST_r05, SIGABRT inside Trainer.capture) and no world > 1 run of it
+    exists;
+  * mode "graph" (opt-in, RCCL only, rounds 5-6): the all-reduces are CAPTURED.  A launch point first joins the
+    chunk's filter-gradient branch into the current (capture) stream (pre_launch), then forks the chunk's comm stream
+    off that stream alone -- every fork of the capture is ONE level deep (round 6: round 5 made the comm branch also
+    wait on the filter-gradient branch, a fork of a fork, the shape DESIGN.md §5 records as crashing
+    hipStreamEndCapture) -- and the bucket's all-reduce (ReduceOp.SUM) becomes a graph node on that branch;
+    `join(chunk)` at the end of the program's backward joins it back, so no graph is cut.  Each chunk all-reduces on
+    a communicator of its own (created in chunk order on every rank).  With the net overlap two graphs replay
+    concurrently on two streams, so two communicators would run in an order no rank controls: Trainer refuses graph
+    mode with the net overlap at world > 1, and an explicit `group` shared by several chunks is refused here.
     Bucket size: measured on one GPU (config 4, world-1 RCCL group, bench.py --exchange on), every comm-branch fork
     in the middle of a backward stalls the other network's chain (its wait packets sit in FIFO hardware queues shared
     with it, GPU_MAX_HW_QUEUES = 4): 32 / 64 / 128 MB buckets 782 / 720 / 897 pairs/s, one bucket per
-    network (256 MB) 1049-1055, against 1089-1093 without the exchange -- hence Trainer.enable_ddp's 256 MB default.
-    (Issuing the all-reduce on the reporting stream itself, no branch at all, measured 780-784: worse.)
+    network (256 MB) 1049-1055, against 1089-1093 without the exchange -- hence Trainer.enable_ddp's 256 MB default
+    (DESIGN.md §6 derives the same default from a world-8 model).
     The 1/world of the mean is NOT a pass of its own: chunk.grad holds the replicas' SUM after the exchange and Adam
-    applies `grad_scale` (= 1/world, Trainer.enable_ddp) as it reads the gradient.  ReduceOp.AVG would fold the scale
-    into RCCL instead, but RCCL runs AVG as a pre-multiplied sum with an extra kernel per call -- at world 1 a
-    oneRankReduce copy pass, 52 calls x 219 us per config-4 step, measured 1048-1051 pairs/s against 1083-1087 with
-    SUM (profiles/r05/bench_ab_exchange_sum.md);
-  * mode "segments" (rounds 2-4; gloo falls back to it): a launch point closes the current graph segment and replay
-    runs segment, its buckets eagerly, next segment ... so RCCL stays outside the graphs.
+    applies `grad_scale` (= 1/world) as it reads the gradient (train.Adam reads it from this object at every update).
+    ReduceOp.AVG would fold the scale into RCCL instead, but RCCL runs AVG as a pre-multiplied sum with an extra kernel
+    per call -- at world 1 a oneRankReduce copy pass, 52 calls x 219 us per config-4 step, measured 1048-1051 pairs/s
+    against 1083-1087 with SUM (profiles/r05/bench_ab_exchange_sum.md).
 
 On CPU (gloo, device 'cpu') the same bookkeeping runs synchronously; tests/test_ddp.py drives it with
 world_size 2.
@@ -107,12 +116,13 @@ class GradSync:
 
     def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None, side_streams=None,
                  mode=None, pre_fork=None):
-        import torch.distributed as dist
         self.world, self.group = world, group
-        # pre_launch(chunk): called before a bucket launch point UNDER CAPTURE -- joins the streams that write the
-        # chunk's gradients beside the capture stream (its program's filter-gradient branch, NetProgram.join_wgrad),
-        # since a graph segment can only end with its forked branches joined.  Eagerly the compute stream never
-        # waits: side_streams(chunk) lists those streams and the comm stream waits on an event at each one's tail.
+        # pre_launch(chunk): joins the streams that write the chunk's gradients beside the current stream (its
+        # program's filter-gradient branch, NetProgram.join_wgrad) into it.  Called before every graph-mode fork (so
+        # the comm branch forks from the current stream alone) and, in segments mode, before a launch point under
+        # capture (a graph segment can only end with its forked branches joined).  Eagerly in segments mode the
+        # compute stream never waits: side_streams(chunk) lists those streams and the comm stream waits on an event
+        # at each one's tail.
         self.pre_launch = pre_launch
         self.side_streams = side_streams
         self.chunks = list(chunks)
@@ -128,13 +138,18 @@ class GradSync:
         self.device = self.chunks[0].grad.device if self.chunks else torch.device("cpu")
         self.gpu = self.device.type == "cuda"
         # a dedicated HIP stream (never one of torch's pooled streams, which a capture stream may alias)
-        self.comm = _lib.dedicated_stream() if self.gpu else None
+        self.comm = self._new_stream() if self.gpu else None
         self.capturing = None       # set by Trainer.capture: callable(buckets) closing a graph segment
         self.log = []               # launch order (names), for tests
-        nccl = self.gpu and dist.is_initialized() and dist.get_backend(group) == "nccl"
-        self.mode = mode or ("graph" if nccl else "segments")
+        nccl = self._rccl(group)
+        self.mode = mode or "segments"
         if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
             raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
+        if self.mode == "graph" and group is not None and len(self.chunks) > 1:
+            #  graph mode gives every chunk a comm branch of its own; one explicit communicator under
+            # several branches would see their collectives in an order no rank controls
+            raise ValueError("exchange mode 'graph' with an explicit group and several parameter chunks: one "
+                             "communicator would serve concurrent graph branches; use mode 'segments'")
         self.captured = self.mode != "segments"
         # what the optimizer multiplies the exchanged gradient by: graph mode leaves the replicas' SUM in chunk.grad
         # (no scale pass on the comm branch), segments mode the mean
@@ -146,10 +161,41 @@ class GradSync:
         self.comm_of, self.group_of = {}, {}
         if self.captured:
             for i, c in enumerate(self.chunks):
-                self.comm_of[id(c)] = _lib.dedicated_stream()
-                self.group_of[id(c)] = pooled_group("exchange", i) if group is None else group
+                self.comm_of[id(c)] = self._new_stream()
+                self.group_of[id(c)] = self._chunk_group(i) if group is None else group
         self.forked = set()         # chunks whose comm stream has work not yet joined (graph mode)
         self.begin_step()
+
+    # ---- stream / collective primitives (tests/test_ddp.py replays the graph-mode topology through a subclass that
+    # records them instead of touching HIP or a process group)
+    def _rccl(self, group):
+        import torch.distributed as dist
+        return self.gpu and dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+    @staticmethod
+    def _new_stream():
+        return _lib.dedicated_stream()
+
+    @staticmethod
+    def _chunk_group(i):
+        return pooled_group("exchange", i)
+
+    @staticmethod
+    def _current():
+        return torch.cuda.current_stream()
+
+    @staticmethod
+    def _on(stream):
+        return torch.cuda.stream(stream)
+
+    @staticmethod
+    def _wait(waiter, waitee):
+        _lib.wait_stream(waiter, waitee)
+
+    @staticmethod
+    def _all_reduce(view, group):
+        import torch.distributed as dist
+        dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
 
     # ---- per-step bookkeeping
     def begin_step(self):
@@ -219,22 +265,23 @@ class GradSync:
                 _lib.check(lib.tde_scale(v.numel(), _lib.ptr(v), 1.0 / self.world, st), "grad scale")
 
     def launch_forked(self, buckets, chunk):
-        """Graph mode: all-reduce (sum; Adam applies 1/world) `buckets` on the chunk's comm stream, forked from the current stream (and
-        after the chunk's side streams' tails) by events -- capture-legal, so under capture the all-reduces are graph
-        nodes of a branch that join(chunk) merges back; eagerly the same stream order."""
-        import torch.distributed as dist
+        """Graph mode: all-reduce (sum; Adam applies 1/world) `buckets` on the chunk's comm stream.  The chunk's
+        filter-gradient branch is first joined into the current stream (pre_launch: its deferred calls issued, then
+        the current stream waits on its tail), and the comm stream is forked from the current stream ALONE -- one
+        level deep under capture, where the all-reduces become graph nodes of a branch that join(chunk) merges back;
+        eagerly the same stream order."""
         self.log.extend(list(b.names) for b in buckets)
         if chunk is None:
             chunk = buckets[0].chunk
-        if self.pre_fork is not None:
+        if self.pre_launch is not None:
+            self.pre_launch(chunk)
+        elif self.pre_fork is not None:
             self.pre_fork(chunk)
         comm = self.comm_of[id(chunk)]
-        _lib.wait_stream(comm, torch.cuda.current_stream())
-        for sd in (self.side_streams(chunk) if self.side_streams else ()):
-            _lib.wait_stream(comm, sd)
-        with torch.cuda.stream(comm):
+        self._wait(comm, self._current())
+        with self._on(comm):
             for b in buckets:
-                dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.group_of[id(chunk)])
+                self._all_reduce(b.view(), self.group_of[id(chunk)])
         self.forked.add(id(chunk))
 
     def join(self, chunk):
@@ -248,7 +295,7 @@ class GradSync:
                 b.launched = True
             self.launch_forked(rest, chunk)
         if id(chunk) in self.forked:
-            _lib.wait_stream(torch.cuda.current_stream(), self.comm_of[id(chunk)])
+            self._wait(self._current(), self.comm_of[id(chunk)])
             self.forked.discard(id(chunk))
 
     def leftovers(self):

@@ -50,10 +50,16 @@ class Adam:
 
     def __init__(self, chunk, lr=2e-4, beta1=0.9, beta2=0.999, eps=1e-8):
         self.chunk, self.lr, self.b1, self.b2, self.eps = chunk, lr, beta1, beta2, eps
-        self.t = torch.zeros(1, device="cuda", dtype=torch.float32)
-        # applied to the gradient as Adam reads it: 1/world when the captured exchange leaves the replicas' SUM in
-        # chunk.grad (ddp.GradSync graph mode)
-        self.grad_scale = 1.0
+        self.t = torch.zeros(1, device=chunk.flat.device, dtype=torch.float32)
+        # the exchange whose gradient convention applies (link_grad_scale / Trainer.enable_ddp): graph mode leaves
+        # the replicas' SUM in chunk.grad, segments mode the mean
+        self.scale_src = None
+
+    @property
+    def grad_scale(self):
+        """What the gradient is multiplied by as Adam reads it, looked up at every update: 1/world
+        while a captured exchange (ddp.GradSync graph mode) leaves the replicas' SUM in chunk.grad, else 1."""
+        return 1.0 if self.scale_src is None else float(self.scale_src.grad_scale)
 
     def step(self):
         self.begin()
@@ -74,6 +80,17 @@ class Adam:
             return ctypes.c_void_p(t.data_ptr() + 4 * lo)
         _lib.check(lib.tde_adam_update(hi - lo, at(c.flat), at(c.grad), at(c.adam_m), at(c.adam_v), ptr(self.t),
                                        self.lr, self.b1, self.b2, self.eps, self.grad_scale, st), "adam")
+
+
+def optimizers(opt):
+    """The Adam instances behind a trainer's optimizer (an Adam or a MultiAdam)."""
+    return list(opt.opts) if hasattr(opt, "opts") else [opt]
+
+
+def link_grad_scale(opt, sync):
+    """Make every Adam behind `opt` read its gradient scale from `sync` (a ddp.GradSync, or None to unlink)."""
+    for o in optimizers(opt):
+        o.scale_src = sync
 
 
 class AdamOverlap:
@@ -292,6 +309,7 @@ class Trainer:
             raise ValueError("net overlap is for the step without Adam overlap / deferred Adam / host-side SyncBN")
         if on:
             self._check_sync_bn_streams(net=True)
+            self._check_exchange_streams(net=True)
         self.net_stream = _lib.owned_stream(self, "net") if on else None
         return self
 
@@ -383,6 +401,18 @@ class Trainer:
             raise ValueError("SyncBN with an explicit process group shares one communicator over several streams: "
                              "no overlap or bucketed exchange with it")
 
+    def _check_exchange_streams(self, net=False):
+        """The captured exchange (GradSync graph mode) all-reduces each network's buckets on a communicator and graph
+        branch of its own.  With the net overlap the two networks' graphs replay concurrently on two streams, so at
+        world > 1 the two communicators' collectives would meet in an order no rank fixes: refused --
+        segments mode (the default) issues every collective from the host, in program order, on one comm stream."""
+        gs = self.grad_sync
+        if gs is None or not getattr(gs, "captured", False) or gs.world <= 1:
+            return
+        if net or self.net_stream is not None:
+            raise ValueError("the captured (graph-mode) gradient exchange at world > 1 with the net overlap would run "
+                             "two communicators in an unfixed order: use exchange mode 'segments' (the default)")
+
     timeline = None           # program.StepTimeline (diagnostic, probe/step_timeline.py)
 
     def set_timeline(self, tl):
@@ -445,10 +475,12 @@ class Trainer:
                 q._flush_wgrad()
 
     def enable_ddp(self, world, bucket_mb=256.0, group=None, mode=None):
-        """Bucketed gradient all-reduce overlapped with backward (ddp.GradSync).  mode "graph" (default over RCCL):
-        the all-reduces are captured into the step's graphs on a per-network comm branch, joined at the end of that
-        network's backward (its Adam then runs inline, as in the single-GPU step); "segments": the round-2 scheme,
-        graphs cut at every bucket launch point and RCCL issued eagerly between segment replays."""
+        """Bucketed gradient all-reduce overlapped with backward (ddp.GradSync).  mode "segments" (the default since
+        round 6): graphs cut at every bucket launch point and every collective issued eagerly by the host between
+        segment replays, in program order, on one comm stream; "graph" (opt-in, RCCL): the all-reduces are captured
+        into the step's graphs on a per-network comm branch forked one level deep, joined at the end of that network's
+        backward (its Adam then runs inline, as in the single-GPU step) -- refused with the net overlap at world > 1
+        (_check_exchange_streams).  256 MB = one bucket per network at config 4 (the world-8 model)."""
         from .ddp import GradSync
         if self.adam_ov is not None:
             raise ValueError("Adam overlap and the data-parallel exchange are exclusive")
@@ -456,9 +488,9 @@ class Trainer:
         self.grad_sync = GradSync(self.chunks, world, bucket_mb=bucket_mb, uses=uses, group=group,
                                   pre_launch=self._join_chunk_wgrad, side_streams=self._chunk_side_streams, mode=mode,
                                   pre_fork=self._flush_chunk_wgrad)
-        for o in (self.opt.opts if hasattr(self.opt, "opts") else [self.opt]):
-            o.grad_scale = self.grad_sync.grad_scale
+        link_grad_scale(self.opt, self.grad_sync)
         self._check_sync_bn_streams()
+        self._check_exchange_streams()
         return self.grad_sync
 
     def enable_sync_bn(self, world, group=None):
@@ -511,6 +543,13 @@ class Trainer:
         if gs is not None:
             gs()
         self._update()
+
+    def segment_cuts(self):
+        """Graph cuts the segmented exchange made in the captured step (0 without it, or in graph mode)."""
+        seq = getattr(self, "ov_seq", None)
+        if seq is not None:
+            return sum(max(0, len(segs) - 1) for _, segs in seq if segs is not None)
+        return max(0, len(self.segments) - 1) if self.segments is not None else 0
 
     def release_graphs(self):
         """Drop the captured graphs (their memory pools go with them); step() runs eagerly until the next capture."""
