@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TDE_ABI_VERSION 9
+#define TDE_ABI_VERSION 10
 
 /* An operand bound (tde_conv_desc_t.*_absmax, tde_bn_bwd dz_absmax) is an array of this many floats whose
  * maximum is the bound: producers raise one slot per workgroup (atomic max), consumers read all. */
@@ -321,6 +321,28 @@ typedef struct {
   int out_coff[TDE_MAX_FRAMES];
 } tde_image_batch_t;
 int tde_image_resize_unpack(const tde_image_batch_t* args, void* stream);
+
+/* ---------------------------------------------------------------- inference pre / post-processing (ABI 10)
+ * The OpenCV steps of batch_prediction.py:62,72-73 on the GPU, restated from OpenCV 4.x's scalar reference code
+ * (cv2 is a pip dependency of the reference, not vendored; parity unpinned -- oracle/cv_ops.py restates the same):
+ *   I = cv2.resize(I, (224, 224), interpolation=cv2.INTER_AREA)   (:62, replaces the host cv2 call)
+ * src uint8 [B,H,W,C] (C <= 4, dense) -> [B,OH,OW,C]: dst_u8 (dense) and / or dst_f32 (float of the same values,
+ * pixel stride f32_cstride: e.g. the network's padded input buffer); true area averaging when both scales are >= 1
+ * (integer scales: the box mean), OpenCV's area-emulating fixed-point linear path otherwise. */
+int tde_resize_area_u8(int B, int H, int W, int C, const uint8_t* src, int OH, int OW, uint8_t* dst_u8,
+                       float* dst_f32, int f32_cstride, void* stream);
+/*   z = cv2.resize(pred[0][0,:,:,0], (image_width, image_height), interpolation=cv2.INTER_CUBIC)   (:72)
+ * one channel (channel s_coff of a view with pixel stride s_cstride, e.g. a disparity output) [B,H,W] ->
+ * dense float [B,OH,OW]; bicubic A = -0.75, edge taps replicated. */
+int tde_resize_cubic_f32(int B, int H, int W, const float* src, int s_cstride, int s_coff, int OH, int OW,
+                         float* dst, void* stream);
+/*   z = cv2.bilateralFilter(z, 9, 75, 75)   (:73)
+ * dense float [B,H,W] -> [B,H,W] (src != dst), each image filtered on its own: circular window of radius d/2,
+ * spatial weights exp(-r^2 / 2 sigma_space^2), colour weights from a 4096-bin exp table over the image's value
+ * range, BORDER_REFLECT_101; a constant image is copied.  ws: tde_bilateral_workspace_size(B) bytes. */
+size_t tde_bilateral_workspace_size(int B);
+int tde_bilateral_f32(int B, int H, int W, const float* src, float* dst, int d, double sigma_color,
+                      double sigma_space, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- loss head
  * Fused forward+backward of the scalar loss terms: each call ADDS weight*term to loss[0] (a

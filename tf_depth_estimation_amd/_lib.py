@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must be imported first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtde.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 BOUND_SLOTS = 16   # TDE_BOUND_SLOTS: an operand bound is the max of this many device floats
 # tde_set_conv_math modes (include/tde.h): exact fp32 MFMA, bf16x3 (~2^-16 per product), and the
 # fp32-accurate three-way bf16 split ("bf16x6": staged in LDS / split in registers)
@@ -89,6 +89,11 @@ _SIGS = {
     "tde_conv2d_split_weights_size": (c_size_t, [P, c_int]),
     "tde_conv2d_split_weights": (c_int, [c_int, P, P, P, P, P]),
     "tde_image_resize_unpack": (c_int, [P, P]),
+    "tde_resize_area_u8": (c_int, [c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, c_int, P]),
+    "tde_resize_cubic_f32": (c_int, [c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "tde_bilateral_workspace_size": (c_size_t, [c_int]),
+    "tde_bilateral_f32": (c_int, [c_int, c_int, c_int, P, P, c_int, ctypes.c_double, ctypes.c_double, P, c_size_t,
+                                  P]),
     "tde_loss_depth_pyramid": (c_int, [P, P]),
     "tde_warp_loss_multi": (c_int, [P, c_int, P]),
     "tde_loss_depth_pyramid_multi": (c_int, [P, c_int, P]),

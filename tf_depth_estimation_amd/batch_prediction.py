@@ -12,11 +12,15 @@ pose, masks).  Here:
     no separate normalisation pass;
   * the whole forward is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed per call,
     so a batch-1 prediction is one graph launch (latency-bound at batch 1: ~30 layers);
-  * `restore(prefix)` reads the TF-1 V2 bundle (checkpoint.Saver) and re-folds/re-captures.
-
-The host-side post-processing of batch_prediction.py:72-75 (cv2.resize INTER_CUBIC to the output size,
-cv2.bilateralFilter, .tofile) stays on the host with the caller: it is OpenCV, outside the GPU path.
+  * `restore(prefix)` reads the TF-1 V2 bundle (checkpoint.Saver) and re-folds/re-captures;
+  * the script's OpenCV steps run on the GPU too (csrc/postproc.hip, restated from OpenCV's published scalar
+    code -- cv2 is not vendored, parity unpinned): `resize_area` for `cv2.resize(I, (224, 224), INTER_AREA)` (:62),
+    written straight into the network input, `resize_cubic` + `bilateral_filter` for
+    `cv2.resize(pred[0][0,:,:,0], (image_width, image_height), INTER_CUBIC)` and `cv2.bilateralFilter(z, 9, 75, 75)`
+    (:72-73); `Predictor.predict_depth_map` is the loop body of batch_prediction.py:58-75 (uint8 image -> z map).
 """
+import ctypes
+
 import torch
 
 from . import _api, _lib, _netlib, checkpoint, pose_ops, variables
@@ -31,6 +35,70 @@ NETS = {
     "depth_net": ("depth_cam_net", _netlib.depth_net_spec, 6, dict(levels=2),
                   "nets_optflow_depth.depth_net (batch_prediction_cam_est.py)"),
 }
+
+
+def resize_area(images, oh, ow, out=None, out_f32=None):
+    """cv2.resize(I, (ow, oh), interpolation=cv2.INTER_AREA) (batch_prediction.py:62) of a uint8 [B,H,W,C] device
+    batch (C <= 4) -> uint8 [B,oh,ow,C] (`out`), and / or its float values into `out_f32` ([B,oh,ow,>=C], e.g. a
+    network input).  Returns `out` (allocated when neither output is given)."""
+    if images.dtype != torch.uint8 or images.dim() != 4 or not images.is_contiguous():
+        raise ValueError("resize_area expects a contiguous uint8 [B,H,W,C] tensor")
+    B, H, W, C = images.shape
+    if out is None and out_f32 is None:
+        out = torch.empty((B, oh, ow, C), dtype=torch.uint8, device=images.device)
+    fcs = 0
+    if out_f32 is not None:
+        if out_f32.dtype != torch.float32 or tuple(out_f32.shape[:3]) != (B, oh, ow) or out_f32.shape[3] < C:
+            raise ValueError("out_f32 must be float32 [B,oh,ow,>=C]")
+        fcs = out_f32.stride(2)
+        if out_f32.stride(1) != ow * fcs or out_f32.stride(0) != oh * ow * fcs:
+            raise ValueError("out_f32 must be a pixel-major channel view")
+    if out is not None and (tuple(out.shape) != (B, oh, ow, C) or out.dtype != torch.uint8 or not out.is_contiguous()):
+        raise ValueError("out must be a contiguous uint8 [B,oh,ow,C] tensor")
+    lib = _lib.load()
+    _lib.check(lib.tde_resize_area_u8(B, H, W, C, _lib.ptr(images), oh, ow, _lib.ptr(out), _lib.ptr(out_f32), fcs,
+                                      _lib.stream_ptr()), "resize_area")
+    return out
+
+
+def resize_cubic(maps, oh, ow, out=None):
+    """cv2.resize(z, (ow, oh), interpolation=cv2.INTER_CUBIC) (batch_prediction.py:72) of a float [B,H,W] batch or
+    of channel 0 of a [B,H,W,C] view (e.g. a disparity output) -> float [B,oh,ow]."""
+    if maps.dtype != torch.float32:
+        raise ValueError("resize_cubic expects float32 maps")
+    t = maps if maps.dim() == 4 else maps.unsqueeze(-1)
+    B, H, W, _ = t.shape
+    cs = t.stride(2)
+    if t.stride(1) != W * cs or t.stride(0) != H * W * cs:
+        raise ValueError("resize_cubic expects a pixel-major [B,H,W(,C)] view")
+    if out is None:
+        out = torch.empty((B, oh, ow), dtype=torch.float32, device=maps.device)
+    lib = _lib.load()
+    _lib.check(lib.tde_resize_cubic_f32(B, H, W, _lib.ptr(t), cs, 0, oh, ow, _lib.ptr(out), _lib.stream_ptr()),
+               "resize_cubic")
+    return out
+
+
+_BIL_WS = {}
+
+
+def bilateral_filter(maps, d=9, sigma_color=75.0, sigma_space=75.0, out=None):
+    """cv2.bilateralFilter(z, d, sigma_color, sigma_space) (batch_prediction.py:73) of each map of a dense float
+    [B,H,W] batch (BORDER_REFLECT_101) -> float [B,H,W]."""
+    if maps.dtype != torch.float32 or maps.dim() != 3 or not maps.is_contiguous():
+        raise ValueError("bilateral_filter expects a contiguous float32 [B,H,W] tensor")
+    B, H, W = maps.shape
+    if out is None:
+        out = torch.empty_like(maps)
+    lib = _lib.load()
+    nb = lib.tde_bilateral_workspace_size(B)
+    ws = _BIL_WS.get((maps.device, B))
+    if ws is None:
+        ws = _BIL_WS[(maps.device, B)] = torch.empty(max(nb // 4, 4), dtype=torch.float32, device=maps.device)
+    _lib.check(lib.tde_bilateral_f32(B, H, W, _lib.ptr(maps), _lib.ptr(out), int(d), ctypes.c_double(sigma_color),
+                                     ctypes.c_double(sigma_space), _lib.ptr(ws), nb, _lib.stream_ptr()),
+               "bilateral_filter")
+    return out
 
 
 class Predictor:
@@ -83,6 +151,27 @@ class Predictor:
         """saver.restore(sess, checkpoint) (batch_prediction.py:55), then re-fold / re-capture."""
         checkpoint.Saver().restore(None, save_path)
         self.refresh()
+
+    def predict_depth_map(self, image_u8, out_hw=(240, 720)):
+        """The body of batch_prediction.py:58-75 for one decoded image (uint8 [h,w,3] or a [B,h,w,3] batch, host or
+        device): INTER_AREA resize into the network input (:62; the pixel values 0..255 are fed as they are -- the
+        script's /255 is commented out, :65-67), the prediction (:70), then the INTER_CUBIC resize of disp1's map to
+        out_hw = (FLAGS.image_height, FLAGS.image_width) (:72) and the 9 / 75 / 75 bilateral filter (:73).  Returns
+        the float [B, out_h, out_w] maps the script writes with .tofile (:75)."""
+        if self.net != "disp_net":
+            raise ValueError("predict_depth_map is batch_prediction.py's disp_net path")
+        img = image_u8 if image_u8.dim() == 4 else image_u8.unsqueeze(0)
+        img = img.to(device=self.x.device, dtype=torch.uint8).contiguous()
+        B, H, W = self.x.shape[:3]
+        if img.shape[0] != B or img.shape[3] != 3:
+            raise ValueError(f"expected {B} RGB image(s), got {tuple(img.shape)}")
+        resize_area(img, H, W, out_f32=self.x)
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.outs = self._forward()
+        z = resize_cubic(self.outs[0], out_hw[0], out_hw[1])
+        return bilateral_filter(z, 9, 75.0, 75.0)
 
     def __call__(self, images):
         """images: [batch, H, W, cin] float32 (host or device).  Returns the output list."""
