@@ -7,8 +7,22 @@ import os
 import numpy as np
 
 
+def _rigid(rng):
+    """A random small rigid motion as a 4x4 matrix (Rodrigues of a random angle-axis, a unit-ish translation)."""
+    ax = rng.standard_normal(3)
+    ax /= np.linalg.norm(ax)
+    th = rng.uniform(0.02, 0.2)
+    K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    T = np.eye(4)
+    T[:3, :3] = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+    T[:3, 3] = 0.1 * rng.standard_normal(3)
+    return T
+
+
 def make_dataset(root, n, strip_hw=(60, 180), image_hw=(30, 90), split="train", seed=0, sizes=None,
-                 quality=92):
+                 quality=92, rigid=False):
+    """rigid=True: the two 4x4 matrices of each tgt2src_proj file are a rigid motion and its inverse (a camera
+    pose the config-4 cam loss can take), else 32 random numbers."""
     from PIL import Image
     rng = np.random.default_rng(seed)
     lines = []
@@ -28,7 +42,11 @@ def make_dataset(root, n, strip_hw=(60, 180), image_hw=(30, 90), split="train", 
         cam = [fx, 0.0, rng.uniform(40, 60), 0.0, fy, rng.uniform(10, 20), 0.0, 0.0, 1.0]
         with open(os.path.join(root, sub, fid + "_cam.txt"), "w") as f:
             f.write(",".join(f"{v:.6f}" for v in cam))
-        proj = list(rng.normal(0, 1, 32)) + [rng.uniform(0.5, 2.0)]
+        if rigid:
+            T = _rigid(rng)
+            proj = list(T.reshape(-1)) + list(np.linalg.inv(T).reshape(-1)) + [rng.uniform(0.5, 2.0)]
+        else:
+            proj = list(rng.normal(0, 1, 32)) + [rng.uniform(0.5, 2.0)]
         with open(os.path.join(root, sub, fid + "_tgt2src_proj.txt"), "w") as f:
             f.write(" ".join(f"{v:.6f}" for v in proj) + " ")
         lines.append(f"{sub} {a} {b}\n")

@@ -160,3 +160,71 @@ def test_loader_feeds_a_training_step(tmp_path):
         assert np.isfinite(tr.total_loss())
     finally:
         dl.close()
+
+
+def _pose_vec(T):
+    """[B,4,4] rigid motions -> [B,6] (translation, angle-axis rotation): the gt_right_cam layout of
+    train_depth_then_cam_lr.py:117-118 (concat(translation, rotation))."""
+    from scipy.spatial.transform import Rotation
+    T = np.asarray(T, np.float64)
+    return np.concatenate([T[:, :3, 3], Rotation.from_matrix(T[:, :3, :3]).as_rotvec()], 1).astype(np.float32)
+
+
+def test_loader_feeds_a_config4_step(tmp_path):
+    """config 4 (train_depth_then_cam_lr.py:117-154 wiring, with the imageselect loader the
+    script has commented in at :104-115) trained from the built loader: tgt -> image_left, src -> image_right (both
+    /255 - 0.5), the label, the loader's multi-scale intrinsics, and the camera from the first tgt2src projection
+    (a rigid motion -> (t, angle-axis)).  The first step's loss terms equal the float64 oracle's on the same batch
+    (1e-5; consistency 1e-4), and captured steps on the next batches stay finite."""
+    from oracle import losses as OL
+    from oracle import nets as ON
+    from test_gpu_nets import oracle_params_from
+    from tf_depth_estimation_amd import _api, train, variables
+    from tf_depth_estimation_amd.imageselect_Dataloader_optflow import DataLoader
+    B, H, W = 2, 64, 96
+    root = make_dataset(str(tmp_path), 6, strip_hw=(64, 192), image_hw=(H, W), rigid=True)
+    dl = DataLoader(root, B, H, W, 1, 4, "train", resizedheight=H, resizedwidth=W, shuffle=False, num_epochs=2)
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    tr = train.DepthThenCamTrainer(B, H, W)
+    try:
+        tgt, src, label, intr, projs, m = dl.load_train_batch()
+        il, ir = tgt / 255.0 - 0.5, src[..., :3] / 255.0 - 0.5
+        gt = torch.from_numpy(_pose_vec(projs[:, 0].cpu().numpy())).cuda()
+        assert intr.shape == (B, 4, 3, 3) and projs.shape == (B, 2, 4, 4)
+        tr.set_batch(il, ir, label, intr, gt)
+        P = {dt: (oracle_params_from(tr.single.chunk, "", dt), oracle_params_from(tr.pair.chunk, "", dt))
+             for dt in (torch.float64,)}
+        tr.phase_compute()
+        torch.cuda.synchronize()
+        parts = tr.loss_parts()
+        Pss, Ppp = P[torch.float64]
+        x = {k: v.detach().double().cpu() for k, v in dict(il=il, ir=ir).items()}
+        dsl = ON.disp_net(Pss, x["il"], True, scope="model_singledepth/depth_net")
+        dsr = ON.disp_net(Pss, x["ir"], True, scope="model_singledepth/depth_net")
+        dpl, pr, ml = ON.depth_net(Ppp, torch.cat([x["il"], x["ir"]], -1), True, scope="model_pairdepth/depth_cam_net",
+                                   levels=4)
+        dpr, pl, mr = ON.depth_net(Ppp, torch.cat([x["ir"], x["il"]], -1), True, scope="model_pairdepth/depth_cam_net",
+                                   levels=4)
+        total, rp = OL.loss_depth_then_cam_lr(dsl, dsr, dpl, dpr, pr, pl, ml, mr, x["il"], x["ir"],
+                                              label.double().cpu(), intr.double().cpu(), gt.double().cpu())
+
+        def val(t):
+            return t.item() if torch.is_tensor(t) else float(t)
+        for k in ("smooth", "depth", "exp", "cam"):
+            assert abs(parts[k] - val(rp[k])) <= 1e-5 * abs(val(rp[k])) + 1e-9, (k, parts[k], val(rp[k]))
+        assert abs(parts["photo"] - val(rp["pixel"])) <= 1e-5 * val(rp["pixel"]) + 1e-9
+        assert abs(parts["consist"] - val(rp["consist"])) <= 1e-4 * val(rp["consist"]) + 1e-9
+        tr.capture(warmup=1)
+        for _ in range(2):
+            tgt, src, label, intr, projs, m = dl.load_train_batch()
+            tr.set_batch(tgt / 255.0 - 0.5, src[..., :3] / 255.0 - 0.5, label, intr,
+                         torch.from_numpy(_pose_vec(projs[:, 0].cpu().numpy())).cuda())
+            tr.step()
+        torch.cuda.synchronize()
+        assert np.isfinite(tr.total_loss())
+        assert all(torch.isfinite(c.flat).all() for c in tr.chunks)
+    finally:
+        dl.close()
+        tr.release_graphs()
+        _api.clear_programs()
