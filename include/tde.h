@@ -101,13 +101,6 @@ uint32_t tde_crc32c(const void* data, size_t n, uint32_t crc);
  *       accumulation (<= ~3 * 2^-22 relative per product), half the MFMAs of bf16x6.  DEFAULT. */
 int tde_set_conv_math(int mode);
 int tde_get_conv_math(void);
-/* Which conv calls of conv math 4 run the LDS-DMA ring tiles (process-wide, set before capture): a mask of
- * 1 = forward calls (tde_conv2d_fwd*, tde_deconv2d_fwd*), 2 = data-gradient calls (tde_*_bwd_data and the data half
- * of tde_*_bwd), 4 = filter-gradient GEMMs, 8 = forward calls whose GEMM gets 64-row tiles (the deep levels).
- * Default 0 (env TDE_RING): measured slower at config 4.  Returns the previous mask, -1 if out of range.
- * Results are the same either way (tests/test_gpu_kernels.py::test_ring_*); only speed differs. */
-int tde_set_conv_ring(int roles);
-int tde_get_conv_ring(void);
 /* Measurement hook (no reference counterpart: bench.py's roofline timing).  Arms the calling thread's pair of
  * device timestamp slots for the NEXT conv entry call (any tde_conv2d_* / tde_deconv2d_* compute function): a
  * one-wave kernel writes the 100 MHz real-time counter into *stamp_begin right before the call's first
@@ -119,8 +112,7 @@ int tde_conv_span_arm(unsigned long long* stamp_begin, unsigned long long* stamp
  * real-time counter into *slot when the stream reaches it (inside a capture: when the replayed graph does). */
 int tde_stamp(unsigned long long* slot, void* stream);
 size_t tde_conv2d_workspace_size(const tde_conv_desc_t* d, int op /*0 fwd,1 bwd_data,2 bwd_filter*/);
-/* Weight pre-split (the halo-tiled stride-1 path and the ring tiles keep the layer's weights as split fp16 / bf16
- * tiles): bytes of the split image op & 1 (0: the FWD GEMM's, read by a conv's forward; 1: the DGRAD GEMM's, read by
+/* Weight pre-split (the halo-tiled stride-1 path keeps the layer's weights as split fp16 / bf16 tiles): bytes of the split image op & 1 (0: the FWD GEMM's, read by a conv's forward; 1: the DGRAD GEMM's, read by
  * a conv's data gradient) of layer d needs under the current conv math; add 2 to op when d is a deconv's virtual
  * conv (its forward reads image 1, its data gradient image 0), so the size is that of the image the calls of that
  * role read.  0 = that call takes no split weights (then leave d->w_split[op & 1] NULL).  tde_conv2d_split_weights writes

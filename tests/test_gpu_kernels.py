@@ -316,135 +316,6 @@ def test_conv_bwd_data_pixel_shuffle(L, acc, k):
     assert torch.equal(got[..., xco + cin:], base[..., xco + cin:].float().double())
 
 
-RING_CASES = [
-    # deconv?, N, H, W, C(in), C(view), K, k, s, x_cs, x_coff: layers whose forward / data-gradient GEMMs take the LDS-DMA
-    # ring tiles (conv_ring.hip) in fp16x3 (conv: input H x W; deconv: input h x w)
-    (False, 4, 24, 32, 256, 256, 128, 3, 1, 384, 128),   # split-K FWD / DGRAD, offset view, 128-row tiles
-    (False, 2, 13, 17, 30, 32, 64, 5, 2, 36, 4),         # stride 2: 4 DGRAD classes with 3 / 2 taps, w_cin < C
-    (False, 8, 12, 16, 512, 512, 256, 3, 1, 512, 0),     # icnv5-like: 64-row tiles, 2 column tiles of 128
-    (False, 2, 9, 11, 129, 132, 96, 3, 1, 132, 0),       # padded concat, 96-wide column tiles, ragged rows
-    (True, 8, 24, 32, 128, 128, 64, 3, 2, 128, 0),       # deconv: 4 parity classes (class GEMMs) / FWD data grad
-    (True, 8, 64, 64, 32, 32, 16, 3, 2, 32, 0),          # deconv on the pixel-shuffle GEMM (32768 input pixels)
-]
-
-
-@pytest.mark.parametrize("roles", [1, 7])
-@pytest.mark.parametrize("case", RING_CASES)
-def test_ring_presplit_weights(L, case, roles):
-    """The ring tiles' B operand pre-split once (tde_conv2d_split_weights: the per-step image every layer's forward
-    and backward share, include/tde.h w_split) gives results bit-identical to the same call splitting its own copy into
-    the workspace, and both meet the 1e-5 bar against the fp64 oracle: forward, data gradient (single call and the
-    fused data + filter gradient entry) and the filter gradient.  roles = tde_set_conv_ring mask: 1 (ring
-    forward calls only; the backward on the register-staged tiles), 7 every GEMM on the ring."""
-    deconv, N, H, W, cin, C, K, k, s, xcs, xco = case
-    lib = L.load()
-    st = L.stream_ptr()
-    prev = lib.tde_get_conv_math()
-    prev_ring = lib.tde_set_conv_ring(roles)
-    assert prev_ring >= 0
-    L.check(lib.tde_set_conv_math(4))
-    try:
-        if deconv:
-            Hb, Wb = 2 * H, 2 * W
-            _, pt, _ = T.same_pad(Hb, k, 2)
-            _, pl, _ = T.same_pad(Wb, k, 2)
-            # virtual conv: x = deconv output [N, 2H, 2W, K], y = deconv input [N, H, W, C]
-            d = conv_desc(L, N=N, H=Hb, W=Wb, C=K, OH=H, OW=W, K=C, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
-                          w_cin=K, x_cstride=K, x_coff=0, y_cstride=xcs, y_coff=xco)
-            wt = rnd(k, k, K, cin, seed=72) * 0.2
-            wfull = torch.zeros(k, k, K, C, dtype=torch.float64)
-            wfull[..., :cin] = wt
-            w = wfull
-        else:
-            OH, pt, _ = T.same_pad(H, k, s)
-            OW, pl, _ = T.same_pad(W, k, s)
-            d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=s, pad_top=pt, pad_left=pl,
-                          w_cin=cin, x_cstride=xcs, x_coff=xco, y_cstride=K, y_coff=0)
-            w = rnd(k, k, cin, K, seed=72) * 0.2
-        # image op codes: + 2 for a deconv (its forward reads image 1); an image no call of the enabled roles reads
-        # has size 0 and stays NULL
-        codes = [o | (2 if deconv else 0) for o in (0, 1)]
-        sizes = [lib.tde_conv2d_split_weights_size(ctypes.byref(d), oc) for oc in codes]
-        fwd_img = 1 if deconv else 0
-        assert sizes[fwd_img] > 0, f"ring forward not taken: {sizes}"
-        if roles == 1:
-            assert sizes[1 - fwd_img] == 0, f"data-gradient image without the ring data-gradient role: {sizes}"
-        gw = dev(w)
-        imgs = [torch.empty(sz // 4 + 64, device="cuda") if sz else None for sz in sizes]
-        todo = [o for o in (0, 1) if sizes[o]]
-        descs = (ctypes.c_void_p * len(todo))(*[ctypes.addressof(d) for _ in todo])
-        ops = (ctypes.c_int * len(todo))(*[codes[o] for o in todo])
-        wps = (ctypes.c_void_p * len(todo))(*[gw.data_ptr() for _ in todo])
-        outs = (ctypes.c_void_p * len(todo))(*[imgs[o].data_ptr() for o in todo])
-        L.check(lib.tde_conv2d_split_weights(len(todo), descs, ops, wps, outs, st))
-        ws = ws_for(L, d, deconv=deconv)
-        qb = lib.tde_deconv2d_bwd_workspace_size if deconv else lib.tde_conv2d_bwd_workspace_size
-        if qb(ctypes.byref(d)) > ws.numel() * 4:
-            ws = torch.empty(qb(ctypes.byref(d)) // 4 + 16, device="cuda")
-        wsb = ws.numel() * 4
-        # the forward of the layer and its data gradient, without and with the pre-split images
-        if deconv:
-            xin = rnd(N, H, W, xcs, seed=71)
-            xin[..., xco + cin:] = 0.0
-            gx = dev(xin)
-            dyb = rnd(N, 2 * H, 2 * W, K, seed=73)
-            gdy = dev(dyb)
-        else:
-            xin = rnd(N, H, W, xcs, seed=71)
-            xin[..., xco + cin:xco + C] = 0.0
-            gx = dev(xin)
-            dyb = rnd(N, d.OH, d.OW, K, seed=73)
-            gdy = dev(dyb)
-        res = []
-        for split in (False, True):
-            d.w_split[0], d.w_split[1] = [im.data_ptr() if split and im is not None else None for im in imgs]
-            if deconv:
-                y = torch.zeros(N, 2 * H, 2 * W, K, device="cuda")
-                L.check(lib.tde_deconv2d_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(y), 0, L.ptr(ws), wsb, st))
-                dx = torch.zeros(N, H, W, xcs, device="cuda")
-                L.check(lib.tde_deconv2d_bwd_data(ctypes.byref(d), L.ptr(gdy), L.ptr(gw), L.ptr(dx), 0, L.ptr(ws), wsb, st))
-                dx2 = torch.zeros(N, H, W, xcs, device="cuda")
-                dw2 = torch.empty_like(gw)
-                L.check(lib.tde_deconv2d_bwd(ctypes.byref(d), L.ptr(gdy), L.ptr(gx), L.ptr(gw), L.ptr(dx2), 0, L.ptr(dw2),
-                                             0, L.ptr(ws), wsb, st))
-            else:
-                y = torch.zeros(N, d.OH, d.OW, K, device="cuda")
-                L.check(lib.tde_conv2d_fwd(ctypes.byref(d), L.ptr(gx), L.ptr(gw), L.ptr(y), 0, L.ptr(ws), wsb, st))
-                dx = torch.zeros(N, H, W, xcs, device="cuda")
-                L.check(lib.tde_conv2d_bwd_data(ctypes.byref(d), L.ptr(gdy), L.ptr(gw), L.ptr(dx), 0, L.ptr(ws), wsb, st))
-                dx2 = torch.zeros(N, H, W, xcs, device="cuda")
-                dw2 = torch.empty_like(gw)
-                L.check(lib.tde_conv2d_bwd(ctypes.byref(d), L.ptr(gx), L.ptr(gdy), L.ptr(gw), L.ptr(dx2), 0, L.ptr(dw2),
-                                           0, L.ptr(ws), wsb, st))
-            torch.cuda.synchronize()
-            res.append((y.cpu(), dx.cpu(), dx2.cpu(), dw2.cpu()))
-        d.w_split[0], d.w_split[1] = None, None
-        for a, b, what in zip(res[0], res[1], ("fwd", "bwd_data", "bwd (fused entry) data", "bwd filter")):
-            assert torch.equal(a, b), f"{what}: pre-split image differs from the call's own split"
-    finally:
-        L.check(lib.tde_set_conv_math(prev))
-        lib.tde_set_conv_ring(prev_ring)
-    # against the fp64 oracle
-    if deconv:
-        xr = xin[..., xco:xco + cin].clone().requires_grad_(True)
-        wr = wt.clone().requires_grad_(True)
-        yr = T.conv2d_transpose_same(xr, wr, 2)
-        yr.backward(dyb)
-        close(res[1][0], yr, what="ring deconv fwd")
-        close(res[1][1][..., xco:xco + cin], xr.grad, what="ring deconv data grad")
-        close(res[1][2][..., xco:xco + cin], xr.grad, what="ring deconv data grad (fused entry)")
-        close(res[1][3][..., :cin], wr.grad, what="ring deconv filter grad")
-    else:
-        xr = xin[..., xco:xco + cin].clone().requires_grad_(True)
-        wr = w.clone().requires_grad_(True)
-        yr = T.conv2d_same(xr, wr, s)
-        yr.backward(dyb)
-        close(res[1][0], yr, what="ring conv fwd")
-        close(res[1][1][..., xco:xco + cin], xr.grad, what="ring conv data grad")
-        close(res[1][2][..., xco:xco + cin], xr.grad, what="ring conv data grad (fused entry)")
-        close(res[1][3], wr.grad, what="ring conv filter grad")
-
-
 BN_FUSED_CASES = [
     # deconv?, N, H, W, C(in view), K, k, s      (conv: input H x W;  deconv: input h x w, output 2h x 2w)
     (False, 8, 96, 128, 4, 32, 7, 2),            # cnv1: 768 row tiles, no split

@@ -114,8 +114,6 @@ _SIGS = {
     "tde_crc32c": (ctypes.c_uint32, [P, c_size_t, ctypes.c_uint32]),
     "tde_status_string": (ctypes.c_char_p, [c_int]),
     "tde_set_conv_math": (c_int, [c_int]),
-    "tde_set_conv_ring": (c_int, [c_int]),
-    "tde_get_conv_ring": (c_int, []),
     "tde_get_conv_math": (c_int, []),
     "tde_conv_span_arm": (c_int, [P, P]),
     "tde_stamp": (c_int, [P, P]),

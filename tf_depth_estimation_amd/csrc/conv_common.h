@@ -54,44 +54,7 @@ struct ConvArgs {
   // MODE_PSW: the dy window (T x T from -PW) and its division
   int ps_T, ps_PW;
   FDiv fpsT;
-  // ring tiles (conv_ring.hip): the pre-split fp16 hi / lo B-operand image [class][k-tile][column tile][2][BN][32]
-  // (ring_wprep) and its k-tile / column-tile counts
-  const unsigned short* wimg;
-  int img_nkt, img_ncolt;
 };
-
-// ---- LDS-DMA ring tiles (conv_ring.hip): FWD / DGRAD / PS on fp16x3 with the weights pre-split in HBM
-constexpr int RING_BK = 32;
-// 16-byte slot swizzles, conflict-free for gfx950's ds_read_b128 lane groups (brute-forced over linear XOR maps):
-// A image [BM][32] fp32 (128-byte rows): logical 4-k chunk j of row r sits in slot j ^ ring_fa(r);
-// B image [BN][32] fp16 per plane (64-byte rows): logical 8-k chunk q of row r in slot q ^ ring_fb(r)
-__host__ __device__ inline int ring_fa(int r) { return ((r & 2) << 1) | ((r & 4) >> 1); }
-__host__ __device__ inline int ring_fb(int r) { return (r & 4) >> 1; }
-
-// Ring tile plan of one GEMM (host): rows / columns per tile, image geometry.
-struct RingGeom {
-  int mode, bm, bn, ncls, nkt, ncolt;
-  size_t image_bytes() const { return (size_t)ncls * nkt * ncolt * bn * RING_BK * 4; }
-};
-// B-operand image job (tde_conv2d_split_weights / the ring path's own split): one layer's weights -> its image
-struct RingJob {
-  const float* w;
-  unsigned short* out;
-  const float* wmax;
-  long total;             // u16 elements of the image
-  int block0, nblocks;    // the job's blocks in a batched launch
-  int mode, C, K, KH, KW, S, PT, PL, wcin, Kd, Nn, ncls, nkt, ncolt, bn, ps_C, ps_K;
-  long wn;                // floats of w (the buffer-load range: reads past it are zeros)
-  FDiv fC, fK, fpsC;      // divisions of the index decode
-};
-constexpr int RING_MAXJ = 20;
-struct RingJobs {
-  int njobs;
-  RingJob j[RING_MAXJ];
-};
-void ring_wprep_launch(const RingJobs& jobs, int blocks, hipStream_t st);
-// one ring GEMM launch (grid = row tiles x column tiles x splits * classes)
-void ring_launch(int mode, int bm, int bn, dim3 grid, const ConvArgs& a, hipStream_t st);
 
 // The folded-BN epilogue: TF's Relu keeps NaN (same test as bn_apply_kernel).
 __device__ __forceinline__ float bias_act(float v, const float* bias, int col, int relu) {

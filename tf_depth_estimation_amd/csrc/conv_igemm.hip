@@ -1224,139 +1224,18 @@ static bool ps_ok(const tde_conv_desc_t& d, int* bm = nullptr, int* bn = nullptr
 static bool psw_ok(const tde_conv_desc_t& d);
 static Plan psw_plan(const tde_conv_desc_t& d);
 
-// ---- LDS-DMA ring tiles (conv_ring.hip) for the fp16x3 GEMMs that take neither the halo nor the skinny path, by
-// the role of the call (TDE_RING / tde_set_conv_ring: a mask of RING_FWD = the forward calls tde_conv2d_fwd* /
-// tde_deconv2d_fwd*, RING_DATA = the data-gradient calls (tde_*_bwd_data, the data half of tde_*_bwd), RING_FILTER =
-// the filter-gradient GEMMs, RING_DEEP = the forward calls whose GEMM the planner gives 64-row tiles: the deep
-// levels).  Measured on config 4 (profiles/r05/ring_ab.md), the ring tiles win the deep forward GEMMs (icnv5 / icnv6
-// -25 %) but lose the backward ones, whose two GEMMs the register-staged tiles run as ONE fused launch (igemm_bwd2)
-// that fills the chip where neither alone does, and the per-step B images cost 4 bytes per weight of prep (384 MB
-// for every forward GEMM of the two networks, ~190 us): 1066 pairs/s with every forward call on the ring vs 1079
-// without, 994 with every GEMM on it, 1076-1078 with the deep forward calls only (their layers hold nearly all the
-// weights, so the prep stays) vs 1085-1092 without.  Default 0: opt-in.
-enum { RING_FWD = 1, RING_DATA = 2, RING_FILTER = 4, RING_ALL = 7, RING_DEEP = 8 };
-static long g_ring = env_long("TDE_RING", 0);
-
-// Plan + B-image geometry of the ring GEMM of d in `mode` (MODE_FWD / MODE_DGRAD / MODE_PS / MODE_WGRAD) for a call
-// of `role` (RING_ALL: any call -- the workspace queries); false: not on the ring.  The column tile follows
-// make_plan's rule over the ring widths {32, 64, 96, 128}; make_plan picks rows and splits.
-static bool ring_plan(const tde_conv_desc_t& d, int mode, Plan& pl, RingGeom& rg, int role) {
-  if (g_conv_math != 4) return false;
-  const bool full = (g_ring & role & RING_ALL) != 0;
-  const bool deep = !full && (g_ring & RING_DEEP) && (role & RING_FWD);   // 64-row forward tiles only
-  if (!full && !deep) return false;
-  if (mode == MODE_WGRAD) {
-    // the filter gradient of every layer the halo-tiled WGRAD does not take; no B image (both operands activations)
-    HwgPlan wp;
-    if (!(g_ring & role & RING_FILTER) || hwg_plan(d, wp, g_conv_math)) return false;
-    long M, Nn, Kd;
-    int ncls;
-    gemm_dims(d, mode, M, Nn, Kd, ncls);
-    static const int wc[] = {32, 64, 96, 128};
-    int bn = 0;
-    long best = -1;
-    for (int b : wc) {
-      const long t = tde_cdiv(Nn, b), cost = t * b + 24 * t;
-      if (best < 0 || cost < best || (cost == best && b > bn)) { best = cost; bn = b; }
-    }
-    pl = make_plan(d, mode, 0, bn);
-    rg = RingGeom{mode, pl.bm, bn, 1, 0, 0};
-    return true;
-  }
-  if (mode == MODE_PS) {
-    int bm = 0, bn = 0;
-    // (the ring's B-image prep gathers the 3x3 form only: larger kernels take the register-staged PS tile)
-    if (d.KH != 3 || !ps_ok(d, &bm, &bn)) return false;
-    const long M = (long)d.N * d.OH * d.OW;
-    const int Nn = 4 * d.C;
-    pl = Plan{};
-    pl.bm = bm; pl.bn = bn; pl.splits = 1; pl.kt_per = tde_cdiv(4L * d.K, BK3);
-    pl.gx = tde_cdiv(M, bm); pl.gy = Nn / bn; pl.gz = 1;
-    pl.rows = (int)((long)d.N * d.H * d.W); pl.cols = d.C;
-    if (deep && bm != 64) return false;
-    rg = RingGeom{MODE_PS, bm, bn, 1, tde_cdiv(4L * d.K, BK3), Nn / bn};
-    return true;
-  }
-  if (mode != MODE_FWD && mode != MODE_DGRAD) return false;
-  HaloPlan hp;
-  if (halo_plan(d, mode == MODE_FWD ? 0 : 1, g_conv_math, hp)) return false;
-  if (mode == MODE_DGRAD && ps_ok(d)) return false;      // its GEMM is MODE_PS
-  long M, Nn, Kd;
-  int ncls;
-  gemm_dims(d, mode, M, Nn, Kd, ncls);
-  static const int cands[] = {32, 64, 96, 128};
-  int bn = 0;
-  long best = -1;
-  for (int b : cands) {
-    const long t = tde_cdiv(Nn, b), cost = t * b + 24 * t;
-    if (best < 0 || cost < best || (cost == best && b > bn)) { best = cost; bn = b; }
-  }
-  pl = make_plan(d, mode, 0, bn);
-  if (pl.skinny_tm > 0) return false;
-  // the narrow GEMMs whose column tile would be 16 or 48 in the register-staged planner (16-channel outputs: a 32-wide
-  // ring tile computes twice the columns) stay there
-  if (make_plan(d, mode).bn % 32 != 0) return false;
-  if (deep && pl.bm != 64) return false;
-  rg = RingGeom{mode, pl.bm, bn, ncls, tde_cdiv(Kd, BK3), tde_cdiv(Nn, bn)};
-  return true;
-}
-
-// The pre-split B image job of d's ring GEMM (weights w; out: rg.image_bytes(), 16-byte aligned).
-static RingJob ring_job(const tde_conv_desc_t& d, const RingGeom& rg, const float* w, void* out) {
-  RingJob J{};
-  J.w = w; J.out = static_cast<unsigned short*>(out); J.wmax = d.w_absmax;
-  J.total = (long)(rg.image_bytes() / 2);
-  J.mode = rg.mode;
-  J.KH = d.KH; J.KW = d.KW; J.S = d.stride; J.PT = d.pad_top; J.PL = d.pad_left; J.wcin = d.w_cin;
-  J.ncls = rg.ncls; J.nkt = rg.nkt; J.ncolt = rg.ncolt; J.bn = rg.bn;
-  if (rg.mode == MODE_FWD) {
-    J.C = d.C; J.K = d.K; J.Kd = d.KH * d.KW * d.C; J.Nn = d.K;
-  } else if (rg.mode == MODE_DGRAD) {
-    J.C = d.C; J.K = d.K; J.Nn = d.C;
-  } else {   // MODE_PS: the 2x2 stride-1 virtual conv over the deconv input (K channels) into 4 x C columns
-    J.C = d.K; J.K = 4 * d.C; J.Kd = 4 * d.K; J.Nn = 4 * d.C; J.ps_C = d.C; J.ps_K = d.K;
-  }
-  J.wn = rg.mode == MODE_PS ? 9L * d.C * d.K : (long)d.KH * d.KW * d.w_cin * d.K;
-  J.fC = make_fdiv(J.C); J.fK = make_fdiv(J.K); J.fpsC = make_fdiv(J.ps_C > 0 ? J.ps_C : 1);
-  return J;
-}
-
-// Prep launches for a list of jobs (RING_MAXJ per launch; a block per B tile, <= 2048 blocks per job).
-static void ring_prep(const std::vector<RingJob>& jobs, hipStream_t st) {
-  for (size_t i0 = 0; i0 < jobs.size(); i0 += RING_MAXJ) {
-    RingJobs B{};
-    int blocks = 0;
-    for (size_t i = i0; i < jobs.size() && i < i0 + RING_MAXJ; ++i) {
-      RingJob J = jobs[i];
-      J.nblocks = std::min(2048, std::max(1, J.ncls * J.nkt * J.ncolt));   // one B tile per block
-      J.block0 = blocks;
-      blocks += J.nblocks;
-      B.j[B.njobs++] = J;
-    }
-    ring_wprep_launch(B, blocks, st);
-  }
-}
-
 static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
-  // the register-staged plan, or the ring plan (+ the B image when the caller passes no pre-split weights: the call
-  // splits them itself) of any call role
   const Plan pl = make_plan(d, mode);
-  size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
-  Plan pr;
-  RingGeom rg;
-  if (ring_plan(d, mode, pr, rg, RING_ALL))
-    igemm = std::max(igemm, pr.ws_bytes + (bn ? bn_plan(d, mode, pr).part_bytes : 0) + rg.image_bytes());
+  const size_t igemm = pl.ws_bytes + (bn ? bn_plan(d, mode, pl).part_bytes : 0);
   const size_t halo = halo_ws_bytes(d, mode, bn);
   size_t b = igemm > halo ? igemm : halo;
   int pbm = 0, pbn = 0;
   if (mode == MODE_DGRAD && ps_ok(d, &pbm, &pbn)) {
-    // pixel-shuffle path: one partial record [2][C] per (row tile, column tile) (+ its ring image)
-    size_t pb = bn ? std::max((size_t)tde_cdiv((long)d.N * d.OH * d.OW, pbm) * (4 * d.C / pbn) * 2 * d.C * sizeof(double),
-                              bn_part_bytes((long)d.N * d.H * d.W, d.C))
-                   : 0;
-    Plan pp;
-    RingGeom rp;
-    if (ring_plan(d, MODE_PS, pp, rp, RING_ALL)) pb += rp.image_bytes();
+    // pixel-shuffle path: one partial record [2][C] per (row tile, column tile)
+    const size_t pb = bn ? std::max((size_t)tde_cdiv((long)d.N * d.OH * d.OW, pbm) * (4 * d.C / pbn) * 2 * d.C *
+                                        sizeof(double),
+                                    bn_part_bytes((long)d.N * d.H * d.W, d.C))
+                         : 0;
     if (pb > b) b = pb;
   }
   if (mode == MODE_WGRAD && hwg_ws_bytes(d) > b) b = hwg_ws_bytes(d);
@@ -1614,21 +1493,8 @@ static ConvArgs ps_args(const tde_conv_desc_t* d, const ConvArgs& a0, int accumu
   return a;
 }
 
-// One pixel-shuffle GEMM launch: the ring tile (B image from d->w_split[1], else split into `img_ws`) or the
-// register-staged tile.
-static void launch_ps(const tde_conv_desc_t* d, ConvArgs& a, int BM, int BN, dim3 grid, const Plan* rpl,
-                      const RingGeom* rg, void* img_ws, hipStream_t st) {
-  if (rpl != nullptr) {
-    const void* img = d->w_split[1];
-    if (img == nullptr) {
-      ring_prep({ring_job(*d, *rg, a.w, img_ws)}, st);
-      img = img_ws;
-    }
-    a.wimg = static_cast<const unsigned short*>(img);
-    a.img_nkt = rg->nkt; a.img_ncolt = rg->ncolt;
-    ring_launch(MODE_PS, BM, BN, grid, a, st);
-    return;
-  }
+// One pixel-shuffle GEMM launch (register-staged tile).
+static void launch_ps(ConvArgs& a, int BM, int BN, dim3 grid, hipStream_t st) {
   if (BM == 128 && BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else if (BM == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 128, 64, 2, 2, 1>), grid, dim3(NT), 0, st, a);
   else if (BN == 128) hipLaunchKernelGGL((igemmx_kernel<4, MODE_PS, 64, 128, 2, 2, 1>), grid, dim3(NT), 0, st, a);
@@ -1636,7 +1502,7 @@ static void launch_ps(const tde_conv_desc_t* d, ConvArgs& a, int BM, int BN, dim
 }
 
 static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, const tde_bn_train_t* bn, void* ws,
-                  size_t ws_bytes, void* stream, int role) {
+                  size_t ws_bytes, void* stream) {
   ConvArgs a = ps_args(d, a0, accumulate);
   const long M = (long)d->N * d->OH * d->OW, rows = (long)d->N * d->H * d->W;
   const int Nn = 4 * d->C;
@@ -1645,16 +1511,12 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
   int BM = 0, BN = 0;
   ps_ok(*d, &BM, &BN);
   const dim3 grid(tde_cdiv(M, BM), Nn / BN, 1);
-  Plan rpl;
-  RingGeom rg;
-  const bool ring = ring_plan(*d, MODE_PS, rpl, rg, role);
   // BN statistics from the epilogue (one record per (row tile, column tile)) when every row group is whole row tiles
   // and a tile covers whole classes; else a grouped partial pass over z
   const bool epi = bn && rows / G > BN_SMALL_M && (M % G == 0) && ((M / G) % BM == 0) && BN % d->C == 0;
   const size_t epi_bytes = (size_t)grid.x * grid.y * 2 * d->C * sizeof(double);
   const size_t part_bytes = bn ? std::max(bn_part_bytes(rows, d->C), epi ? epi_bytes : (size_t)0) : 0;
-  const size_t img_bytes = ring && d->w_split[1] == nullptr ? rg.image_bytes() : 0;
-  if ((bn || img_bytes) && (!ws || !tde_aligned16(ws) || part_bytes + img_bytes > ws_bytes)) return TDE_ERR_WORKSPACE;
+  if (bn && (!ws || !tde_aligned16(ws) || part_bytes > ws_bytes)) return TDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
   double* part = bn ? reinterpret_cast<double*>(tde_ws_body(ws)) : nullptr;
   if (epi) {
@@ -1662,8 +1524,7 @@ static int run_ps(const tde_conv_desc_t* d, const ConvArgs& a0, int accumulate, 
     a.bn_gy = (int)grid.y;
   }
   span_mark(0, st);
-  launch_ps(d, a, BM, BN, grid, ring ? &rpl : nullptr, ring ? &rg : nullptr,
-            img_bytes ? tde_ws_body(ws) + part_bytes : nullptr, st);
+  launch_ps(a, BM, BN, grid, st);
   span_mark(1, st);
   if (bn) {
     BnOut o{bn->beta, bn->eps, bn->decay, bn->bessel, bn->moving_mean, bn->moving_var, bn->save_mean,
@@ -1733,9 +1594,9 @@ static void launch_psw_reduce(const Plan& pl, const ConvArgs& a, hipStream_t st)
 
 template <int MODE>
 static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_bn_train_t* bn, void* ws,
-               size_t ws_bytes, void* stream, int role) {
+               size_t ws_bytes, void* stream) {
   if constexpr (MODE == MODE_DGRAD) {
-    if (ps_ok(*d) && !skip_conv(d)) return run_ps(d, a, accumulate, bn, ws, ws_bytes, stream, role);
+    if (ps_ok(*d) && !skip_conv(d)) return run_ps(d, a, accumulate, bn, ws, ws_bytes, stream);
   }
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
@@ -1788,18 +1649,12 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     }
     return tde_launch_status();
   }
-  Plan pl;
-  RingGeom rg;
-  const bool ring = ring_plan(*d, MODE, pl, rg, role);
-  if (!ring) pl = make_plan(*d, MODE);
+  const Plan pl = make_plan(*d, MODE);
   BnPlan bp{};
   const int G = bn && bn->groups > 1 ? bn->groups : 1;
   if (pl.rows % G != 0) return TDE_ERR_ARG;
   if (bn) bp = bn_plan(*d, MODE, pl, G);
-  const bool need_img = ring && MODE != MODE_WGRAD;   // (the ring WGRAD reads two activations: no B image)
-  const void* img = need_img ? d->w_split[MODE == MODE_FWD ? 0 : 1] : nullptr;
-  const size_t img_bytes = need_img && img == nullptr ? rg.image_bytes() : 0;
-  if (pl.ws_bytes + bp.part_bytes + img_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  if (pl.ws_bytes + bp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   double* part = reinterpret_cast<double*>(body + pl.slab_bytes);
   a.ws = reinterpret_cast<float*>(body);
@@ -1811,17 +1666,7 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   a.bn_G = G;
   hipStream_t st = static_cast<hipStream_t>(stream);
   span_mark(0, st);
-  if (ring && !skip) {
-    if (need_img && img == nullptr) {
-      img = body + pl.slab_bytes + bp.part_bytes;
-      ring_prep({ring_job(*d, rg, a.w, const_cast<void*>(img))}, st);
-    }
-    a.wimg = static_cast<const unsigned short*>(img);
-    a.img_nkt = rg.nkt; a.img_ncolt = rg.ncolt;
-    ring_launch(MODE, pl.bm, pl.bn, dim3(pl.gx, pl.gy, pl.gz), a, st);
-  } else if (!skip) {
-    launch_mode<MODE>(pl, a, st);
-  }
+  if (!skip) launch_mode<MODE>(pl, a, st);
   float* z = MODE == MODE_FWD ? a.y : (MODE == MODE_DGRAD ? a.dx : a.dw);
   if (!skipr && !(bn && bp.path == BN_REDUCE)) launch_reduce<MODE>(pl, a, st);
   if (bn && bp.path == BN_REDUCE && !skipr)
@@ -1878,18 +1723,6 @@ static void launch_bwd2(const Plan& p1, const ConvArgs& a1, const Plan& p2, cons
 static const long g_bwd_fuse = env_long("TDE_BWD_FUSE", 1);   // 0: two launches (A/B experiments)
 
 
-// The filter-gradient GEMM of run_bwd: its plan (the ring WGRAD where it applies, else the register-staged tile;
-// fix_bm / fix_bn: the fused launch's shared tile) and the launch.
-static Plan wgrad_plan(const tde_conv_desc_t& d, bool& ring, int fix_bm = 0, int fix_bn = 0) {
-  Plan pl;
-  RingGeom rg;
-  ring = !fix_bm && ring_plan(d, MODE_WGRAD, pl, rg, RING_FILTER);
-  return ring ? pl : make_plan(d, MODE_WGRAD, fix_bm, fix_bn);
-}
-static void launch_wgrad(const Plan& p2, bool ring, const ConvArgs& a2, hipStream_t st) {
-  if (ring) ring_launch(MODE_WGRAD, p2.bm, p2.bn, dim3(p2.gx, p2.gy, p2.gz), a2, st);
-  else launch_mode<MODE_WGRAD>(p2, a2, st);
-}
 
 // Data + filter gradient of one layer.  MODE1 = the data-gradient GEMM of the virtual conv (DGRAD for a
 // conv, FWD for a deconv); the filter gradient is always its WGRAD.  One fused launch when the data
@@ -1922,8 +1755,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   }
   if (MODE1 == MODE_DGRAD && halo_plan(*d, 1, g_conv_math, hp)) {
     // data gradient on the halo path, filter gradient on the implicit GEMM (two launches + its reduce)
-    bool r2;
-    const Plan p2 = wgrad_plan(*d, r2);
+    const Plan p2 = make_plan(*d, MODE_WGRAD);
     if (hp.wbytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
     char* body = tde_ws_body(ws);
     a2.ws = reinterpret_cast<float*>(body + hp.wbytes);
@@ -1931,44 +1763,31 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (!skip) {
       halo_launch(hp, *d, a1.dy, a1.w, a1.dx, acc1, body, nullptr, st);
-      if (!g_skip_wgrad) launch_wgrad(p2, r2, a2, st);
+      if (!g_skip_wgrad) launch_mode<MODE_WGRAD>(p2, a2, st);
     }
     if (!skipr && !g_skip_wgrad) launch_reduce<MODE_WGRAD>(p2, a2, st);
     return tde_launch_status();
   }
-  // the data gradient on the ring tiles where they apply (a 3x3 stride-2 conv's as the pixel-shuffle GEMM), then the
-  // filter gradient as its own launch; else the fused data + filter gradient launch
-  Plan p1;
-  RingGeom rg1;
-  int m1 = MODE1;
-  bool ring1 = ring_plan(*d, MODE1, p1, rg1, RING_DATA);
-  if (!ring1 && MODE1 == MODE_DGRAD && ring_plan(*d, MODE_PS, p1, rg1, RING_DATA)) {
-    ring1 = true;
-    m1 = MODE_PS;
-  }
   // a stride-2 conv whose data gradient fits the pixel-shuffle GEMM (ps_ok: the high-resolution 3x3 / 5x5 / 7x7 layers)
-  // runs it off the ring too: one 4 x C-wide launch without split-K, then the filter gradient as its own launch
-  // (config 4, cnv2's 5x5: 1090 -> 1092-1095 pairs/s against the fused class-GEMM launch, profiles/r05/ps_ab.md)
+  // runs it as one 4 x C-wide launch without split-K, then the filter gradient as its own launch (config 4, cnv2's
+  // 5x5: 1090 -> 1092-1095 pairs/s against the fused class-GEMM launch, profiles/r05/ps_ab.md); else the fused data +
+  // filter gradient launch
+  Plan p1;
   int pbm = 0, pbn = 0;
-  const bool ps1 = !ring1 && MODE1 == MODE_DGRAD && ps_ok(*d, &pbm, &pbn);
+  const bool ps1 = MODE1 == MODE_DGRAD && ps_ok(*d, &pbm, &pbn);
   if (ps1) {
     p1 = Plan{};
     p1.bm = pbm; p1.bn = pbn; p1.splits = 1; p1.gz = 1;
     p1.gx = (int)tde_cdiv((long)d->N * d->OH * d->OW, pbm); p1.gy = 4 * d->C / pbn;
-  } else if (!ring1) {
+  } else {
     p1 = make_plan(*d, MODE1);
   }
-  bool r2 = false;
-  const Plan p2w = wgrad_plan(*d, r2);
   // the filter gradient of a stride-2 layer in the pixel-shuffle form (MODE_PSW) where it applies
-  const bool psw2 = !r2 && !g_skip_wgrad && psw_ok(*d);
-  // fused data + filter gradient launch only when neither GEMM is on the ring tiles or a pixel-shuffle GEMM
-  const bool fuse = !ring1 && !ps1 && !psw2 && !r2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 &&
-                    !g_skip_wgrad;
-  const Plan p2 = psw2 ? psw_plan(*d) : (fuse ? make_plan(*d, MODE_WGRAD, p1.bm, p1.bn) : p2w);
-  const void* img = ring1 ? d->w_split[MODE1 == MODE_FWD ? 0 : 1] : nullptr;
-  const size_t img_bytes = ring1 && img == nullptr ? rg1.image_bytes() : 0;
-  if (p1.slab_bytes + p2.slab_bytes + img_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  const bool psw2 = !g_skip_wgrad && psw_ok(*d);
+  // fused data + filter gradient launch only when neither GEMM is a pixel-shuffle GEMM
+  const bool fuse = !ps1 && !psw2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
+  const Plan p2 = psw2 ? psw_plan(*d) : make_plan(*d, MODE_WGRAD, fuse ? p1.bm : 0, fuse ? p1.bn : 0);
+  if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   a1.ws = reinterpret_cast<float*>(body);
   a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
@@ -1979,28 +1798,12 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   auto wgrad = [&] {
     if (g_skip_wgrad) return;
     if (psw2) launch_psw(p2, a2p, st);
-    else launch_wgrad(p2, r2, a2, st);
+    else launch_mode<MODE_WGRAD>(p2, a2, st);
   };
   if (skip) {
-  } else if (ring1) {
-    if (img == nullptr) {
-      img = body + p1.slab_bytes + p2.slab_bytes;
-      ring_prep({ring_job(*d, rg1, a1.w, const_cast<void*>(img))}, st);
-    }
-    if (m1 == MODE_PS) {
-      ConvArgs ap = ps_args(d, a1, acc1);
-      ap.wimg = static_cast<const unsigned short*>(img);
-      ap.img_nkt = rg1.nkt; ap.img_ncolt = rg1.ncolt;
-      ring_launch(MODE_PS, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), ap, st);
-    } else {
-      a1.wimg = static_cast<const unsigned short*>(img);
-      a1.img_nkt = rg1.nkt; a1.img_ncolt = rg1.ncolt;
-      ring_launch(MODE1, p1.bm, p1.bn, dim3(p1.gx, p1.gy, p1.gz), a1, st);
-    }
-    wgrad();
   } else if (ps1) {
     ConvArgs ap = ps_args(d, a1, acc1);
-    launch_ps(d, ap, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), nullptr, nullptr, nullptr, st);
+    launch_ps(ap, p1.bm, p1.bn, dim3(p1.gx, p1.gy, 1), st);
     wgrad();
   } else if (fuse) {
     launch_bwd2<MODE1>(p1, a1, p2, a2, st);
@@ -2022,27 +1825,17 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
   const size_t split = p1.slab_bytes + make_plan(d, MODE_WGRAD).slab_bytes;
   size_t b = fused > split ? fused : split;
   {
-    // the ring data gradient: its slab + the filter gradient's + the B image (no pre-split weights)
-    Plan pr{};
-    RingGeom rg{};
-    bool r2;
-    const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
-    if (ring_plan(d, mode1, pr, rg, RING_ALL) || (mode1 == MODE_DGRAD && ring_plan(d, MODE_PS, pr, rg, RING_ALL))) {
-      const size_t r = pr.slab_bytes + w2 + rg.image_bytes();
-      if (r > b) b = r;
-    }
+    const size_t w2 = make_plan(d, MODE_WGRAD).slab_bytes;
     if (p1.slab_bytes + w2 > b) b = p1.slab_bytes + w2;
     if (psw_ok(d)) {
       // the pixel-shuffle filter gradient beside any data gradient above
-      const size_t pw = psw_plan(d).slab_bytes;
-      const size_t r = std::max(p1.slab_bytes, pr.slab_bytes + rg.image_bytes()) + pw;
+      const size_t r = p1.slab_bytes + psw_plan(d).slab_bytes;
       if (r > b) b = r;
     }
   }
   if (mode1 == MODE_DGRAD) {
     const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
-    bool r2;
-    const size_t w2 = std::max(wgrad_plan(d, r2).slab_bytes, make_plan(d, MODE_WGRAD).slab_bytes);
+    const size_t w2 = make_plan(d, MODE_WGRAD).slab_bytes;
     if (h && h + w2 > b) b = h + w2;
     const size_t hw = hwg_ws_bytes(d);
     if (hw) {
@@ -2126,31 +1919,10 @@ int tde_set_conv_math(int mode) {
 
 int tde_get_conv_math(void) { return g_conv_math; }
 
-int tde_set_conv_ring(int roles) {
-  if (roles < 0 || roles > (RING_ALL | RING_DEEP)) return -1;
-  const int prev = (int)g_ring;
-  g_ring = roles;
-  return prev;
-}
-
-int tde_get_conv_ring(void) { return (int)g_ring; }
-
-// The ring GEMM behind split image op & 1 of d (0: the FWD GEMM, 1: the DGRAD GEMM -- the pixel-shuffle GEMM where
-// ps_ok holds), if the call that reads it runs on the ring: op & 2 marks d as a deconv's virtual conv, whose forward
-// call reads image 1 and data-gradient calls image 0 (a conv: the other way round).
-static bool ring_for_op(const tde_conv_desc_t& d, int op, Plan& pl, RingGeom& rg) {
-  const int role = ((op & 1) == ((op >> 1) & 1)) ? RING_FWD : RING_DATA;
-  if ((op & 1) == 0) return ring_plan(d, MODE_FWD, pl, rg, role);
-  return ring_plan(d, MODE_DGRAD, pl, rg, role) || ring_plan(d, MODE_PS, pl, rg, role);
-}
-
 size_t tde_conv2d_split_weights_size(const tde_conv_desc_t* d, int op) {
   if (!desc_ok(d) || op < 0 || op > 3) return 0;
   HaloPlan hp;
   if (halo_plan(*d, op & 1, g_conv_math, hp)) return hp.wbytes;
-  Plan pl;
-  RingGeom rg;
-  if (ring_for_op(*d, op, pl, rg)) return rg.image_bytes();
   return 0;
 }
 
@@ -2158,28 +1930,22 @@ int tde_conv2d_split_weights(int n, const tde_conv_desc_t* const* descs, const i
                              void* const* outs, void* stream) {
   tde_clear_error();
   TDE_CHECK_ARG(n >= 0 && (n == 0 || (descs && ops && weights && outs)));
-  // halo-path images (halo_wprep_batch) and ring B images (ring_prep), one batched launch per kind
+  // halo-path images (halo_wprep_batch), one batched launch
   std::vector<HaloPlan> hps;
   std::vector<const tde_conv_desc_t*> hd;
   std::vector<const float*> hw;
   std::vector<void*> ho;
-  std::vector<RingJob> rj;
   for (int i = 0; i < n; ++i) {
     TDE_CHECK_ARG(desc_ok(descs[i]) && ops[i] >= 0 && ops[i] <= 3 && weights[i] && outs[i] && tde_aligned16(outs[i]));
     HaloPlan hp;
-    Plan pl;
-    RingGeom rg;
     if (halo_plan(*descs[i], ops[i] & 1, g_conv_math, hp)) {
       hps.push_back(hp); hd.push_back(descs[i]); hw.push_back(weights[i]); ho.push_back(outs[i]);
-    } else if (ring_for_op(*descs[i], ops[i], pl, rg)) {
-      rj.push_back(ring_job(*descs[i], rg, weights[i], outs[i]));
     } else {
       return TDE_ERR_ARG;   // a layer / op that takes no split (tde_conv2d_split_weights_size == 0): the caller's error
     }
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!hps.empty()) halo_wprep_batch((int)hps.size(), hps.data(), hd.data(), hw.data(), ho.data(), st);
-  if (!rj.empty()) ring_prep(rj, st);
   return tde_launch_status();
 }
 
@@ -2203,7 +1969,7 @@ int tde_conv2d_fwd(const tde_conv_desc_t* d, const float* x, const float* w, flo
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y;
-  return run<MODE_FWD>(d, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_FWD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, float* z, const tde_bn_train_t* bn,
@@ -2213,7 +1979,7 @@ int tde_conv2d_fwd_bn(const tde_conv_desc_t* d, const float* x, const float* w, 
   TDE_CHECK_ARG(d->y_cstride == d->K && d->y_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = z;
-  return run<MODE_FWD>(d, a, 0, bn, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_FWD>(d, a, 0, bn, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* w, float* dx, int accumulate,
@@ -2225,7 +1991,7 @@ int tde_conv2d_bwd_data(const tde_conv_desc_t* d, const float* dy, const float* 
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.dy = dy; a.w = w; a.dx = dx;
-  return run<MODE_DGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_DATA);
+  return run<MODE_DGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float* dy, float* dw, int accumulate,
@@ -2237,7 +2003,7 @@ int tde_conv2d_bwd_filter(const tde_conv_desc_t* d, const float* x, const float*
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.x = x; a.dy = dy; a.dw = dw;
-  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FILTER);
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float* w, float* y_big,
@@ -2247,7 +2013,7 @@ int tde_deconv2d_fwd(const tde_conv_desc_t* d, const float* x_small, const float
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x_small) && tde_aligned16(w) && tde_aligned16(y_big));
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = y_big;
-  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_DGRAD>(d, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 // Folded-BN inference conv: y = relu?(conv(x, w_folded) + bias) into the y view of d.
@@ -2257,7 +2023,7 @@ int tde_conv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x, const floa
   TDE_CHECK_ARG(desc_ok(d) && tde_aligned16(x) && tde_aligned16(w) && tde_aligned16(y) && (relu == 0 || relu == 1));
   ConvArgs a = make_args(*d);
   a.x = x; a.w = w; a.y = y; a.bias = bias; a.relu = relu;
-  return run<MODE_FWD>(d, a, 0, nullptr, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_FWD>(d, a, 0, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, const float* w, const float* bias,
@@ -2267,7 +2033,7 @@ int tde_deconv2d_fwd_bias_act(const tde_conv_desc_t* d, const float* x_small, co
                 (relu == 0 || relu == 1) && d->w_cin == d->C);
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = y_big; a.bias = bias; a.relu = relu;
-  return run<MODE_DGRAD>(d, a, 0, nullptr, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_DGRAD>(d, a, 0, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const float* w, float* z_big,
@@ -2277,7 +2043,7 @@ int tde_deconv2d_fwd_bn(const tde_conv_desc_t* d, const float* x_small, const fl
   TDE_CHECK_ARG(d->x_cstride == d->C && d->x_coff == 0);   // z is the dense pre-BN output
   ConvArgs a = make_args(*d);
   a.dy = x_small; a.w = w; a.dx = z_big;
-  return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream, RING_FWD);
+  return run<MODE_DGRAD>(d, a, 0, bn, ws, ws_bytes, stream);
 }
 
 size_t tde_conv2d_bwd_workspace_size(const tde_conv_desc_t* d) {
@@ -2332,7 +2098,7 @@ int tde_deconv2d_bwd_data(const tde_conv_desc_t* d, const float* dy_big, const f
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);   // the virtual conv's forward, in a data-gradient role
   a.x = dy_big; a.w = w; a.y = dx_small;
-  return run<MODE_FWD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_DATA);
+  return run<MODE_FWD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const float* x_small, float* dw,
@@ -2344,7 +2110,7 @@ int tde_deconv2d_bwd_filter(const tde_conv_desc_t* d, const float* dy_big, const
   if (rc != TDE_OK) return rc;
   ConvArgs a = make_args(db);
   a.x = dy_big; a.dy = x_small; a.dw = dw;
-  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream, RING_FILTER);
+  return run<MODE_WGRAD>(&db, a, accumulate, nullptr, ws, ws_bytes, stream);
 }
 
 int tde_stamp(unsigned long long* slot, void* stream) {

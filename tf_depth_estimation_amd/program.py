@@ -331,7 +331,7 @@ class NetProgram:
         """The convs whose forward or data-gradient call takes the halo-tiled path (their weights are kept as
         split MFMA tiles, tde_conv2d_split_weights): [(op index, op, desc, buffer)], cached per (N, conv math)."""
         lib = _lib.load()
-        key = (N, lib.tde_get_conv_math(), lib.tde_get_conv_ring())
+        key = (N, lib.tde_get_conv_math())
         plan = self._wsplit.get(key)
         if plan is None:
             plan = []
@@ -379,7 +379,7 @@ class NetProgram:
 
     def _use_split(self, d, i, N):
         cur = getattr(self, "_cur_split", None)
-        if cur is not None and cur[0] == (N, _lib.load().tde_get_conv_math(), _lib.load().tde_get_conv_ring()):
+        if cur is not None and cur[0] == (N, _lib.load().tde_get_conv_math()):
             sp = cur[1].get(i)
             if sp is not None:
                 d.w_split[0], d.w_split[1] = sp[0], sp[1]
