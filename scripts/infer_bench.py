@@ -56,8 +56,37 @@ def main():
                          "ms_per_call": round(s * 1e3, 4), "images_per_s": round(B / s, 1),
                          "conv_tflops": round(f / s / 1e12, 2)})
             print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    # the whole loop body of batch_prediction.py:58-75 on the GPU: INTER_AREA of a decoded 480x640 uint8 image into
+    # the 224x224 input, the folded-BN graph, INTER_CUBIC of disp1 to 240x720 and bilateralFilter(9, 75, 75); and
+    # each OpenCV step alone (HIP events on the current stream)
+    variables.get_store().reset(seed=1)
+    _api.clear_programs()
+    pred = batch_prediction.Predictor("disp_net", 224, 224, batch=1)
+    img = torch.randint(0, 256, (1, 480, 640, 3), dtype=torch.uint8, device="cuda")
+    s = timed(lambda x: pred.predict_depth_map(x, out_hw=(240, 720)), img, args.iters, args.warmup)
+    post = {"chain_ms_per_image": round(s * 1e3, 4), "input": "480x640 uint8 -> 224x224 -> z 240x720"}
+    d1 = pred.outs[0]
+    z = batch_prediction.resize_cubic(d1, 240, 720)
+    for name, fn, nbytes in (
+            ("resize_area_u8 480x640x3 -> 224x224 (float view)",
+             lambda: batch_prediction.resize_area(img, 224, 224, out_f32=pred.x), 480 * 640 * 3 + 224 * 224 * 12),
+            ("resize_cubic 224x224 -> 240x720", lambda: batch_prediction.resize_cubic(d1, 240, 720, out=z),
+             224 * 224 * 4 + 240 * 720 * 4),
+            ("bilateral 240x720 d=9", lambda: batch_prediction.bilateral_filter(z, 9, 75.0, 75.0), 2 * 240 * 720 * 4)):
+        for _ in range(args.warmup):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+        post[name] = {"us": round(us, 2), "algorithmic_GBps": round(nbytes / (us * 1e-6) / 1e9, 1)}
+    print(json.dumps(post), file=sys.stderr, flush=True)
     print(json.dumps({"metric": "disp_net inference (batch_prediction.py path)", "math": args.math,
-                      "data": "synthetic U(-0.5,0.5) images, Glorot weights", "rows": rows}))
+                      "data": "synthetic U(-0.5,0.5) images, Glorot weights", "rows": rows,
+                      "predict_depth_map": post}))
 
 
 if __name__ == "__main__":
