@@ -105,8 +105,8 @@ class _TopologySync(ddp.GradSync):
         return _Stream(f"comm{len(self.ops) if self.ops is not None else 0}_{id(self) % 997}")
 
     @staticmethod
-    def _chunk_group(i):
-        return f"group{i}"
+    def _chunk_comm(i, group):
+        return f"{group or 'world'}/comm{i}"
 
     def _current(self):
         return _TopologySync.cur
@@ -173,20 +173,50 @@ def test_graph_mode_forks_one_level_deep(mb):
     for i in waits_comm:                  # the filter-gradient branch was joined right before each fork
         assert ops[i - 1] == ("wait", cap, wgrad), ops[i - 1:i + 1]
     reduces = [(a, g) for k, a, g in ops if k == "allreduce"]
-    assert len(reduces) == len(gs.buckets) and all(a is comm and g == "group0" for a, g in reduces)
+    assert len(reduces) == len(gs.buckets) and all(a is comm and g == "world/comm0" for a, g in reduces)
     assert ops[-1] == ("wait", cap, comm), "the comm branch is not joined back at the end"
     assert all(b.launched for b in gs.buckets)
 
 
-def test_graph_mode_refuses_shared_group_over_chunks():
-    """an explicit communicator under several chunks' comm branches is refused in graph mode."""
+@pytest.mark.parametrize("mode", ["graph", "segments"])
+def test_every_chunk_reduces_on_a_communicator_of_its_own(mode):
+    """one communicator under several chunks' streams would see their collectives in an order no rank
+    controls.  Over RCCL every chunk gets a direct communicator of its own (rccl.pooled_comm by chunk index), with the
+    default group and with an explicit one; segments mode over RCCL issues inline (no comm stream) and leaves the SUM
+    for Adam's 1/world."""
     _, c1 = _chunk()
     _, c2 = _chunk()
     _TopologySync.ops = []
-    with pytest.raises(ValueError):
-        _TopologySync([c1, c2], 2, bucket_mb=1.0, mode="graph", group="explicit")
-    gs = _TopologySync([c1, c2], 2, bucket_mb=1.0, mode="graph")
-    assert gs.group_of[id(c1)] != gs.group_of[id(c2)]
+    for group in (None, "explicit"):
+        gs = _TopologySync([c1, c2], 2, bucket_mb=1.0, mode=mode, group=group)
+        assert gs.group_of[id(c1)] != gs.group_of[id(c2)]
+        assert gs.grad_scale == 0.5 and gs.comm is None
+        assert gs.inline == (mode == "segments")
+
+
+def test_segments_inline_launch_order():
+    """Segments mode over RCCL, eagerly: at each launch point the chunk's filter-gradient branch is joined into the
+    current stream (pre_launch) and the bucket is all-reduced on that same stream, on the chunk's communicator."""
+    import ddp_worker
+    spec, chunk = _chunk()
+    cap, wgrad = _Stream("cap"), _Stream("wgrad")
+    _TopologySync.ops, _TopologySync.cur = [], cap
+    gs = _TopologySync([chunk], 2, bucket_mb=4.0, mode="segments",
+                       pre_launch=lambda c: _TopologySync.ops.append(("wait", _TopologySync.cur, wgrad)))
+    gs.begin_step()
+    hook = gs.hook(chunk)
+    for names in ddp_worker.schedule(spec):
+        hook(names)
+    gs.join(chunk)
+    gs.finish()
+    ops = _TopologySync.ops
+    red = [i for i, o in enumerate(ops) if o[0] == "allreduce"]
+    assert len(red) == len(gs.buckets) and all(ops[i][1] is cap for i in red)
+    for i in red:     # each launch point: join, then its bucket(s) on the same stream
+        j = i
+        while ops[j - 1][0] == "allreduce":
+            j -= 1
+        assert ops[j - 1] == ("wait", cap, wgrad), ops[j - 1:i + 1]
 
 
 def test_adam_reads_grad_scale_from_the_exchange():

@@ -177,7 +177,7 @@ def test_graph_exchange_refused_with_net_overlap_beyond_world1(pg):
         tr.enable_net_overlap()
     tr2 = train.DepthThenCamTrainer(1, 64, 96)
     gs2 = tr2.enable_ddp(2)
-    assert gs2.mode == "segments" and all(o.grad_scale == 1.0 for o in tr2.opt.opts)
+    assert gs2.mode == "segments" and gs2.inline and all(o.grad_scale == 0.5 for o in tr2.opt.opts)
     tr2.enable_net_overlap()
     _api.clear_programs()
 
@@ -235,3 +235,30 @@ def test_sync_bn_captured_config4(pg):
         for a, b in zip(o_loc[k], o_sb1[k]):
             err = ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
             assert err <= 1e-4, (k, err)
+
+
+def test_direct_rccl_communicator(pg):
+    """rccl.Communicator (the exchange's direct RCCL path): a world-1 communicator built through the process group's
+    unique-id broadcast; in-place SUM on a given stream, eagerly and captured in a hipGraph, is the identity at one
+    rank; bad operands are refused on the host."""
+    from tf_depth_estimation_amd import rccl
+    c = rccl.Communicator()
+    assert c.world == 1 and c.rank == 0 and c.comm.value
+    t = torch.randn(1 << 20, device="cuda")
+    ref = t.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    c.all_reduce_sum(t, s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        c.all_reduce_sum(t)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+    with pytest.raises(ValueError):
+        c.all_reduce_sum(t.double())
+    assert rccl.pooled_comm("test", 0) is rccl.pooled_comm("test", 0)

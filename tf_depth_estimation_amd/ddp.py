@@ -11,39 +11,35 @@ op order, so backward finishes them roughly from the end of the buffer toward it
 are contiguous slices cut from the end at parameter boundaries (<= bucket_bytes each, a larger
 parameter gets a bucket of its own).  `NetProgram.backward` reports each op's parameters as soon
 as their gradient is written (`on_grads`); a bucket whose parameters have all received their last
-contribution of the step (`uses` backward calls per chunk) is launched at once:
-    event on the compute stream -> comm stream waits -> all_reduce(SUM) -> scale 1/world
-so the exchange of late layers overlaps the backward conv of early ones.  `finish()` launches any
-bucket never reported and makes the compute stream wait for the comm stream before Adam.
+contribution of the step (`uses` backward calls per chunk) is launched at once, so the exchange of one network
+overlaps the other network's chain (and, with several buckets, the backward conv of its own early layers).
+`join()` / `finish()` launch any bucket never reported before the Adam that reads it.
 
-Under hipGraph capture there are two modes:
-  * mode "segments" (the default; gloo and RCCL): a launch point closes the current graph segment (the program's
-    filter-gradient branch joined first) and replay runs segment, its buckets eagerly, next segment ... so the
-    collectives stay OUTSIDE the graphs.  Every all-reduce of a step is issued by the host thread, in replay order,
-    on ONE comm stream and ONE communicator: the issue order is the program order on every rank, whatever the GPU
-    timing (tests/test_ddp.py `order` case), and ProcessGroupNCCL's watchdog only ever polls events recorded
-    eagerly.  Round 6 made this the default everywhere: the captured mode below
-    aborted once in the driver's GPU suite (GPUTEST_r05, SIGABRT inside Trainer.capture) and no world > 1 run of it
-    exists;
-  * mode "graph" (opt-in, RCCL only, rounds 5-6): the all-reduces are CAPTURED.  A launch point first joins the
-    chunk's filter-gradient branch into the current (capture) stream (pre_launch), then forks the chunk's comm stream
-    off that stream alone -- every fork of the capture is ONE level deep (round 6: round 5 made the comm branch also
-    wait on the filter-gradient branch, a fork of a fork, the shape DESIGN.md §5 records as crashing
-    hipStreamEndCapture) -- and the bucket's all-reduce (ReduceOp.SUM) becomes a graph node on that branch;
-    `join(chunk)` at the end of the program's backward joins it back, so no graph is cut.  Each chunk all-reduces on
-    a communicator of its own (created in chunk order on every rank).  With the net overlap two graphs replay
-    concurrently on two streams, so two communicators would run in an order no rank controls: Trainer refuses graph
-    mode with the net overlap at world > 1, and an explicit `group` shared by several chunks is refused here.
-    Bucket size: measured on one GPU (config 4, world-1 RCCL group, bench.py --exchange on), every comm-branch fork
-    in the middle of a backward stalls the other network's chain (its wait packets sit in FIFO hardware queues shared
-    with it, GPU_MAX_HW_QUEUES = 4): 32 / 64 / 128 MB buckets 782 / 720 / 897 pairs/s, one bucket per
-    network (256 MB) 1049-1055, against 1089-1093 without the exchange -- hence Trainer.enable_ddp's 256 MB default
-    (DESIGN.md §6 derives the same default from a world-8 model).
-    The 1/world of the mean is NOT a pass of its own: chunk.grad holds the replicas' SUM after the exchange and Adam
-    applies `grad_scale` (= 1/world) as it reads the gradient (train.Adam reads it from this object at every update).
-    ReduceOp.AVG would fold the scale into RCCL instead, but RCCL runs AVG as a pre-multiplied sum with an extra kernel
-    per call -- at world 1 a oneRankReduce copy pass, 52 calls x 219 us per config-4 step, measured 1048-1051 pairs/s
-    against 1083-1087 with SUM (profiles/r05/bench_ab_exchange_sum.md).
+Over RCCL the collectives are direct `ncclAllReduce` calls on communicators of our own (rccl.py: one per parameter
+chunk, i.e. per network, created in chunk order on every rank) -- ProcessGroupNCCL, its Work objects, events and
+watchdog thread are not in the data path.  The replicas' SUM stays in chunk.grad; Adam applies 1/world as it loads
+the gradient (`grad_scale`, read by train.Adam at every update; no scale pass).  (ReduceOp.AVG would fold the scale
+into RCCL, but RCCL runs AVG as a pre-multiplied sum with an extra kernel per call: at world 1 a oneRankReduce copy
+pass, 52 calls x 219 us per config-4 step, profiles/r05/bench_ab_exchange_sum.md.)  Two modes:
+  * "segments" (the default): a launch point joins the reporting program's filter-gradient branch into its stream;
+    under capture it closes the current graph segment, and replay runs segment, the bucket's all-reduce issued by the
+    host on THAT stream, next segment ...  No collective is inside a graph, no extra stream exists (round 6: a
+    dedicated comm stream shared one of the GPU_MAX_HW_QUEUES = 4 FIFO hardware queues with a compute chain and cost
+    28 % at world 1, profiles/r06/bench_r06c_xseg_*), and each network's Adam follows its own exchange inline on its
+    stream.  Every collective is issued by one host thread in program order, each communicator from one stream: the
+    same sequence on every rank whatever the GPU timing (tests/test_ddp.py `order`);
+  * "graph" (opt-in, rounds 5-6): the all-reduces are CAPTURED.  A launch point first joins the chunk's filter-gradient
+    branch into the current (capture) stream (pre_launch), then forks the chunk's comm stream off that stream alone --
+    every fork of the capture is ONE level deep (round 6: round 5 made the comm branch also wait on the
+    filter-gradient branch, a fork of a fork, the shape DESIGN.md §5 records as crashing hipStreamEndCapture) -- and
+    the bucket's all-reduce becomes a graph node on that branch; `join(chunk)` at the end of the program's backward
+    joins it back, so no graph is cut.  With the net overlap two graphs replay concurrently on two streams:
+    Trainer refuses graph mode with it at world > 1.
+  Bucket size: measured on one GPU (config 4, world-1 RCCL, bench.py --exchange on), every mid-backward launch point
+  costs a join of the filter-gradient branch (and, in segments mode, a graph cut); DESIGN.md §6 derives the default,
+  one bucket per network (256 MB), from a world-8 model.
+Over gloo (CPU tensors, or GPU tensors in tests/test_gpu_ddp_world2.py) the launch goes through torch.distributed
+(on a comm stream for GPU tensors) and leaves the mean.
 
 On CPU (gloo, device 'cpu') the same bookkeeping runs synchronously; tests/test_ddp.py drives it with
 world_size 2.
@@ -112,17 +108,24 @@ def make_buckets(chunk, bucket_bytes):
 class GradSync:
     """Bucketed, overlapped gradient mean over the default process group (RCCL on GPU, gloo on CPU).
 
-    chunks: ParamChunks updated by the step; uses: {id(chunk): backward calls per step} (default 1)."""
+    chunks: ParamChunks updated by the step; uses: {id(chunk): backward calls per step} (default 1).
+
+    Over RCCL (GPU tensors, nccl backend) every chunk all-reduces on a direct RCCL communicator of its own
+    (rccl.pooled_comm: created in chunk order on every rank, so chunk i's communicator is the same everywhere) and the
+    replicas' SUM stays in chunk.grad: `grad_scale` = 1/world is what the optimizer applies (train.Adam reads it at
+    every update).  `inline` (segments mode over RCCL): the all-reduce is issued on the stream of the network that
+    reports the bucket, so its Adam may follow in the same stream (Trainer._inline_adam).  Over gloo the collectives
+    run through torch.distributed and leave the mean (grad_scale 1)."""
 
     def __init__(self, chunks, world, bucket_mb=32.0, uses=None, group=None, pre_launch=None, side_streams=None,
                  mode=None, pre_fork=None):
         self.world, self.group = world, group
         # pre_launch(chunk): joins the streams that write the chunk's gradients beside the current stream (its
         # program's filter-gradient branch, NetProgram.join_wgrad) into it.  Called before every graph-mode fork (so
-        # the comm branch forks from the current stream alone) and, in segments mode, before a launch point under
-        # capture (a graph segment can only end with its forked branches joined).  Eagerly in segments mode the
-        # compute stream never waits: side_streams(chunk) lists those streams and the comm stream waits on an event
-        # at each one's tail.
+        # the comm branch forks from the current stream alone), before every RCCL launch point of segments mode
+        # (the all-reduce follows on that stream) and, under capture, before a segment ends (a graph segment can
+        # only end with its forked branches joined).  Over gloo on GPU tensors (eager) the compute stream never
+        # waits: side_streams(chunk) lists those streams and the comm stream waits on an event at each one's tail.
         self.pre_launch = pre_launch
         self.side_streams = side_streams
         self.chunks = list(chunks)
@@ -137,32 +140,31 @@ class GradSync:
         self.pending = {}
         self.device = self.chunks[0].grad.device if self.chunks else torch.device("cpu")
         self.gpu = self.device.type == "cuda"
-        # a dedicated HIP stream (never one of torch's pooled streams, which a capture stream may alias)
-        self.comm = self._new_stream() if self.gpu else None
         self.capturing = None       # set by Trainer.capture: callable(buckets) closing a graph segment
         self.log = []               # launch order (names), for tests
         nccl = self._rccl(group)
+        self.rccl = nccl
         self.mode = mode or "segments"
         if self.mode not in ("graph", "segments") or (self.mode == "graph" and not nccl):
             raise ValueError(f"exchange mode {self.mode!r}: 'graph' needs RCCL (nccl backend), else 'segments'")
-        if self.mode == "graph" and group is not None and len(self.chunks) > 1:
-            #  graph mode gives every chunk a comm branch of its own; one explicit communicator under
-            # several branches would see their collectives in an order no rank controls
-            raise ValueError("exchange mode 'graph' with an explicit group and several parameter chunks: one "
-                             "communicator would serve concurrent graph branches; use mode 'segments'")
         self.captured = self.mode != "segments"
-        # what the optimizer multiplies the exchanged gradient by: graph mode leaves the replicas' SUM in chunk.grad
-        # (no scale pass on the comm branch), segments mode the mean
-        self.grad_scale = 1.0 / world if self.captured else 1.0
-        # graph mode: per chunk a comm stream and a communicator of its own (same creation order on every rank)
+        self.inline = nccl and not self.captured
+        # what the optimizer multiplies the exchanged gradient by: over RCCL the replicas' SUM stays in chunk.grad (no
+        # scale pass), over gloo the launch leaves the mean
+        self.grad_scale = 1.0 / world if nccl else 1.0
+        # gloo on GPU tensors: one dedicated comm stream (a HIP stream of its own, never one of torch's pooled streams,
+        # which a capture stream may alias)
+        self.comm = self._new_stream() if (self.gpu and not nccl) else None
+        # over RCCL: per chunk a direct communicator (and in graph mode a comm stream) of its own
         # pre_fork(chunk): issue whatever the chunk's program still holds back for its side streams (the deferred
         # filter-gradient calls) before a launch point records events on them
         self.pre_fork = pre_fork
         self.comm_of, self.group_of = {}, {}
-        if self.captured:
+        if nccl:
             for i, c in enumerate(self.chunks):
-                self.comm_of[id(c)] = self._new_stream()
-                self.group_of[id(c)] = self._chunk_group(i) if group is None else group
+                self.group_of[id(c)] = self._chunk_comm(i, group)
+                if self.captured:
+                    self.comm_of[id(c)] = self._new_stream()
         self.forked = set()         # chunks whose comm stream has work not yet joined (graph mode)
         self.begin_step()
 
@@ -177,8 +179,9 @@ class GradSync:
         return _lib.dedicated_stream()
 
     @staticmethod
-    def _chunk_group(i):
-        return pooled_group("exchange", i)
+    def _chunk_comm(i, group):
+        from .rccl import pooled_comm
+        return pooled_comm("exchange", i, group)
 
     @staticmethod
     def _current():
@@ -193,9 +196,8 @@ class GradSync:
         _lib.wait_stream(waiter, waitee)
 
     @staticmethod
-    def _all_reduce(view, group):
-        import torch.distributed as dist
-        dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
+    def _all_reduce(view, comm):
+        comm.all_reduce_sum(view)      # on the current stream
 
     # ---- per-step bookkeeping
     def begin_step(self):
@@ -234,15 +236,25 @@ class GradSync:
             if self.pre_launch is not None:
                 self.pre_launch(chunk)
             self.capturing(buckets)      # graph segment boundary; launched at replay
+        elif self.inline:
+            if self.pre_launch is not None and chunk is not None:
+                self.pre_launch(chunk)   # the all-reduce follows the chunk's filter gradients on this stream
+            self.launch(buckets)
         else:
             self.launch(buckets, self.side_streams(chunk) if (self.side_streams and chunk is not None) else ())
 
     # ---- the exchange
     def launch(self, buckets, streams=()):
-        """All-reduce `buckets` on the comm stream after everything issued so far on the current stream and on
-        `streams` (events: neither the current stream nor the side streams wait for anything)."""
+        """Segments mode.  Over RCCL: all-reduce (SUM) `buckets` on the CURRENT stream, each on its chunk's
+        communicator (at replay: the stream of the piece whose segment just ended, which joined its filter-gradient
+        branch before the cut).  Over gloo: on the comm stream after everything issued so far on the current stream
+        and on `streams` (events: neither the current stream nor the side streams wait), then the 1/world scale."""
         import torch.distributed as dist
         self.log.extend(list(b.names) for b in buckets)
+        if self.rccl:
+            for b in buckets:
+                self._all_reduce(b.view(), self.group_of[id(b.chunk)])
+            return
         if not self.gpu:
             for b in buckets:
                 v = b.view()
@@ -285,25 +297,28 @@ class GradSync:
         self.forked.add(id(chunk))
 
     def join(self, chunk):
-        """Graph mode: launch the chunk's buckets never reported, then order the current stream after its comm stream
-        (the end of the program's backward: its Adam may follow)."""
-        if not self.captured:
-            return
+        """End of a program's backward (its Adam may follow).  Graph mode: launch the chunk's buckets never reported
+        on its branch, then order the current stream after its comm stream.  Inline segments mode: the chunk's
+        unreported buckets become a launch point of their own (under capture a segment cut), so they are reduced
+        before the Adam that follows on this stream."""
         rest = [b for b in self.buckets if b.chunk is chunk and not b.launched]
-        if rest:
-            for b in rest:
-                b.launched = True
-            self.launch_forked(rest, chunk)
-        if id(chunk) in self.forked:
-            self._wait(self._current(), self.comm_of[id(chunk)])
-            self.forked.discard(id(chunk))
+        if self.captured:
+            if rest:
+                for b in rest:
+                    b.launched = True
+                self.launch_forked(rest, chunk)
+            if id(chunk) in self.forked:
+                self._wait(self._current(), self.comm_of[id(chunk)])
+                self.forked.discard(id(chunk))
+        elif self.inline and rest:
+            self._ready(rest, chunk)
 
     def leftovers(self):
         return [b for b in self.buckets if not b.launched]
 
     def finish(self, streams=()):
         """Launch what was never reported (after `streams` too), then order the compute stream after the comm
-        stream."""
+        stream (gloo on GPU tensors)."""
         if self.captured:
             for c in self.chunks:
                 self.join(c)
@@ -313,7 +328,7 @@ class GradSync:
             for b in rest:
                 b.launched = True
             self.launch(rest, streams)
-        if self.gpu:
+        if self.comm is not None:
             torch.cuda.current_stream().wait_stream(self.comm)
 
     def __call__(self):

@@ -276,6 +276,7 @@ class Trainer:
 
     graphs = None
     segments = None          # [(graph, buckets launched after it)] when capturing with a GradSync
+    seg_update = None        # the segmented capture's update graph (None when Adam runs inline)
     grad_sync = None
     BACKWARD_USES = 1        # backward calls per chunk per step (shared-variable nets call it twice)
 
@@ -443,6 +444,10 @@ class Trainer:
         else:
             self.phase_update()
 
+    def _inline_adam(self):
+        """Whether each program's Adam runs inside phase_compute right after its own backward (DepthThenCamTrainer)."""
+        return False
+
     def _program_of(self, chunk):
         for p in self.programs():
             if p.chunk is chunk:
@@ -553,7 +558,7 @@ class Trainer:
 
     def release_graphs(self):
         """Drop the captured graphs (their memory pools go with them); step() runs eagerly until the next capture."""
-        self.graphs = self.segments = None
+        self.graphs = self.segments = self.seg_update = None
         if hasattr(self, "ov_seq"):
             self.ov_seq = None
         if hasattr(self, "ov_upd"):
@@ -622,15 +627,19 @@ class Trainer:
                 state["g"].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
                 self.phase_compute()
                 segs.append((_end_segment(state["g"]), gs.leftovers()))
-                upd = torch.cuda.CUDAGraph()
-                upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
-                self.phase_update()
-                upd.capture_end()
+                upd = None
+                if not self._inline_adam():
+                    # (over RCCL a program's Adam follows its own exchange inside phase_compute: no update graph)
+                    upd = torch.cuda.CUDAGraph()
+                    upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+                    self.phase_update()
+                    upd.capture_end()
         finally:
             gs.capturing = None
         torch.cuda.synchronize()
         self.segments = segs
-        self.graphs = [g for g, _ in segs if g is not None] + [upd]
+        self.seg_update = upd
+        self.graphs = [g for g, _ in segs if g is not None] + ([upd] if upd is not None else [])
         return self.graphs
 
     def step(self):
@@ -647,7 +656,8 @@ class Trainer:
                         b.launched = True
                     gs.launch(buckets)
             gs.finish()
-            self.graphs[-1].replay()
+            if self.seg_update is not None:
+                self.seg_update.replay()
         elif len(self.graphs) == 1:
             if self.dadam is not None and self.dadam.pending != self._graph_owes:
                 # an eager flush() (checkpoint save, read-out) already applied the update the graph would apply
@@ -988,7 +998,8 @@ class DepthThenCamTrainer(Trainer):
         backward on that backward's stream -- depth_net's update overlaps disp_net's backward tail (and the
         other way round) instead of both updates waiting for the join.  The same update arithmetic."""
         gs = self.grad_sync
-        return (gs is None or getattr(gs, "captured", False)) and self.adam_ov is None and self.dadam is None
+        return ((gs is None or getattr(gs, "captured", False) or getattr(gs, "inline", False)) and
+                self.adam_ov is None and self.dadam is None)
 
     def _p_bwd_pair(self):
         if self.twin:
@@ -996,8 +1007,8 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("pr", self.pair, True)
             self._bwd("pl", self.pair, False)     # (backward ends by joining its filter-gradient stream)
-        if self.grad_sync is not None and getattr(self.grad_sync, "captured", False):
-            self.grad_sync.join(self.pair.chunk)  # depth_net's exchange branch back before its Adam
+        if self.grad_sync is not None and hasattr(self.grad_sync, "join"):
+            self.grad_sync.join(self.pair.chunk)  # depth_net's exchange (branch joined / leftovers reduced) before its Adam
         if self._inline_adam():
             self.opt.opts[1].step()
             self._tl("pair adam")
@@ -1008,7 +1019,7 @@ class DepthThenCamTrainer(Trainer):
         else:
             self._bwd("sr", self.single, True)
             self._bwd("sl", self.single, False)
-        if self.grad_sync is not None and getattr(self.grad_sync, "captured", False):
+        if self.grad_sync is not None and hasattr(self.grad_sync, "join"):
             self.grad_sync.join(self.single.chunk)
         if self._inline_adam():
             self.opt.opts[0].step()
@@ -1088,11 +1099,14 @@ class DepthThenCamTrainer(Trainer):
             if seg:
                 gs.capturing = None
                 leftovers = gs.leftovers()
-                upd = torch.cuda.CUDAGraph()
-                with torch.cuda.stream(main):
-                    upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
-                    self.phase_update()
-                    upd.capture_end()
+                upd = None
+                if not self._inline_adam():
+                    # (over RCCL each chain's Adam follows its own exchange inline: no separate update graph)
+                    upd = torch.cuda.CUDAGraph()
+                    with torch.cuda.stream(main):
+                        upd.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+                        self.phase_update()
+                        upd.capture_end()
                 self.ov_upd = (leftovers, upd)
         finally:
             if seg:
@@ -1100,7 +1114,7 @@ class DepthThenCamTrainer(Trainer):
         torch.cuda.synchronize()
         self.ov_seq = seq
         self.graphs = [g for _, segs in seq if segs is not None for g, _ in segs if g is not None]
-        if seg:
+        if seg and self.ov_upd[1] is not None:
             self.graphs.append(self.ov_upd[1])
         return self.graphs
 
@@ -1136,7 +1150,8 @@ class DepthThenCamTrainer(Trainer):
                         gs.launch(buckets)      # the comm stream waits on this stream's tail
         if seg:
             gs.finish()
-            self.ov_upd[1].replay()
+            if self.ov_upd[1] is not None:
+                self.ov_upd[1].replay()
 
     def _p_loss(self):
         from . import losses as Ls
