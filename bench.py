@@ -446,10 +446,11 @@ def main():
                     help="gradient exchange: auto = with N > 1; on = also at N = 1 over a world-1 RCCL group (times the "
                          "multi-GPU code path on one GPU)")
     ap.add_argument("--exchange-mode", default="segments", choices=["graph", "segments"],
-                    help="bucket all-reduces issued eagerly by the host between graph segments cut at each bucket "
-                         "launch point, in program order on one comm stream (segments, the default since round 6), or "
-                         "captured into the step's graphs on per-network comm branches (graph; refused with the net "
-                         "overlap at N > 1, see ddp.py)")
+                    help="bucket all-reduces (direct RCCL, one communicator per network) issued by the host between "
+                         "graph segments cut at each bucket launch point, on the reporting network's own stream, each "
+                         "network's Adam inline after its exchange (segments, the default since round 6), or captured "
+                         "into the step's graphs on per-network comm branches (graph; refused with the net overlap at "
+                         "N > 1, see ddp.py)")
     args = ap.parse_args()
     knobs = env_knobs()
 

@@ -254,7 +254,8 @@ def test_direct_rccl_communicator(pg):
     assert torch.equal(t, ref)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
-        c.all_reduce_sum(t)
+        c.all_reduce_sum(t)      # (at one rank RCCL records no node for an in-place SUM)
+        t.mul_(1.0)              # keep the graph non-empty
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
