@@ -11,7 +11,8 @@ rc=$?; tail -3 gpurun_out/gpu_tests_${tag}.txt; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${tag}.txt 2>&1 || { tail -5 gpurun_out/smoke_${tag}.txt; exit 1; }
 timeout -k 10 500 python3 bench.py --graph-spans gpurun_out/spans_${tag}.json > gpurun_out/bench_${tag}.json 2> gpurun_out/bench_${tag}.err || { tail -5 gpurun_out/bench_${tag}.err; exit 1; }
 cat gpurun_out/bench_${tag}.json | head -c 600; echo
-for b in 256 64; do
+timeout -k 10 300 python3 scripts/infer_bench.py --iters 100 > gpurun_out/infer_${tag}.json 2> gpurun_out/infer_${tag}.err || { tail -5 gpurun_out/infer_${tag}.err; exit 1; }
+for b in 256; do
   timeout -k 10 300 python3 bench.py --exchange on --bucket-mb $b --no-cpu-baseline --no-secondary --steps 60 --warmup 15 > gpurun_out/bench_${tag}_xseg_b$b.json 2> gpurun_out/bench_${tag}_xseg_b$b.err || { tail -5 gpurun_out/bench_${tag}_xseg_b$b.err; exit 1; }
   head -c 300 gpurun_out/bench_${tag}_xseg_b$b.json; echo
 done

@@ -48,24 +48,6 @@ import torch
 
 from . import _lib
 
-_GROUPS = {}
-
-
-def pooled_group(purpose, idx):
-    """The idx-th RCCL communicator of `purpose` ("exchange", "syncbn") over the default process group, created on
-    first use and reused by every later trainer of this process (all ranks ask in the same order, so the i-th group
-    of a purpose is the same communicator everywhere).  One new group per trainer would pile up communicators -- and
-    their device buffers and proxy threads -- in a process that builds many trainers (the GPU tests).  Entries hold
-    the default group they were made under, so a re-initialised default group gets fresh ones."""
-    import torch.distributed as dist
-    world = dist.distributed_c10d._get_default_group()
-    key = (id(world), purpose, idx)
-    hit = _GROUPS.get(key)
-    if hit is None:
-        hit = _GROUPS[key] = (world, dist.new_group(backend="nccl"))
-    return hit[1]
-
-
 class Bucket:
     __slots__ = ("chunk", "lo", "hi", "names", "launched", "opt")
 

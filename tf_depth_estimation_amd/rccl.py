@@ -21,7 +21,9 @@ import os
 import torch
 
 NCCL_FLOAT32 = 7     # ncclDataType_t ncclFloat32
+NCCL_FLOAT64 = 8     # ncclDataType_t ncclFloat64
 NCCL_SUM = 0         # ncclRedOp_t ncclSum
+_DTYPES = {torch.float32: NCCL_FLOAT32, torch.float64: NCCL_FLOAT64}
 
 _LIB = None
 
@@ -80,12 +82,12 @@ class Communicator:
         _check(lib().ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank), "ncclCommInitRank")
 
     def all_reduce_sum(self, t, stream=None):
-        """In-place SUM over the ranks of a contiguous float32 CUDA tensor, issued on `stream` (default: the current
-        stream).  Stream-ordered, no host synchronisation, capturable."""
-        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
-            raise ValueError("all_reduce_sum expects a contiguous float32 CUDA tensor")
+        """In-place SUM over the ranks of a contiguous float32 / float64 CUDA tensor (gradients / SyncBN's fp64 sums),
+        issued on `stream` (default: the current stream).  Stream-ordered, no host synchronisation, capturable."""
+        if t.dtype not in _DTYPES or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("all_reduce_sum expects a contiguous float32 or float64 CUDA tensor")
         st = (stream or torch.cuda.current_stream()).cuda_stream
-        _check(lib().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_FLOAT32, NCCL_SUM, self.comm,
+        _check(lib().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPES[t.dtype], NCCL_SUM, self.comm,
                                    ctypes.c_void_p(st)), "ncclAllReduce")
 
 

@@ -503,10 +503,11 @@ class Trainer:
         replicas (one all-reduce of fp64 per-channel sums per BN layer and direction, all row groups of a twin
         run in one) -- the reference's semantics at the global batch.
 
-        Over RCCL the sums all-reduce on a communicator of their own (a new process group: the gradient exchange's
-        bucket all-reduces run on another stream, and two streams' collectives on ONE communicator may meet in
-        different orders on different GPUs) and the step can be captured: the all-reduces become nodes of the
-        graph.  Over gloo (host collectives) the step runs eagerly."""
+        Over RCCL the sums all-reduce on direct RCCL communicators of their own (rccl.py; one per program, created
+        in program order on every rank: each program's collectives are issued from its one stream in a fixed order,
+        so the two networks of config 4 may run on two streams, and none of them shares a communicator with the
+        gradient exchange) and the step can be captured: the all-reduces become nodes of the graph, with no
+        ProcessGroupNCCL event or watchdog involved.  Over gloo (host collectives) the step runs eagerly."""
         import torch.distributed as dist
         nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
 
@@ -515,14 +516,15 @@ class Trainer:
                 dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
             return sync
 
-        from .ddp import pooled_group
+        def make_rccl_sync(comm):
+            def sync(t):
+                comm.all_reduce_sum(t)       # on the current stream
+            return sync
+
+        from .rccl import pooled_comm
         for pi, p in enumerate(self.programs()):
-            # over RCCL one communicator PER PROGRAM (created in program order on every rank): each program's
-            # collectives are then issued from one stream in a fixed order, so the two networks of config 4 may run
-            # on two streams (enable_net_overlap) without their all-reduces meeting in different orders on
-            # different GPUs
-            g = pooled_group("syncbn", pi) if nccl and group is None else group
-            p.bn_sync, p.bn_world = make_sync(g), world
+            sync = make_rccl_sync(pooled_comm("syncbn", pi, group)) if nccl else make_sync(group)
+            p.bn_sync, p.bn_world = sync, world
         self.sync_bn = True
         self.sync_bn_capturable = nccl
         self._sync_bn_group = group
