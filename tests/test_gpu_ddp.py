@@ -260,6 +260,11 @@ def test_direct_rccl_communicator(pg):
         g.replay()
     torch.cuda.synchronize()
     assert torch.equal(t, ref)
-    with pytest.raises(ValueError):
-        c.all_reduce_sum(t.double())
+    d = torch.ones(1000, dtype=torch.float64, device="cuda")      # SyncBN's fp64 sums
+    c.all_reduce_sum(d)
+    torch.cuda.synchronize()
+    assert torch.equal(d, torch.ones_like(d))
+    for bad in (t.to(torch.int32), t.view(2, -1).t(), t.cpu()):
+        with pytest.raises(ValueError):
+            c.all_reduce_sum(bad)
     assert rccl.pooled_comm("test", 0) is rccl.pooled_comm("test", 0)
