@@ -91,6 +91,34 @@ __global__ void __launch_bounds__(256) resize_area_kernel(const AreaArgs a) {
     const int r = (int)(p - (long)b * a.OH * a.OW);
     const int dy = r / a.OW, dx = r - dy * a.OW;
     const unsigned char* S = a.src + (long)b * a.H * a.W * a.C;
+    unsigned char area_out[4] = {0, 0, 0, 0};
+    if (a.mode == 2) {
+      // ResizeArea_Invoker: for each source row of the y-span (in table order) the row's x-span sum
+      // buf = sum_k S*alpha_k (float, from 0), then sum = beta_0*buf_0, sum += beta_j*buf_j; round.  The spans are
+      // computed once per output pixel, all channels accumulate together (same per-channel operation order).
+      const AreaSpan ty = area_span(dy, a.H, a.sy), tx = area_span(dx, a.W, a.sx);
+      float sum[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < ty.n; ++j) {
+        int sy;
+        float beta;
+        area_tap(ty, j, sy, beta);
+        const unsigned char* row = S + (long)sy * a.W * a.C;
+        float buf[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < tx.n; ++k) {
+          int sx;
+          float alpha;
+          area_tap(tx, k, sx, alpha);
+          const unsigned char* px = row + (long)sx * a.C;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c < a.C) buf[c] = buf[c] + (float)px[c] * alpha;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sum[c] = (j == 0) ? beta * buf[c] : sum[c] + beta * buf[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) area_out[c] = sat_u8(sum[c]);
+    }
     for (int c = 0; c < a.C; ++c) {
       unsigned char out;
       if (a.mode == 0) {
@@ -115,25 +143,7 @@ __global__ void __launch_bounds__(256) resize_area_kernel(const AreaArgs a) {
           out = count ? sat_u8(__fdiv_rn((float)sum, (float)count)) : (unsigned char)0;
         }
       } else if (a.mode == 2) {
-        // ResizeArea_Invoker: for each source row of the y-span (in table order) the row's x-span sum
-        // buf = sum_k S*alpha_k (float, from 0), then sum = beta_0*buf_0, sum += beta_j*buf_j; round
-        const AreaSpan ty = area_span(dy, a.H, a.sy), tx = area_span(dx, a.W, a.sx);
-        float sum = 0.f;
-        for (int j = 0; j < ty.n; ++j) {
-          int sy;
-          float beta;
-          area_tap(ty, j, sy, beta);
-          const unsigned char* row = S + (long)sy * a.W * a.C;
-          float buf = 0.f;
-          for (int k = 0; k < tx.n; ++k) {
-            int sx;
-            float alpha;
-            area_tap(tx, k, sx, alpha);
-            buf = buf + (float)row[(long)sx * a.C + c] * alpha;
-          }
-          sum = (j == 0) ? beta * buf : sum + beta * buf;
-        }
-        out = sat_u8(sum);
+        out = area_out[c];
       } else {
         // area-mode emulation by linear interpolation (resizeGeneric_ with area_mode, 8-bit fixed point):
         // sx = floor(dx*scale), fx = (dx+1) - (sx+1)*inv_scale, fx = fx <= 0 ? 0 : fx - floor(fx); coefficients
@@ -242,14 +252,20 @@ struct SpaceTable {
   short dy[kMaxTaps], dx[kMaxTaps];
 };
 
-constexpr int kBilWs = 4 + kExpBins + 2;   // floats per image
+constexpr int kBilWs = 4 + kExpBins + 2;   // floats per image (then the min / max partials, kMinMaxBlocks x 2 each)
 
-// per image min / max (minMaxLoc over the map; NaN skipped) -> scale_index, copy flag
-__global__ void __launch_bounds__(256) bil_minmax_kernel(const BilateralArgs a) {
-  const int b = blockIdx.x;
+constexpr int kMinMaxBlocks = 64;          // min / max partial blocks per image
+
+struct BilPartials {
+  float* p;                  // [B][kMinMaxBlocks][2] (min, max) partials
+};
+
+// per image min / max partials (minMaxLoc over the map, NaN skipped): block x of image y takes a strided share
+__global__ void __launch_bounds__(256) bil_minmax_kernel(const BilateralArgs a, BilPartials bp) {
+  const int b = blockIdx.y;
   const float* S = a.src + (long)b * a.H * a.W;
   float lo = FLT_MAX, hi = -FLT_MAX;
-  for (int i = threadIdx.x; i < a.H * a.W; i += 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < a.H * a.W; i += kMinMaxBlocks * 256) {
     const float v = S[i];
     if (v == v) {
       lo = fminf(lo, v);
@@ -271,24 +287,41 @@ __global__ void __launch_bounds__(256) bil_minmax_kernel(const BilateralArgs a) 
       lo = fminf(lo, sl[w]);
       hi = fmaxf(hi, sh[w]);
     }
-    float* W = a.ws + (long)b * kBilWs;
-    W[0] = lo;
-    W[1] = hi;
-    // len = (float)(maxVal - minVal) * cn (minMaxLoc returns doubles); scale_index = kExpNumBins / len (float)
-    const float len = (float)((double)hi - (double)lo);
-    W[2] = __fdiv_rn((float)kExpBins, len);
-    W[3] = fabs((double)lo - (double)hi) < FLT_EPSILON ? 1.f : 0.f;
+    bp.p[((long)b * kMinMaxBlocks + blockIdx.x) * 2] = lo;
+    bp.p[((long)b * kMinMaxBlocks + blockIdx.x) * 2 + 1] = hi;
   }
 }
 
+// Each block first folds the image's min / max partials (min / max are order-free: every block gets the same
+// values) -> scale_index and the copy flag (block 0 publishes them), then its share of the table:
 // expLUT[i] = (float)exp(val*val*gauss_color_coeff), double val = i / scale_index (a float division: scale_index is
 // a float)
-__global__ void __launch_bounds__(256) bil_lut_kernel(const BilateralArgs a) {
+__global__ void __launch_bounds__(256) bil_lut_kernel(const BilateralArgs a, BilPartials bp) {
   const int b = blockIdx.y;
   float* W = a.ws + (long)b * kBilWs;
+  __shared__ float s_scale;
+  if (threadIdx.x < 64) {
+    float lo = bp.p[((long)b * kMinMaxBlocks + threadIdx.x) * 2], hi = bp.p[((long)b * kMinMaxBlocks + threadIdx.x) * 2 + 1];
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = fminf(lo, __shfl_down(lo, o, 64));
+      hi = fmaxf(hi, __shfl_down(hi, o, 64));
+    }
+    if (threadIdx.x == 0) {
+      // len = (float)(maxVal - minVal) * cn (minMaxLoc returns doubles); scale_index = kExpNumBins / len (float)
+      const float len = (float)((double)hi - (double)lo);
+      s_scale = __fdiv_rn((float)kExpBins, len);
+      if (blockIdx.x == 0) {
+        W[0] = lo;
+        W[1] = hi;
+        W[2] = s_scale;
+        W[3] = fabs((double)lo - (double)hi) < FLT_EPSILON ? 1.f : 0.f;
+      }
+    }
+  }
+  __syncthreads();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= kExpBins + 2) return;
-  const double val = (double)__fdiv_rn((float)i, W[2]);
+  const double val = (double)__fdiv_rn((float)i, s_scale);
   W[4 + i] = (float)exp(val * val * a.color_coeff);
 }
 
@@ -382,7 +415,9 @@ int tde_resize_cubic_f32(int B, int H, int W, const float* src, int s_cstride, i
   return tde_launch_status();
 }
 
-size_t tde_bilateral_workspace_size(int B) { return B > 0 ? (size_t)B * kBilWs * sizeof(float) : 0; }
+size_t tde_bilateral_workspace_size(int B) {
+  return B > 0 ? (size_t)B * (kBilWs + 2 * kMinMaxBlocks) * sizeof(float) : 0;
+}
 
 int tde_bilateral_f32(int B, int H, int W, const float* src, float* dst, int d, double sigma_color,
                       double sigma_space, void* ws, size_t ws_bytes, void* stream) {
@@ -412,8 +447,9 @@ int tde_bilateral_f32(int B, int H, int W, const float* src, float* dst, int d, 
   a.src = src; a.dst = dst; a.ws = static_cast<float*>(ws);
   a.color_coeff = -0.5 / (sigma_color * sigma_color);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(bil_minmax_kernel, dim3(B), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(bil_lut_kernel, dim3(tde_cdiv(kExpBins + 2, 256), B), dim3(256), 0, st, a);
+  BilPartials bp{static_cast<float*>(ws) + (size_t)B * kBilWs};
+  hipLaunchKernelGGL(bil_minmax_kernel, dim3(kMinMaxBlocks, B), dim3(256), 0, st, a, bp);
+  hipLaunchKernelGGL(bil_lut_kernel, dim3(tde_cdiv(kExpBins + 2, 256), B), dim3(256), 0, st, a, bp);
   hipLaunchKernelGGL(bil_filter_kernel, dim3(blocks_for((long)B * H * W)), dim3(256), 0, st, a, sp);
   return tde_launch_status();
 }
