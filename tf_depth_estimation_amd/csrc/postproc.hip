@@ -98,20 +98,46 @@ __global__ void __launch_bounds__(256) resize_area_kernel(const AreaArgs a) {
       // computed once per output pixel, all channels accumulate together (same per-channel operation order).
       const AreaSpan ty = area_span(dy, a.H, a.sy), tx = area_span(dx, a.W, a.sx);
       float sum[4] = {0.f, 0.f, 0.f, 0.f};
+      // up to kAreaTaps taps per axis (scales < kAreaTaps - 1) with every tap's load of a row issued before its
+      // first use; wider cells take the plain loop
+      constexpr int kAreaTaps = 6;
+      int xs[kAreaTaps];
+      float xa[kAreaTaps];
+      const bool small = tx.n <= kAreaTaps;
+#pragma unroll
+      for (int k = 0; k < kAreaTaps; ++k) {
+        xs[k] = 0;
+        xa[k] = 0.f;
+        if (k < tx.n) area_tap(tx, k, xs[k], xa[k]);
+      }
       for (int j = 0; j < ty.n; ++j) {
         int sy;
         float beta;
         area_tap(ty, j, sy, beta);
         const unsigned char* row = S + (long)sy * a.W * a.C;
         float buf[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < tx.n; ++k) {
-          int sx;
-          float alpha;
-          area_tap(tx, k, sx, alpha);
-          const unsigned char* px = row + (long)sx * a.C;
+        if (small) {
+          unsigned char v[kAreaTaps][4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (c < a.C) buf[c] = buf[c] + (float)px[c] * alpha;
+          for (int k = 0; k < kAreaTaps; ++k)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[k][c] = (k < tx.n && c < a.C) ? row[(long)xs[k] * a.C + c] : 0;
+#pragma unroll
+          for (int k = 0; k < kAreaTaps; ++k)
+            if (k < tx.n) {
+#pragma unroll
+              for (int c = 0; c < 4; ++c) buf[c] = buf[c] + (float)v[k][c] * xa[k];
+            }
+        } else {
+          for (int k = 0; k < tx.n; ++k) {
+            int sx;
+            float alpha;
+            area_tap(tx, k, sx, alpha);
+            const unsigned char* px = row + (long)sx * a.C;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (c < a.C) buf[c] = buf[c] + (float)px[c] * alpha;
+          }
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) sum[c] = (j == 0) ? beta * buf[c] : sum[c] + beta * buf[c];
