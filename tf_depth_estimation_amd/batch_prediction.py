@@ -110,10 +110,13 @@ class Predictor:
     overwrites (clone to keep).  Variables come from the process variable store under `scope`, so a
     network trained in this process predicts directly; `restore()` loads a checkpoint instead."""
 
-    def __init__(self, net="disp_net", H=224, W=224, batch=1, scope="model", fold_bn=True, graph=True):
+    def __init__(self, net="disp_net", H=224, W=224, batch=1, scope="model", fold_bn=True, graph=True, cin=None):
+        """cin: input channels when not the net's usual count -- batch_prediction_optflow.py:43 feeds depth_net an
+        11-channel [I, I1, flow, I_warp] stack at 240x720."""
         if net not in NETS:
             raise ValueError(f"unknown net {net!r}: one of {sorted(NETS)}")
-        net_scope, builder, cin, kw, _ = NETS[net]
+        net_scope, builder, cin0, kw, _ = NETS[net]
+        cin = cin0 if cin is None else int(cin)
         self.net, self.fold, self.use_graph = net, bool(fold_bn), bool(graph)
         with variables.variable_scope(scope):
             self.prog = _api.get_program(net_scope, builder, H, W, cin, **kw)
@@ -172,6 +175,25 @@ class Predictor:
             self.outs = self._forward()
         z = resize_cubic(self.outs[0], out_hw[0], out_hw[1])
         return bilateral_filter(z, 9, 75.0, 75.0)
+
+    def predict_pose(self, image_a_u8, image_b_u8):
+        """The loop body of batch_prediction_cam_est.py:79-98: both decoded images INTER_AREA-resized (:82,88) straight
+        into the two channel halves of the network input (the concat of :90), the depth_net prediction, and the pose
+        [B, 6] the script saves with np.savetxt (:98)."""
+        if self.net != "depth_net" or self.x.shape[3] != 6:
+            raise ValueError("predict_pose is batch_prediction_cam_est.py's 6-channel depth_net path")
+        B, H, W = self.x.shape[:3]
+        for half, img in ((0, image_a_u8), (1, image_b_u8)):
+            t = img if img.dim() == 4 else img.unsqueeze(0)
+            t = t.to(device=self.x.device, dtype=torch.uint8).contiguous()
+            if t.shape[0] != B or t.shape[3] != 3:
+                raise ValueError(f"expected {B} RGB image(s), got {tuple(t.shape)}")
+            resize_area(t, H, W, out_f32=self.x[..., 3 * half:3 * half + 3])
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.outs = self._forward()
+        return self.outs[2].reshape(B, 6)
 
     def __call__(self, images):
         """images: [batch, H, W, cin] float32 (host or device).  Returns the output list."""
