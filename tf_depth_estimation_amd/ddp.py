@@ -48,6 +48,7 @@ import torch
 
 from . import _lib
 
+
 class Bucket:
     __slots__ = ("chunk", "lo", "hi", "names", "launched", "opt")
 
