@@ -46,6 +46,7 @@ SHAPES = [
     ("upcnv3_b16", 16, 48, 64, 64, 128, 3, 2),
     # config 4's stride-2 layers at the twin batch (pixel-shuffle forms: deconv forward / conv dgrad, filter gradient)
     ("cnv1p_b16", 16, 192, 256, 8, 32, 7, 2),
+    ("cnv1c4_b16", 16, 192, 256, 4, 32, 7, 2),
     ("cnv2_b16", 16, 96, 128, 32, 64, 5, 2),
     ("cnv3_b16", 16, 48, 64, 64, 128, 3, 2),
     ("cnv4_b16", 16, 24, 32, 128, 256, 3, 2),

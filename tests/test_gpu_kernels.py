@@ -163,11 +163,12 @@ DECONV_CASES = [
 
 
 F16_SCALE_CASES = [
-    # N, H, W, C, K, k, s: implicit GEMM (split-K), skinny, halo (FWD/DGRAD), halo WGRAD
+    # N, H, W, C, K, k, s: implicit GEMM (split-K), skinny, halo (FWD/DGRAD), halo WGRAD (stride 1 and 2)
     (4, 24, 32, 256, 128, 3, 1),
     (8, 3, 4, 512, 512, 3, 1),
     (2, 96, 128, 32, 32, 7, 1),
     (2, 13, 17, 32, 64, 5, 2),
+    (2, 192, 256, 8, 32, 7, 2),      # stride-2 halo WGRAD (cnv1), pixel-shuffle DGRAD
 ]
 
 
@@ -634,6 +635,86 @@ def test_wgrad_pixel_shuffle(L, k, deconv):
                                             L.ptr(ws), ws.numel() * 4, st))
     torch.cuda.synchronize()
     close(gdw, w0 + w.grad, what=f"pixel-shuffle wgrad k{k} {'deconv' if deconv else 'conv'}")
+
+
+HWH_S2_CASES = [
+    # N, H, W, cin_real, C(view), K, k, x_cs, x_co: stride 2, TDE_HWH_S2_MINC..MAXC (8..16) view channels, >= 16384
+    # dy pixels
+    (2, 192, 256, 6, 8, 32, 7, 12, 4),       # config 4's cnv1 of the pair networks (6 channels), offset view
+    (4, 128, 192, 16, 16, 32, 7, 16, 0),     # exp_upcnv1's virtual conv (16 channels, 7x7)
+    (4, 130, 150, 8, 8, 16, 5, 8, 0),        # ragged: OW = 75 (one partial segment per row), one column fragment
+    (3, 160, 300, 12, 16, 28, 3, 20, 4),     # 3x3, OW = 150 (two segments per row, the second ragged), K = 28
+]
+
+
+@pytest.mark.parametrize("case", HWH_S2_CASES)
+def test_wgrad_halo_stride2(L, case):
+    """The stride-2 filter gradient on the halo-tiled fp16x3 kernel (halo_wgrad.hip hwh_kernel<..., S = 2>: the
+    segment's input row staged as two parity planes, tap kw read from plane kw & 1 at row offset kw / 2), through
+    tde_conv2d_bwd_filter (accumulating onto a prior dw) and through tde_conv2d_bwd (data gradient on its own path,
+    filter gradient here): against the fp64 autograd gradients of conv2d_same (nets_optflow_depth.py:88 cnv1)."""
+    lib = L.load()
+    st = L.stream_ptr()
+    assert lib.tde_get_conv_math() == 4
+    N, H, W, cin, C, K, k, xcs, xco = case
+    OH, pt, _ = T.same_pad(H, k, 2)
+    OW, pl, _ = T.same_pad(W, k, 2)
+    x = rnd(N, H, W, cin, seed=81)
+    gy = rnd(N, OH, OW, K, seed=82)
+    w = rnd(k, k, cin, K, seed=83) * 0.2
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    (T.conv2d_same(xr, wr, 2) * gy).sum().backward()
+    xin = torch.zeros(N, H, W, xcs, dtype=torch.float64)
+    xin[..., xco:xco + cin] = x
+    d = conv_desc(L, N=N, H=H, W=W, C=C, OH=OH, OW=OW, K=K, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
+                  w_cin=cin, x_cstride=xcs, x_coff=xco, y_cstride=K, y_coff=0)
+    ws = ws_for(L, d)
+    nb = lib.tde_conv2d_bwd_workspace_size(ctypes.byref(d))
+    if nb // 4 + 16 > ws.numel():
+        ws = torch.empty(nb // 4 + 16, device="cuda")
+    gx, ggy, gw = dev(xin), dev(gy), dev(w)
+    w0 = rnd(k, k, cin, K, seed=84)
+    gdw = dev(w0)
+    L.check(lib.tde_conv2d_bwd_filter(ctypes.byref(d), L.ptr(gx), L.ptr(ggy), L.ptr(gdw), 1, L.ptr(ws),
+                                      ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    close(gdw, w0 + wr.grad, what="halo wgrad stride 2 (bwd_filter, accumulate)")
+    gdx = torch.zeros(N, H, W, xcs, device="cuda")
+    gdw2 = torch.empty_like(gw)
+    L.check(lib.tde_conv2d_bwd(ctypes.byref(d), L.ptr(gx), L.ptr(ggy), L.ptr(gw), L.ptr(gdx), 0, L.ptr(gdw2), 0,
+                               L.ptr(ws), ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    close(gdw2, wr.grad, what="halo wgrad stride 2 (conv2d_bwd)")
+    close(gdx[..., xco:xco + cin], xr.grad, what="dgrad beside the halo wgrad")
+
+
+@pytest.mark.parametrize("k", [3, 7])
+def test_deconv_bwd_halo_stride2(L, k):
+    """A 16-channel stride-2 deconv's fused backward (tde_deconv2d_bwd: data gradient = the virtual conv's forward,
+    filter gradient on the stride-2 halo kernel; upcnv1 / exp_upcnv1, nets_optflow_depth.py:121,147) against the
+    fp64 autograd gradients of conv2d_transpose_same."""
+    lib = L.load()
+    st = L.stream_ptr()
+    N, h, w_, cin, cout = 4, 48, 96, 32, 16           # 18432 deconv input pixels (>= TDE_HWG_MIN_M)
+    H, W = 2 * h, 2 * w_
+    _, pt, _ = T.same_pad(H, k, 2)
+    _, pl, _ = T.same_pad(W, k, 2)
+    x = rnd(N, h, w_, cin, seed=85)
+    wt = rnd(k, k, cout, cin, seed=86) * 0.2
+    dy = rnd(N, H, W, cout, seed=87)
+    xr, wr = x.clone().requires_grad_(True), wt.clone().requires_grad_(True)
+    (T.conv2d_transpose_same(xr, wr, 2) * dy).sum().backward()
+    d = conv_desc(L, N=N, H=H, W=W, C=cout, OH=h, OW=w_, K=cin, KH=k, KW=k, stride=2, pad_top=pt, pad_left=pl,
+                  w_cin=cout, x_cstride=cout, x_coff=0, y_cstride=cin, y_coff=0)
+    nb = lib.tde_deconv2d_bwd_workspace_size(ctypes.byref(d))
+    ws = torch.empty(nb // 4 + 16, device="cuda")
+    gdx = torch.empty(N, h, w_, cin, device="cuda")
+    gdw = torch.empty(k, k, cout, cin, device="cuda")
+    L.check(lib.tde_deconv2d_bwd(ctypes.byref(d), L.ptr(dev(dy)), L.ptr(dev(x)), L.ptr(dev(wt)), L.ptr(gdx), 0,
+                                 L.ptr(gdw), 0, L.ptr(ws), ws.numel() * 4, st))
+    torch.cuda.synchronize()
+    close(gdx, xr.grad, what=f"deconv k{k} dgrad")
+    close(gdw, wr.grad, what=f"deconv k{k} wgrad (stride-2 halo)")
 
 
 HEAD_CASES = [

@@ -1600,6 +1600,15 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
   }
   const bool skipm = skip_conv(d);
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
+  HwgPlan wp;
+  if (MODE == MODE_WGRAD && hwg_plan(*d, wp, g_conv_math)) {
+    // narrow, high-resolution layer (stride 1, or stride 2 over few input channels): halo-tiled filter gradient (halo_wgrad.hip)
+    if (wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+    span_mark(0, static_cast<hipStream_t>(stream));
+    if (!skip) hwg_launch(wp, *d, a.x, a.dy, a.dw, accumulate, tde_ws_body(ws), static_cast<hipStream_t>(stream));
+    span_mark(1, static_cast<hipStream_t>(stream));
+    return tde_launch_status();
+  }
   if (MODE == MODE_WGRAD && psw_ok(*d)) {
     const Plan pl = psw_plan(*d);
     if (pl.ws_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
@@ -1611,15 +1620,6 @@ static int run(const tde_conv_desc_t* d, ConvArgs a, int accumulate, const tde_b
     if (!skip) launch_psw(pl, ap, st);
     if (!skipr) launch_psw_reduce(pl, ap, st);
     span_mark(1, st);
-    return tde_launch_status();
-  }
-  HwgPlan wp;
-  if (MODE == MODE_WGRAD && hwg_plan(*d, wp, g_conv_math)) {
-    // stride-1, narrow, high-resolution layer: halo-tiled filter gradient (halo_wgrad.hip)
-    if (wp.part_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
-    span_mark(0, static_cast<hipStream_t>(stream));
-    if (!skip) hwg_launch(wp, *d, a.x, a.dy, a.dw, accumulate, tde_ws_body(ws), static_cast<hipStream_t>(stream));
-    span_mark(1, static_cast<hipStream_t>(stream));
     return tde_launch_status();
   }
   HaloPlan hp;
@@ -1734,7 +1734,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   const bool skip = skipm && (g_skip_what & 1), skipr = skipm && (g_skip_what & 2);
   HaloPlan hp;
   HwgPlan wp;
-  if (MODE1 == MODE_DGRAD && hwg_plan(*d, wp, g_conv_math)) {
+  if (MODE1 == MODE_DGRAD && d->stride == 1 && hwg_plan(*d, wp, g_conv_math)) {
     // filter gradient on the halo-tiled WGRAD kernel; data gradient on the halo path or the implicit GEMM
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool hd = halo_plan(*d, 1, g_conv_math, hp);
@@ -1782,12 +1782,17 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   } else {
     p1 = make_plan(*d, MODE1);
   }
-  // the filter gradient of a stride-2 layer in the pixel-shuffle form (MODE_PSW) where it applies
-  const bool psw2 = !g_skip_wgrad && psw_ok(*d);
-  // fused data + filter gradient launch only when neither GEMM is a pixel-shuffle GEMM
-  const bool fuse = !ps1 && !psw2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 && !g_skip_wgrad;
-  const Plan p2 = psw2 ? psw_plan(*d) : make_plan(*d, MODE_WGRAD, fuse ? p1.bm : 0, fuse ? p1.bn : 0);
-  if (p1.slab_bytes + p2.slab_bytes > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
+  // the filter gradient of a stride-2 layer on the halo-tiled kernel (few input channels: hwg_plan) or in the
+  // pixel-shuffle form (MODE_PSW) where they apply
+  const bool hw2 = !g_skip_wgrad && d->stride == 2 && hwg_plan(*d, wp, g_conv_math);
+  const bool psw2 = !g_skip_wgrad && !hw2 && psw_ok(*d);
+  // fused data + filter gradient launch only when the filter gradient is an implicit GEMM and the data gradient is
+  // not a pixel-shuffle GEMM
+  const bool fuse = !ps1 && !psw2 && !hw2 && g_bwd_fuse != 0 && g_conv_math != 1 && p1.skinny_tm == 0 &&
+                    !g_skip_wgrad;
+  const Plan p2 = hw2 ? Plan{} : psw2 ? psw_plan(*d) : make_plan(*d, MODE_WGRAD, fuse ? p1.bm : 0, fuse ? p1.bn : 0);
+  const size_t b2 = hw2 ? wp.part_bytes : p2.slab_bytes;
+  if (p1.slab_bytes + b2 > ws_bytes || !ws || !tde_aligned16(ws)) return TDE_ERR_WORKSPACE;
   char* body = tde_ws_body(ws);
   a1.ws = reinterpret_cast<float*>(body);
   a1.splits = p1.splits; a1.kt_per = p1.kt_per; a1.accumulate = acc1; a1.bnp = nullptr;
@@ -1797,7 +1802,8 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto wgrad = [&] {
     if (g_skip_wgrad) return;
-    if (psw2) launch_psw(p2, a2p, st);
+    if (hw2) hwg_launch(wp, *d, a2.x, a2.dy, a2.dw, acc2, body + p1.slab_bytes, st);   // + its chunk reduce
+    else if (psw2) launch_psw(p2, a2p, st);
     else launch_mode<MODE_WGRAD>(p2, a2, st);
   };
   if (skip) {
@@ -1812,7 +1818,7 @@ static int run_bwd(const tde_conv_desc_t* d, ConvArgs a1, int acc1, ConvArgs a2,
     wgrad();
   }
   if (!skipr) {
-    if (g_skip_wgrad) launch_reduce<MODE1>(p1, a1, st);
+    if (g_skip_wgrad || hw2) launch_reduce<MODE1>(p1, a1, st);
     else if (psw2) launch_reduce2<MODE1, MODE_PSW>(p1, a1, p2, a2p, st);
     else launch_reduce2<MODE1>(p1, a1, p2, a2, st);
   }
@@ -1833,15 +1839,15 @@ static size_t bwd_ws_bytes(const tde_conv_desc_t& d, int mode1) {
       if (r > b) b = r;
     }
   }
-  if (mode1 == MODE_DGRAD) {
-    const size_t h = halo_ws_bytes(d, MODE_DGRAD, false);
+  const size_t h = mode1 == MODE_DGRAD ? halo_ws_bytes(d, MODE_DGRAD, false) : 0;
+  if (h) {
     const size_t w2 = make_plan(d, MODE_WGRAD).slab_bytes;
-    if (h && h + w2 > b) b = h + w2;
-    const size_t hw = hwg_ws_bytes(d);
-    if (hw) {
-      const size_t b1 = h > p1.slab_bytes ? h : p1.slab_bytes;   // halo or igemm data gradient (math-dependent)
-      if (b1 + hw > b) b = b1 + hw;
-    }
+    if (h + w2 > b) b = h + w2;
+  }
+  const size_t hw = hwg_ws_bytes(d);
+  if (hw) {
+    const size_t b1 = h > p1.slab_bytes ? h : p1.slab_bytes;   // halo or igemm data gradient (math-dependent)
+    if (b1 + hw > b) b = b1 + hw;
   }
   return b + 64;
 }

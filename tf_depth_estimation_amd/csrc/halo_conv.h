@@ -38,14 +38,15 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
 void halo_wprep_batch(int n, const HaloPlan* hps, const tde_conv_desc_t* const* ds, const float* const* ws,
                       void* const* outs, hipStream_t st);
 
-// Halo-tiled filter gradient (halo_wgrad.hip) of a stride-1 conv with K <= 32 output channels at high
-// resolution: partial dW per (pixel chunk, kernel row) in fp32 MFMA, then a fixed-order chunk reduce.
+// Halo-tiled filter gradient (halo_wgrad.hip) of a stride-1 (fp16x3 also stride-2) conv with K <= 32 output
+// channels at high resolution: partial dW per (pixel chunk, kernel row) on MFMA, then a fixed-order chunk reduce.
 struct HwgPlan {
   int ok;
   int f16;                // fp16x3 kernel (math 4): CF / NF / nitems = (kw, cf) items / CPS, KPS in fp16 elements
+  int S;                  // stride (2: the fp16x3 kernel's parity planes)
   int CF, NF, nitems;     // 16-channel input / output fragments, (kw, cf, nf) items per block
   int CPS, KPS;           // LDS row strides (floats)
-  int ntw, chunks;        // 64-pixel segments per output row, pixel chunks (grid x; grid y = KH)
+  int ntw, chunks;        // 128-pixel segments per output row, pixel chunks (grid x; grid y = KH)
   long ntiles;
   size_t lds_bytes, part_bytes;
 };

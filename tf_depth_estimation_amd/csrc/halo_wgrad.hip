@@ -31,6 +31,7 @@ constexpr int DQ = 4;         // f4 prefetch registers per thread: dy segment
 
 struct HwgArgs {
   int N, H, W, C, K, KH, KW, PT, PL, wcin;
+  int OH, OW, S;      // output rows / columns (the segments tile them) and stride (1; 2 in the fp16x3 kernel)
   int CF, NF, CPS, KPS, nitems, ntw, chunks;
   int ntiles;
   const float* x; int xcs, xco;
@@ -42,8 +43,8 @@ struct HwgArgs {
 __device__ __forceinline__ void tile_coords(const HwgArgs& a, int t, int& n, int& oh, int& ow0) {
   const int r = t / a.ntw;
   ow0 = (t - r * a.ntw) * TP;
-  n = r / a.H;
-  oh = r - n * a.H;
+  n = r / a.OH;
+  oh = r - n * a.OH;
 }
 
 // per-thread (pixel, channel) coordinates of its prefetch quads: constant over the tiles
@@ -62,19 +63,19 @@ __device__ __forceinline__ void prefetch(const HwgArgs& a, const QuadsT<XQN, DQN
   const bool tv = t < a.ntiles && !(a.diag & 2);
   int n = 0, oh = 0, ow0 = 0;
   if (tv) tile_coords(a, t, n, oh, ow0);
-  const int ih = oh + kh - a.PT;
+  const int ih = oh * a.S + kh - a.PT;
   const bool rowok = tv && (unsigned)ih < (unsigned)a.H;
   const int xrow = ((n * a.H + ih) * a.W) * a.xcs + a.xco;
 #pragma unroll
   for (int i = 0; i < XQN; ++i) {
-    const int iw = ow0 - a.PL + q.xhp[i];
+    const int iw = ow0 * a.S - a.PL + q.xhp[i];
     const bool ok = rowok && (unsigned)iw < (unsigned)a.W;      // xhp < 0: past this thread's quads
     xr[i] = bload(rx, ok ? 4 * (xrow + iw * a.xcs + q.xc[i]) : OOB);
   }
-  const int drow = ((n * a.H + oh) * a.W) * a.ycs + a.yco;
+  const int drow = ((n * a.OH + oh) * a.OW) * a.ycs + a.yco;
 #pragma unroll
   for (int i = 0; i < DQN; ++i) {
-    const bool ok = tv && q.dp[i] >= 0 && ow0 + q.dp[i] < a.W;
+    const bool ok = tv && q.dp[i] >= 0 && ow0 + q.dp[i] < a.OW;
     dr[i] = bload(rd, ok ? 4 * (drow + (ow0 + q.dp[i]) * a.ycs + q.dc[i]) : OOB);
   }
 }
@@ -105,7 +106,7 @@ __global__ void __launch_bounds__(256) hwg_kernel(const HwgArgs a) {
   for (int m = 0; m < NI; ++m) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
   f4 xr[XQ], dr[DQ];
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (long)a.N * a.H * a.W * a.xcs);
-  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (long)a.N * a.H * a.W * a.ycs);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (long)a.N * a.OH * a.OW * a.ycs);
   Quads q;
   {
     const int nx = (TP + a.KW - 1) * cq;
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(256) hwg_kernel(const HwgArgs a) {
 // A wave owns NA (kw, channel fragment) items and computes each against all NF column fragments.
 struct HwhArgs {
   int N, H, W, C, K, KH, KW, PT, PL, wcin;
+  int OH, OW;
   int CF, NF, XS, DS, nA, ntw, chunks;
   int ntiles;
   const float* x; int xcs, xco;
@@ -221,30 +223,38 @@ __device__ __forceinline__ h8 tr_frag(const u16* plane, int S, int row0, int col
 
 constexpr int XQ16 = 12, DQ16 = 4;   // most prefetch quads per thread (input row, dy segment)
 
-// XQN input-row quads per thread (4, 8 or 12: as few registers as the row needs), DQN = 2 NF dy quads
-template <int NA, int NF, int XQN>
+// XQN input-row quads per thread (4, 8 or 12: as few registers as the row needs), DQN = 2 NF dy quads.
+// S = stride (1 or 2).  At stride 2 a segment's input row (2 TP + KW - 1 pixels from 2 ow0 - PL) is staged as two
+// parity planes of R = TP + (KW - 1) / 2 rows -- plane q row r = pixel 2 r + q -- so tap kw of output pixel p reads
+// plane kw & 1 at row p + kw / 2: still a plain row offset for the transposing reads, and each input pixel is
+// staged once (round 6: cnv1, whose 3 / 6 input channels left the implicit GEMM's filter gradient at ~23 TF/s).
+template <int NA, int NF, int XQN, int S>
 __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
   constexpr int DQN = 2 * NF;
   extern __shared__ __attribute__((aligned(16))) u16 lds16[];
-  const int XP = (TP + a.KW - 1) * a.XS, DP = TP * a.DS;
+  const int R = TP + (a.KW - 1) / S;              // rows per parity plane
+  const int XP = S * R * a.XS, DP = TP * a.DS;
   u16* const xh = lds16;
   u16* const xl = xh + XP;
   u16* const dh = xl + XP;
   u16* const dl = dh + DP;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const int kh = blockIdx.y;
+  // (chunk, kernel row) of this block.  (An XCD-grouped order -- the KH blocks of one chunk, which read the same dy
+  // segments, on one XCD -- measured neutral on every layer: profiles/r06/hwh_s2_micro.txt.)
+  const int chunk = blockIdx.x, kh = blockIdx.y;
   // only the real channel quads are staged: the pad channels / columns of the last fragment hold whatever the
   // LDS holds, which reaches only dW rows c >= C and columns n >= K (dropped)
   const int cq = a.C / 4, nq = a.K / 4;
   const float sx = f16x3_scale(a.xmax, 1.f), sd = f16x3_scale(a.dmax, 1.f);
-  int akw[NA], acol[NA];
+  int akw[NA], acol[NA], aoff[NA];
 #pragma unroll
   for (int m = 0; m < NA; ++m) {
     const int ia = wv + 4 * m;
     const int ic = ia < a.nA ? ia : 0;   // dummy items read item 0 (every lane takes part: EXEC all ones)
     akw[m] = ic / a.CF;
     acol[m] = (ic - akw[m] * a.CF) * 16;
+    aoff[m] = ((akw[m] % S) * R + akw[m] / S) * a.XS;   // parity plane + row offset of tap kw
   }
   f4 acc[NA][NF];
 #pragma unroll
@@ -253,14 +263,15 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
     for (int f = 0; f < NF; ++f) acc[m][f] = f4{0.f, 0.f, 0.f, 0.f};
   f4 xr[XQN], dr[DQN];
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x, (long)a.N * a.H * a.W * a.xcs);
-  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (long)a.N * a.H * a.W * a.ycs);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dy, (long)a.N * a.OH * a.OW * a.ycs);
   // the fp32 kernel's prefetch (same quads; HwgArgs view of the geometry)
   HwgArgs ga{};
   ga.N = a.N; ga.H = a.H; ga.W = a.W; ga.C = a.C; ga.K = a.K; ga.KW = a.KW; ga.PT = a.PT; ga.PL = a.PL;
+  ga.OH = a.OH; ga.OW = a.OW; ga.S = S;
   ga.ntw = a.ntw; ga.ntiles = a.ntiles; ga.xcs = a.xcs; ga.xco = a.xco; ga.ycs = a.ycs; ga.yco = a.yco;
+  const int nx = S * R * cq;                      // input-row quads of a segment
   QuadsT<XQN, DQN> q;
   {
-    const int nx = (TP + a.KW - 1) * cq;
 #pragma unroll
     for (int i = 0; i < XQN; ++i) {
       const int e = threadIdx.x + 256 * i;
@@ -278,26 +289,27 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
       q.dc[i] = c;
     }
   }
-  int t = blockIdx.x;
+  int t = chunk;
   prefetch(ga, q, rx, rd, kh, t, xr, dr);
   for (; t < a.ntiles; t += a.chunks) {
     int n, oh, ow0;
     tile_coords(ga, t, n, oh, ow0);
-    const bool live = (unsigned)(oh + kh - a.PT) < (unsigned)a.H;   // uniform over the block
+    const bool live = (unsigned)(oh * S + kh - a.PT) < (unsigned)a.H;   // uniform over the block
     __syncthreads();                                   // the previous segment's reads are done
 #pragma unroll
     for (int i = 0; i < XQN; ++i) {
       const int e = threadIdx.x + 256 * i;
-      if (e < (TP + a.KW - 1) * cq) {
+      if (e < nx) {
         const int hp = e / cq, c = 4 * (e - hp * cq);
+        const int row = (hp % S) * R + hp / S;         // parity plane hp % S, row hp / S
         f4 v = xr[i];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (c + j >= a.wcin) v[j] = 0.f;
         h4 hi, lo;
         split4x2h(v, sx, hi, lo);
-        *reinterpret_cast<h4*>(xh + hp * a.XS + c) = hi;
-        *reinterpret_cast<h4*>(xl + hp * a.XS + c) = lo;
+        *reinterpret_cast<h4*>(xh + row * a.XS + c) = hi;
+        *reinterpret_cast<h4*>(xl + row * a.XS + c) = lo;
       }
     }
 #pragma unroll
@@ -324,8 +336,8 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
       }
 #pragma unroll
       for (int m = 0; m < NA; ++m) {
-        const h8 ah = tr_frag(xh, a.XS, s0 + akw[m], acol[m], g, li);
-        const h8 al = tr_frag(xl, a.XS, s0 + akw[m], acol[m], g, li);
+        const h8 ah = tr_frag(xh + aoff[m], a.XS, s0, acol[m], g, li);
+        const h8 al = tr_frag(xl + aoff[m], a.XS, s0, acol[m], g, li);
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
           acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[f], acc[m][f], 0, 0, 0);
@@ -337,7 +349,7 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
   }
   // lane (li, g) holds dW[kw][c = cf*16 + 4g + r][n = nf*16 + li] (scaled); partial [chunk][kh][kw][wcin][K]
   const float inv = 1.f / (sx * sd);   // power of two: exact
-  float* out = a.part + ((long)blockIdx.x * a.KH + kh) * a.KW * a.wcin * a.K;
+  float* out = a.part + ((long)chunk * a.KH + kh) * a.KW * a.wcin * a.K;
 #pragma unroll
   for (int m = 0; m < NA; ++m) {
     const int ia = wv + 4 * m;
@@ -397,6 +409,12 @@ constexpr long g_hwg_diag = 0;
 const long g_hwg_min_items = env_hwg("TDE_HWG_MIN_ITEMS", 25);
 const long g_hwh = env_hwg("TDE_HWH", 1);                 // 0: fp32 halo WGRAD also in math 4 (A/B)
 const long g_hwh_min_items = env_hwg("TDE_HWH_MIN_ITEMS", 1);
+// stride-2 layers on the fp16x3 kernel for input views of TDE_HWH_S2_MINC..TDE_HWH_S2_MAXC channels (MAXC 0: none).
+// Measured per layer at config 4's twin batch (scripts/conv_micro.py, profiles/r06/hwh_s2_micro.txt), against the
+// implicit GEMM / pixel-shuffle filter gradient: cnv1 over 8 channels 114.7 -> 93-95 us, exp_upcnv1 (16) 139-143 ->
+// 111 us, upcnv1 (16) 57-59 -> 54 us; cnv1 over 4 channels 70 -> 89-94 us (loses: a 16-row fragment holds 4).
+const long g_hwh_s2_minc = env_hwg("TDE_HWH_S2_MINC", 8);
+const long g_hwh_s2_maxc = env_hwg("TDE_HWH_S2_MAXC", 16);
 
 int odd16(int c) {   // smallest odd multiple of 16 >= c
   int f = (c + 15) / 16;
@@ -408,32 +426,39 @@ int odd16(int c) {   // smallest odd multiple of 16 >= c
 
 bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp, int math) {
   hp = HwgPlan{};
-  if (!g_hwg || d.stride != 1 || d.OH != d.H || d.OW != d.W) return false;
+  if (!g_hwg) return false;
+  const bool s1 = d.stride == 1 && d.OH == d.H && d.OW == d.W;
   if (math == 4 && g_hwh) {
-    // fp16x3 kernel: (kw, channel fragment) items per wave x all column fragments
-    if ((long)d.N * d.H * d.W < g_hwg_min_m) return false;
+    // fp16x3 kernel: (kw, channel fragment) items per wave x all column fragments; stride 1, or stride 2 (parity
+    // planes) for input views of TDE_HWH_S2_MINC..MAXC channels
+    const bool s2 = d.stride == 2 && d.C >= g_hwh_s2_minc && d.C <= g_hwh_s2_maxc;
+    if (!s1 && !s2) return false;
+    const int S = d.stride;
+    if ((long)d.N * d.OH * d.OW < g_hwg_min_m) return false;
     if (d.K > 32 || d.K % 4 || d.C % 4 || d.C > 128 || d.KW > 7 || d.KH > 7) return false;
     if (d.x_cstride % 4 || d.x_coff % 4 || d.y_cstride % 4 || d.y_coff % 4) return false;
     const int CF = (d.C + 15) / 16, NF = (d.K + 15) / 16;
     const int nA = d.KW * CF;
     if (nA > 4 * 8 || nA * NF < g_hwh_min_items) return false;
-    if ((TP + d.KW - 1) * (d.C / 4) > 256 * XQ16 || TP * (d.K / 4) > 256 * 2 * NF) return false;
-    hp.ok = 1; hp.f16 = 1;
+    const int R = TP + (d.KW - 1) / S;   // rows per parity plane
+    if (S * R * (d.C / 4) > 256 * XQ16 || TP * (d.K / 4) > 256 * 2 * NF) return false;
+    hp.ok = 1; hp.f16 = 1; hp.S = S;
     hp.CF = CF; hp.NF = NF; hp.nitems = nA;
     hp.CPS = odd16(CF * 16);   // fp16 elements per LDS row
     hp.KPS = odd16(NF * 16);
-    hp.ntw = (d.W + TP - 1) / TP;
-    hp.ntiles = (long)d.N * d.H * hp.ntw;
+    hp.ntw = (d.OW + TP - 1) / TP;
+    hp.ntiles = (long)d.N * d.OH * hp.ntw;
     long chunks = (g_hwg_blocks + d.KH - 1) / d.KH;
     const long maxc = (hp.ntiles + 3) / 4;
     if (chunks > maxc) chunks = maxc;
     if (chunks < 1) chunks = 1;
     hp.chunks = (int)chunks;
-    // two fp16 planes each of the input row and the dy segment
-    hp.lds_bytes = (size_t)(2 * (TP + d.KW - 1) * hp.CPS + 2 * TP * hp.KPS) * sizeof(u16);
+    // two fp16 planes each of the input row (S parity planes of R rows) and the dy segment
+    hp.lds_bytes = (size_t)(2 * S * R * hp.CPS + 2 * TP * hp.KPS) * sizeof(u16);
     hp.part_bytes = ((size_t)chunks * d.KH * d.KW * d.w_cin * d.K * sizeof(float) + 255) / 256 * 256;
     return true;
   }
+  if (!s1) return false;
   if ((long)d.N * d.H * d.W < g_hwg_min_m) return false;
   if (d.K > 32 || d.K % 4 || d.C % 4 || d.C > 128 || d.KW > 7 || d.KH > 7) return false;
   if (d.x_cstride % 4 || d.x_coff % 4 || d.y_cstride % 4 || d.y_coff % 4) return false;
@@ -445,7 +470,7 @@ bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp, int math) {
   // 79 us) -- >= 25 items (7 per wave) unless TDE_HWG_MIN_ITEMS says otherwise
   if (nitems > 4 * MAXI || nitems < g_hwg_min_items) return false;
   if ((TP + d.KW - 1) * CF * 4 > 256 * XQ || TP * NF * 4 > 256 * DQ) return false;
-  hp.ok = 1;
+  hp.ok = 1; hp.S = 1;
   hp.CF = CF; hp.NF = NF; hp.nitems = nitems;
   hp.CPS = odd16(CF * 16);
   hp.KPS = odd16(NF * 16);
@@ -461,17 +486,22 @@ bool hwg_plan(const tde_conv_desc_t& d, HwgPlan& hp, int math) {
   return true;
 }
 
-template <int NA, int XQN>
+template <int NA, int XQN, int S>
 void launch_hwh_x(const HwgPlan& hp, const HwhArgs& a, dim3 grid, hipStream_t st) {
-  if (hp.NF == 1) hipLaunchKernelGGL((hwh_kernel<NA, 1, XQN>), grid, dim3(256), hp.lds_bytes, st, a);
-  else hipLaunchKernelGGL((hwh_kernel<NA, 2, XQN>), grid, dim3(256), hp.lds_bytes, st, a);
+  if (hp.NF == 1) hipLaunchKernelGGL((hwh_kernel<NA, 1, XQN, S>), grid, dim3(256), hp.lds_bytes, st, a);
+  else hipLaunchKernelGGL((hwh_kernel<NA, 2, XQN, S>), grid, dim3(256), hp.lds_bytes, st, a);
+}
+template <int NA, int S>
+void launch_hwh_s(const HwgPlan& hp, const HwhArgs& a, dim3 grid, hipStream_t st) {
+  const int need = (S * (TP + (a.KW - 1) / S) * (a.C / 4) + 255) / 256;
+  if (need <= 4) launch_hwh_x<NA, 4, S>(hp, a, grid, st);
+  else if (need <= 8) launch_hwh_x<NA, 8, S>(hp, a, grid, st);
+  else launch_hwh_x<NA, 12, S>(hp, a, grid, st);
 }
 template <int NA>
 void launch_hwh(const HwgPlan& hp, const HwhArgs& a, dim3 grid, hipStream_t st) {
-  const int need = ((TP + a.KW - 1) * (a.C / 4) + 255) / 256;
-  if (need <= 4) launch_hwh_x<NA, 4>(hp, a, grid, st);
-  else if (need <= 8) launch_hwh_x<NA, 8>(hp, a, grid, st);
-  else launch_hwh_x<NA, 12>(hp, a, grid, st);
+  if (hp.S == 2) launch_hwh_s<NA, 2>(hp, a, grid, st);
+  else launch_hwh_s<NA, 1>(hp, a, grid, st);
 }
 
 void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, const float* dy, float* dw,
@@ -480,6 +510,7 @@ void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, con
     HwhArgs a{};
     a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.K = d.K; a.KH = d.KH; a.KW = d.KW;
     a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
+    a.OH = d.OH; a.OW = d.OW;
     a.CF = hp.CF; a.NF = hp.NF; a.XS = hp.CPS; a.DS = hp.KPS; a.nA = hp.nitems; a.ntw = hp.ntw;
     a.chunks = hp.chunks; a.ntiles = (int)hp.ntiles;
     a.x = x; a.xcs = d.x_cstride; a.xco = d.x_coff;
@@ -505,6 +536,7 @@ void hwg_launch(const HwgPlan& hp, const tde_conv_desc_t& d, const float* x, con
   HwgArgs a{};
   a.N = d.N; a.H = d.H; a.W = d.W; a.C = d.C; a.K = d.K; a.KH = d.KH; a.KW = d.KW;
   a.PT = d.pad_top; a.PL = d.pad_left; a.wcin = d.w_cin;
+  a.OH = d.H; a.OW = d.W; a.S = 1;
   a.CF = hp.CF; a.NF = hp.NF; a.CPS = hp.CPS; a.KPS = hp.KPS; a.nitems = hp.nitems; a.ntw = hp.ntw;
   a.chunks = hp.chunks; a.ntiles = (int)hp.ntiles;
   a.x = x; a.xcs = d.x_cstride; a.xco = d.x_coff;
