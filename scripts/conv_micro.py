@@ -53,6 +53,8 @@ SHAPES = [
     ("expup1_b16", 16, 192, 256, 16, 32, 7, 2),
     # stride-1 64-output-channel layers at the twin batch (halo-tiled filter gradient candidates)
     ("cnv2b_b16", 16, 48, 64, 64, 64, 5, 1),
+    ("cnv1b_b16", 16, 96, 128, 32, 32, 7, 1),
+    ("icnv1_b16", 16, 192, 256, 20, 16, 3, 1),
     ("icnv3_b16", 16, 48, 64, 132, 64, 3, 1),
     ("icnv2_b16", 16, 96, 128, 68, 32, 3, 1),
     ("cnv3b_b16", 16, 24, 32, 128, 128, 3, 1),

@@ -221,6 +221,14 @@ __device__ __forceinline__ h8 tr_frag(const u16* plane, int S, int row0, int col
   return h8{l4[0], l4[1], l4[2], l4[3], h4v[0], h4v[1], h4v[2], h4v[3]};
 }
 
+// the same fragment from a per-lane pointer p = plane + (row0 + 4g + qq) S + col0 + 4p; `up` = 16 rows
+__device__ __forceinline__ h8 tr_frag2(const u16* p, int up) {
+  const hp4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hp4_t)(p));
+  const hp4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hp4_t)(p + up));
+  const h4 l4 = __builtin_bit_cast(h4, lo), h4v = __builtin_bit_cast(h4, hi);
+  return h8{l4[0], l4[1], l4[2], l4[3], h4v[0], h4v[1], h4v[2], h4v[3]};
+}
+
 constexpr int XQ16 = 12, DQ16 = 4;   // most prefetch quads per thread (input row, dy segment)
 
 // XQN input-row quads per thread (4, 8 or 12: as few registers as the row needs), DQN = 2 NF dy quads.
@@ -296,27 +304,25 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
     tile_coords(ga, t, n, oh, ow0);
     const bool live = (unsigned)(oh * S + kh - a.PT) < (unsigned)a.H;   // uniform over the block
     __syncthreads();                                   // the previous segment's reads are done
+    // the quads' (pixel, channel) coordinates come from the prefetch table (no per-segment divisions: round 6,
+    // the integer divisions by C / 4 and K / 4 were ~40 % of the kernel's VALU instructions)
 #pragma unroll
     for (int i = 0; i < XQN; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      if (e < nx) {
-        const int hp = e / cq, c = 4 * (e - hp * cq);
+      if (q.xhp[i] >= 0) {
+        const int hp = q.xhp[i], c = q.xc[i];
         const int row = (hp % S) * R + hp / S;         // parity plane hp % S, row hp / S
-        f4 v = xr[i];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (c + j >= a.wcin) v[j] = 0.f;
+        // no pad-channel mask: channel c of the view only ever meets MFMA A row c, i.e. dW row c, and rows
+        // c >= w_cin are dropped at the store (round 6: the per-quad masks cost ~60 VALU per segment)
         h4 hi, lo;
-        split4x2h(v, sx, hi, lo);
+        split4x2h(xr[i], sx, hi, lo);
         *reinterpret_cast<h4*>(xh + row * a.XS + c) = hi;
         *reinterpret_cast<h4*>(xl + row * a.XS + c) = lo;
       }
     }
 #pragma unroll
     for (int i = 0; i < DQN; ++i) {
-      const int e = threadIdx.x + 256 * i;
-      if (e < TP * nq) {
-        const int p = e / nq, c = 4 * (e - p * nq);
+      if (q.dp[i] >= 0) {
+        const int p = q.dp[i], c = q.dc[i];
         h4 hi, lo;
         split4x2h(dr[i], sd, hi, lo);
         *reinterpret_cast<h4*>(dh + p * a.DS + c) = hi;
@@ -326,18 +332,22 @@ __global__ void __launch_bounds__(256) hwh_kernel(const HwhArgs a) {
     __syncthreads();
     prefetch(ga, q, rx, rd, kh, t + a.chunks, xr, dr);   // next segment's loads in flight under the MFMAs
     if (!live) continue;
+    // per-lane read pointers advanced by one 32-pixel step per iteration; the lo planes and the upper 16 pixels are
+    // immediate offsets (round 6: recomputing each fragment's address cost 60 VALU per 24 MFMAs)
+    const u16* pb = dh + (4 * g + (li >> 2)) * a.DS + 4 * (li & 3);
+    const u16* pa = xh + (4 * g + (li >> 2)) * a.XS + 4 * (li & 3);
 #pragma unroll 1
-    for (int s0 = 0; s0 < TP; s0 += 32) {
+    for (int s0 = 0; s0 < TP; s0 += 32, pb += 32 * a.DS, pa += 32 * a.XS) {
       h8 bh[NF], bl[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        bh[f] = tr_frag(dh, a.DS, s0, 16 * f, g, li);
-        bl[f] = tr_frag(dl, a.DS, s0, 16 * f, g, li);
+        bh[f] = tr_frag2(pb + 16 * f, 16 * a.DS);
+        bl[f] = tr_frag2(pb + DP + 16 * f, 16 * a.DS);
       }
 #pragma unroll
       for (int m = 0; m < NA; ++m) {
-        const h8 ah = tr_frag(xh + aoff[m], a.XS, s0, acol[m], g, li);
-        const h8 al = tr_frag(xl + aoff[m], a.XS, s0, acol[m], g, li);
+        const h8 ah = tr_frag2(pa + aoff[m] + acol[m], 16 * a.XS);
+        const h8 al = tr_frag2(pa + XP + aoff[m] + acol[m], 16 * a.XS);
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
           acc[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[f], acc[m][f], 0, 0, 0);
