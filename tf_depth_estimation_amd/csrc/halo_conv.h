@@ -11,6 +11,7 @@ struct HaloPlan {
   int NW, TN;             // waves per block (pixel rows 2*NW), 16-column MFMA fragments per wave
   int HWd, HP;            // halo width (16 + KW - 1), halo pixels
   int CC, nch, SA;        // channels per chunk (multiple of 8), chunks, LDS row stride (u16)
+  int swz;                // 0: padded rows; 4 / 8: rows of 4 / 8 XOR-swizzled 16-byte chunks (fp16x3)
   int steps, ntap;        // 32-deep k-steps per chunk, KH*KW
   int KH, KW, PT, PL;     // geometry of the conv as executed (DGRAD: flipped taps and pads)
   int Cv, ics, ico;       // input view: channels read, cstride, coff

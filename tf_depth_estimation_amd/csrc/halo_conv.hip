@@ -41,6 +41,7 @@ struct HaloArgs {
   int HWd, HP, CC, nch, SA, steps, ntap, KW, PT, PL;
   int Cv, ics, ico, Ncols, ocs, oco, ncolt, NcolsP;
   int accumulate;
+  int swz;             // halo row layout: 0 padded rows (SA from lds_stride); 4 / 8 = 16-byte chunks per row, XOR-swizzled
   FDiv fCC, fKW, fC4, fHWd;
   const float* in;
   float* out;
@@ -126,6 +127,16 @@ __global__ void __launch_bounds__(256) halo_wprep_batch_kernel(const WprepBatch 
     wprep_elem(J, ws, idx);
 }
 
+// 16-byte chunk `chunk` of halo row `row` (u16 offset within the row).  Padded layout (swz 0): rows of SA u16 whose
+// 16-byte count is 2 mod 4.  Swizzled layouts (round 6, fp16x3): rows of exactly 4 / 8 chunks (SA 32 / 64), chunk ^
+// (row >> 1) & 3 or chunk ^ row & 7 -- conflict-free for the fragment reads of every tap shift (bank model over
+// gfx950's ds_read_b128 lane groups), with 1/3 (32 channels) / 1/5 (64) less LDS per halo row than
+// the padding, so e.g. cnv1b's 7x7 blocks fit two per CU.
+__device__ __forceinline__ int halo_chunk_off(int swz, int row, int chunk) {
+  const int x = swz == 8 ? (row & 7) : (swz == 4 ? ((row >> 1) & 3) : 0);
+  return 8 * (chunk ^ x);
+}
+
 // Workgroup barrier that waits only for this wave's LDS operations.  __syncthreads() is a release/acquire
 // fence + s_barrier, and the fence makes the compiler drain every outstanding global load (vmcnt(0))
 // first, which would retire the weight-tile DMAs still in flight.  The "memory" clobber keeps the
@@ -194,7 +205,7 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
         const int idx = base + u * NT + tid;
         if (idx < total) {
           const int hp = fdiv(idx, p.fC4), c4 = idx - hp * nc4;
-          u16* d = As + hp * p.SA + 4 * c4;
+          u16* d = As + hp * p.SA + halo_chunk_off(p.swz, hp, c4 >> 1) + 4 * (c4 & 1);
           if constexpr (MATH == 4) {
             h4 hi, lo;
             split4x2h(v[u], sIn, hi, lo);
@@ -218,8 +229,8 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // LDS offset (u16) of this lane's A fragment rows at tap (0, 0): pixel rows 2*wv + a, column r16
-  const int arow0 = ((2 * wv) * p.HWd + r16) * p.SA, arow1 = arow0 + p.HWd * p.SA;
+  // halo row of this lane's A fragment rows at tap (0, 0): pixel rows 2*wv + a, column r16
+  const int hrow0 = (2 * wv) * p.HWd + r16, hrow1 = hrow0 + p.HWd;
 
   // one k-step s from ring slot `slot`
   auto compute = [&](int s, int slot) __attribute__((always_inline)) {
@@ -228,12 +239,13 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
     int tap = fdiv(r0, p.fCC), cc = r0 - tap * p.CC;
     if (tap >= p.ntap) { tap = 0; cc = 0; }
     const int kh = fdiv(tap, p.fKW), kw = tap - kh * p.KW;
-    const int toff = (kh * p.HWd + kw) * p.SA + cc;
+    const int trow = kh * p.HWd + kw;
     if constexpr (MATH == 4) {
       h8 ah[2], al[2], bh[TN], bl[TN];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        const u16* src = As + (a ? arow1 : arow0) + toff;
+        const int row = (a ? hrow1 : hrow0) + trow;
+        const u16* src = As + row * p.SA + halo_chunk_off(p.swz, row, cc >> 3);
         ah[a] = *reinterpret_cast<const h8*>(src);
         al[a] = *reinterpret_cast<const h8*>(src + PLANE);
       }
@@ -256,7 +268,7 @@ __global__ void __launch_bounds__(64 * NW) halo_conv_kernel(const HaloArgs p) {
     bf8 ah[2], am[2], al[2], bh[TN], bm[TN], bl[TN];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      const u16* src = As + (a ? arow1 : arow0) + toff;
+      const u16* src = As + ((a ? hrow1 : hrow0) + trow) * p.SA + cc;   // (padded rows only: swz 0 in bf16x6)
       ah[a] = *reinterpret_cast<const bf8*>(src);
       am[a] = *reinterpret_cast<const bf8*>(src + PLANE);
       al[a] = *reinterpret_cast<const bf8*>(src + 2 * PLANE);
@@ -408,6 +420,7 @@ const long g_halo_min_m = tde_env_pos("TDE_HALO_MIN_M", 8192);  // output pixels
 const long g_halo_nw = env_l("TDE_HALO_NW", 0);           // force 4 or 8 waves per block
 const long g_halo_lds = tde_env_pos("TDE_HALO_LDS_KB", 150) << 10;
 const long g_halo_minch = tde_env_pos("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
+const long g_halo_swz = env_l("TDE_HALO_SWZ", 1);         // 0: padded halo rows only (A/B)
 
 int lds_stride(int cc) {   // smallest row stride (u16) >= cc whose 16-byte count is 2 mod 4
   int s = cc;
@@ -478,7 +491,11 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
     for (int nch = (int)g_halo_minch; nch <= cp8 / 8 && tried < 3; ++nch) {
       const int cc = ((cp8 + nch - 1) / nch + 7) / 8 * 8;
       if (nch > 1 && (cp8 + cc - 1) / cc < nch) continue;   // same chunking as a smaller nch
-      const int sa = lds_stride(cc);
+      int sa = lds_stride(cc), swz = 0;
+      if (g_halo_swz && hp.planes == 2) {   // fp16x3: swizzled rows of 4 / 8 chunks where they beat the padding
+        if (cc > 16 && cc <= 32 && sa > 32) { sa = 32; swz = 4; }
+        else if (cc > 32 && cc <= 64 && sa > 64) { sa = 64; swz = 8; }
+      }
       const size_t lds = (size_t)hp.planes * hh * hp.HWd * sa * 2 + ring;
       if (lds > (size_t)g_halo_lds) continue;
       ++tried;
@@ -495,7 +512,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
                          2.0 * nchr;   // + halo staging per chunk
       if (best_est < 0 || est < best_est - 1e-9) {
         best_est = est;
-        hp.NW = nw; hp.CC = cc; hp.nch = nchr; hp.SA = sa; hp.HP = hh * hp.HWd;
+        hp.NW = nw; hp.CC = cc; hp.nch = nchr; hp.SA = sa; hp.swz = swz; hp.HP = hh * hp.HWd;
         hp.lds_bytes = lds; hp.ok = 1;
       }
     }
@@ -550,7 +567,7 @@ void halo_launch(const HaloPlan& hp, const tde_conv_desc_t& d, const float* in, 
   a.HWd = hp.HWd; a.HP = hp.HP; a.CC = hp.CC; a.nch = hp.nch; a.SA = hp.SA; a.steps = hp.steps; a.ntap = hp.ntap;
   a.KW = hp.KW; a.PT = hp.PT; a.PL = hp.PL;
   a.Cv = hp.Cv; a.ics = hp.ics; a.ico = hp.ico; a.Ncols = hp.Ncols; a.ocs = hp.ocs; a.oco = hp.oco;
-  a.ncolt = hp.ncolt; a.NcolsP = hp.NcolsP; a.accumulate = accumulate;
+  a.ncolt = hp.ncolt; a.NcolsP = hp.NcolsP; a.accumulate = accumulate; a.swz = hp.swz;
   a.fCC = make_fdiv(hp.CC); a.fKW = make_fdiv(hp.KW); a.fC4 = make_fdiv(hp.CC / 4); a.fHWd = make_fdiv(hp.HWd);
   a.in = in; a.out = out; a.wp = wp; a.bnp = bnp; a.bias = bias; a.relu = relu;
   a.inmax = hp.mode == 0 ? d.x_absmax : d.y_absmax;
