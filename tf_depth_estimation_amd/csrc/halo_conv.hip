@@ -21,6 +21,7 @@
 // implicit GEMM's epilogue partials.
 #include "halo_conv.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -418,6 +419,8 @@ long env_l(const char* name, long dflt) {
 const long g_halo = env_l("TDE_HALO", 1);                 // 0: never take the halo path (A/B)
 const long g_halo_min_m = tde_env_pos("TDE_HALO_MIN_M", 8192);  // output pixels (N*H*W) from which it pays (r04: 16384 -> 8192, +0.5 %)
 const long g_halo_nw = env_l("TDE_HALO_NW", 0);           // force 4 or 8 waves per block
+const long g_halo_tn = env_l("TDE_HALO_TN", 0);           // force 1-4 column fragments per wave (A/B)
+const long g_halo_verbose = env_l("TDE_HALO_VERBOSE", 0); // print every plan to stderr (tuning runs)
 const long g_halo_lds = tde_env_pos("TDE_HALO_LDS_KB", 150) << 10;
 const long g_halo_minch = tde_env_pos("TDE_HALO_MINCH", 1);     // force at least this many channel chunks
 const long g_halo_swz = env_l("TDE_HALO_SWZ", 1);         // 0: padded halo rows only (A/B)
@@ -470,7 +473,7 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
   long best = -1;
   for (int tn = 1; tn <= 4; ++tn) {
     const long nt = tde_cdiv(hp.Ncols, 16 * tn), cost = nt * (16 * tn + 32);
-    if (best < 0 || cost < best) { best = cost; hp.TN = tn; }
+    if (g_halo_tn ? tn == g_halo_tn : (best < 0 || cost < best)) { best = cost; hp.TN = tn; }
   }
   hp.ncolt = tde_cdiv(hp.Ncols, 16 * hp.TN);
   hp.NcolsP = hp.ncolt * 16 * hp.TN;
@@ -518,6 +521,9 @@ bool halo_plan(const tde_conv_desc_t& d, int mode, int math, HaloPlan& hp) {
     }
   }
   if (!hp.ok) return false;
+  if (g_halo_verbose)
+    fprintf(stderr, "[halo] mode %d N %d H %d W %d C %d K %d k %d: NW %d TN %d CC %d nch %d SA %d swz %d lds %zu\n",
+            mode, d.N, d.H, d.W, hp.Cv, hp.Ncols, d.KH, hp.NW, hp.TN, hp.CC, hp.nch, hp.SA, hp.swz, hp.lds_bytes);
   hp.steps = tde_cdiv((long)hp.ntap * hp.CC, 32);
   hp.gx = tde_cdiv(d.W, 16);
   hp.gy = tde_cdiv(d.H, 2 * hp.NW);
