@@ -703,8 +703,15 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #ifndef TDE_PF2_WAVES
 #define TDE_PF2_WAVES 2
 #endif
+// TDE_GEMM_WAVES: waves per SIMD the fp16x3 one-tile-in-flight tiles are allocated for (round 6: 3 -- the 128 x 64 tiles
+// and the fused backward's 64 x 128 tiles drop from 172-184 to 143-151 registers, no spills, 2 -> 3 waves per SIMD,
+// which their 48 KB of LDS already allowed; tiles over 128 x 64 cannot fit 3 and keep the default allocation)
+#ifndef TDE_GEMM_WAVES
+#define TDE_GEMM_WAVES 3
+#endif
 template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PF == 2 ? TDE_PF2_WAVES : 1)))
+__global__ void __launch_bounds__(NT)
+__attribute__((amdgpu_waves_per_eu(PF == 2 ? TDE_PF2_WAVES : (MATH == 4 && BM * BN <= 8192 ? TDE_GEMM_WAVES : 1))))
 igemmx_kernel(const ConvArgs p) {
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
   conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
@@ -715,7 +722,8 @@ igemmx_kernel(const ConvArgs p) {
 // filter gradient (WGRAD).  Both
 // only read dz, so they are independent; at the deep levels neither fills the chip alone.
 template <int MATH, int MODE1, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT) igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MATH == 4 && BM * BN <= 8192 ? TDE_GEMM_WAVES : 1)))
+igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
                                                         int gxw, int gyw, int nd) {
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
   int id = blockIdx.x;
