@@ -1045,6 +1045,7 @@ static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to whi
 // FWD / DGRAD GEMMs with at most this many rows (and < 256 tiles) take 64-row tiles (more blocks); above it, and
 // for every WGRAD, 128 (half the weight re-reads of a weight-streaming deep layer per row tile)
 static const long g_bm64_maxm = env_long("TDE_BM64_MAXM", 4096);
+static const long g_tile_ovh = env_long("TDE_TILE_OVH", 24);   // per-tile overhead of the N-tile rule, in columns
 
 // fix_bm / fix_bn > 0: plan with that tile (the fused backward launch needs one tile for both GEMMs)
 static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fix_bn = 0) {
@@ -1081,7 +1082,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
     long best = -1;
     for (int bn : cands) {
       const long t = tde_cdiv(Nn, bn);
-      const long cost = t * bn + 24 * t;
+      const long cost = t * bn + g_tile_ovh * t;
       if (best < 0 || cost < best || (cost == best && bn > pl.bn)) { best = cost; pl.bn = bn; }
     }
   }
