@@ -1046,6 +1046,8 @@ static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to whi
 // for every WGRAD, 128 (half the weight re-reads of a weight-streaming deep layer per row tile)
 static const long g_bm64_maxm = env_long("TDE_BM64_MAXM", 4096);
 static const long g_tile_ovh = env_long("TDE_TILE_OVH", 24);   // per-tile overhead of the N-tile rule, in columns
+static const long g_maxbn = env_long("TDE_MAXBN", 0);           // cap on the N tile (0: none; A/B of the 3-wave tiles)
+static const long g_maxbn_modes = env_long("TDE_MAXBN_MODES", 7);   // bit m: the cap applies to mode m
 
 // fix_bm / fix_bn > 0: plan with that tile (the fused backward launch needs one tile for both GEMMs)
 static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fix_bn = 0) {
@@ -1081,6 +1083,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
     static const int cands[] = {16, 32, 48, 64, 96, 128};
     long best = -1;
     for (int bn : cands) {
+      if (g_maxbn && ((g_maxbn_modes >> mode) & 1) && bn > g_maxbn) continue;
       const long t = tde_cdiv(Nn, bn);
       const long cost = t * bn + g_tile_ovh * t;
       if (best < 0 || cost < best || (cost == best && bn > pl.bn)) { best = cost; pl.bn = bn; }
