@@ -711,7 +711,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& p, const int bx, const
 #endif
 template <int MATH, int MODE, int BM, int BN, int WM, int WN, int PF>
 __global__ void __launch_bounds__(NT)
-__attribute__((amdgpu_waves_per_eu(PF == 2 ? TDE_PF2_WAVES : (MATH == 4 && BM * BN <= 8192 ? TDE_GEMM_WAVES : 1))))
+__attribute__((amdgpu_waves_per_eu(MATH == 4 ? (BM * BN <= 8192 ? TDE_GEMM_WAVES : 1) : (PF == 2 ? TDE_PF2_WAVES : 1))))
 igemmx_kernel(const ConvArgs p) {
   __shared__ __attribute__((aligned(16))) typename ImgSel<MATH, BM>::T smem[SmemSize<MATH, BM, BN>::N];
   conv_tile<MATH, MODE, BM, BN, WM, WN, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
@@ -1255,6 +1255,10 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
   return b;
 }
 
+// fp16x3 64-row FWD / DGRAD tiles with two tiles in flight (round 6): at the 3-wave register cap (TDE_GEMM_WAVES) they
+// fit in 138-152 registers without spills, so the second tile no longer costs a wave per SIMD (round 3's attempt
+// ran them at 2 waves: neutral, see below).  0: one tile in flight (A/B).
+static const long g_f16_pf2 = env_long("TDE_F16_PF2", 1);
 // prefetch depth (tiles in flight): 1 for 128-row tiles; for the 64-row tiles of the deep layers 2 in the
 // register-split maths, 1 in fp16x3 (depth 2 costs 187 VGPR+AGPR = 2 waves/SIMD, depth 1 136 = 3; measured
 // (scripts/r02zm.sh) icnv5 DGRAD 43.6 -> 36.6 us, config 2 2.82 -> 2.80 ms, config 4 13.30 -> 13.18 ms).
@@ -1285,9 +1289,12 @@ static void launch_cfg(const ConvArgs& a0, dim3 grid, hipStream_t st) {
   constexpr int WN = BN % TDE_WN_DIV == 0 ? 2 : 1;
   constexpr int WM = 4 / WN;
   const int math = tile_math(BN, MODE);
-  const int pf = (BM == 64 && math != 4) ? 2 : 1;
+  const int pf = (BM == 64 && (math != 4 || g_f16_pf2)) ? 2 : 1;
+  constexpr bool F16_PF2 = BM == 64 && MODE != MODE_WGRAD && MODE != MODE_PSW;
   if (math == 1) hipLaunchKernelGGL((igemmx_kernel<1, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 2) hipLaunchKernelGGL((igemmx_kernel<2, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
+  else if (math == 4 && F16_PF2 && pf == 2)
+    hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, F16_PF2 ? 2 : 1>), grid, dim3(NT), 0, st, a);
   else if (math == 4) hipLaunchKernelGGL((igemmx_kernel<4, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
   else if (math == 3 && pf == 2) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 2>), grid, dim3(NT), 0, st, a);
   else if (math == 3) hipLaunchKernelGGL((igemmx_kernel<3, MODE, BM, BN, WM, WN, 1>), grid, dim3(NT), 0, st, a);
