@@ -721,7 +721,7 @@ igemmx_kernel(const ConvArgs p) {
 // data gradient (MODE1: DGRAD of a conv, FWD of a deconv's virtual conv), blocks [nd, nd + nw) the
 // filter gradient (WGRAD).  Both
 // only read dz, so they are independent; at the deep levels neither fills the chip alone.
-template <int MATH, int MODE1, int BM, int BN, int WM, int WN, int PF1 = 1>
+template <int MATH, int MODE1, int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MATH == 4 && BM * BN <= 8192 ? TDE_GEMM_WAVES : 1)))
 igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
                                                         int gxw, int gyw, int nd) {
@@ -730,7 +730,7 @@ igemm_bwd2_kernel(const ConvArgs pd, const ConvArgs pw, int gxd, int gyd,
   if (id < nd) {
     const int bx = id % gxd;
     id /= gxd;
-    conv_tile<MATH, MODE1, BM, BN, WM, WN, PF1>(pd, bx, id % gyd, id / gyd, smem);
+    conv_tile<MATH, MODE1, BM, BN, WM, WN, 1>(pd, bx, id % gyd, id / gyd, smem);
   } else {
     id -= nd;
     const int bx = id % gxw;
@@ -1259,7 +1259,6 @@ static size_t plan_ws_bytes(const tde_conv_desc_t& d, int mode, bool bn) {
 // fit in 138-152 registers without spills, so the second tile no longer costs a wave per SIMD (round 3's attempt
 // ran them at 2 waves: neutral, see below).  0: one tile in flight (A/B).
 static const long g_f16_pf2 = env_long("TDE_F16_PF2", 1);
-static const long g_bwd2_pf2 = env_long("TDE_BWD2_PF2", 0);   // the same inside the fused backward launch
 // prefetch depth (tiles in flight): 1 for 128-row tiles; for the 64-row tiles of the deep layers 2 in the
 // register-split maths, 1 in fp16x3 (depth 2 costs 187 VGPR+AGPR = 2 waves/SIMD, depth 1 136 = 3; measured
 // (scripts/r02zm.sh) icnv5 DGRAD 43.6 -> 36.6 us, config 2 2.82 -> 2.80 ms, config 4 13.30 -> 13.18 ms).
@@ -1720,9 +1719,6 @@ static void launch_bwd2_cfg(const Plan& p1, const ConvArgs& a1, const Plan& p2, 
   else if (math == 3)
     hipLaunchKernelGGL((igemm_bwd2_kernel<3, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
                        p1.gy, p2.gx, p2.gy, nd);
-  else if (math == 4 && BM == 64 && g_bwd2_pf2)   // the data-gradient tiles two in flight (as launch_cfg's)
-    hipLaunchKernelGGL((igemm_bwd2_kernel<4, MODE1, BM, BN, WM, WN, BM == 64 ? 2 : 1>), dim3(nd + nw), dim3(NT), 0,
-                       st, a1, a2, p1.gx, p1.gy, p2.gx, p2.gy, nd);
   else if (math == 4)
     hipLaunchKernelGGL((igemm_bwd2_kernel<4, MODE1, BM, BN, WM, WN>), dim3(nd + nw), dim3(NT), 0, st, a1, a2, p1.gx,
                        p1.gy, p2.gx, p2.gy, nd);
