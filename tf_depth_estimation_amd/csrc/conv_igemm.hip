@@ -1046,8 +1046,6 @@ static const long g_skinny_m = env_long("TDE_SKINNY_M", 32);   // rows up to whi
 // for every WGRAD, 128 (half the weight re-reads of a weight-streaming deep layer per row tile)
 static const long g_bm64_maxm = env_long("TDE_BM64_MAXM", 4096);
 static const long g_tile_ovh = env_long("TDE_TILE_OVH", 24);   // per-tile overhead of the N-tile rule, in columns
-// filter gradients with at most this many rows (taps x channels) on 64-row tiles (0: never; A/B of the 3-wave tiles)
-static const long g_wgrad_bm64_maxm = env_long("TDE_WGRAD_BM64_MAXM", 0);
 static const long g_maxbn = env_long("TDE_MAXBN", 0);           // cap on the N tile (0: none; A/B of the 3-wave tiles)
 static const long g_maxbn_modes = env_long("TDE_MAXBN_MODES", 7);   // bit m: the cap applies to mode m
 
@@ -1099,8 +1097,7 @@ static Plan make_plan(const tde_conv_desc_t& d, int mode, int fix_bm = 0, int fi
   // MFMA-dense 128-row tile; FWD/DGRAD with few tiles trade tile size for more blocks.  (64-row filter-gradient
   // tiles for the low-resolution layers and a column cap on the 64-row tiles were measured no better and removed in
   // round 5.)
-  if ((mode != MODE_WGRAD && tiles < 256 && M <= g_bm64_maxm) || g_force_bm == 64 || fix_bm == 64 ||
-      (mode == MODE_WGRAD && !fix_bm && g_wgrad_bm64_maxm && M <= g_wgrad_bm64_maxm)) {
+  if ((mode != MODE_WGRAD && tiles < 256 && M <= g_bm64_maxm) || g_force_bm == 64 || fix_bm == 64) {
     pl.bm = 64;
     tiles = tde_cdiv(M, pl.bm) * (long)tde_cdiv(Nn, pl.bn) * ncls;
   }
